@@ -1,0 +1,910 @@
+// pm_oracle.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference's small-parsimony path (faithokamoto/panman
+// @ 2025-03-21).  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load this library, and only as the checker / the timed
+// CPU baseline.  The product path (panman_amd/libpanman_amd.so) never links,
+// loads or calls it.
+//
+// Fidelity: every routine restates the reference algorithm with the
+// reference's own data structures where they shape the cost (per-column
+// std::unordered_map<std::string,...> keyed by node name, recursion over
+// Node* children), so that its timing is a faithful stand-in for the
+// reference's CPU path ("cpu_baseline.kind = port").
+//
+// Parity pin: the reference itself is unbuildable in this image without
+// stand-ins for oneTBB / capnp / boost / jsoncpp headers (forbidden by the
+// task rules), so this restatement is pinned against the known-answer tests
+// the survey recorded from the compiled reference (SURVEY.md §8a', committed
+// as tests/golden/kats.json) -- see DESIGN.md "Oracle".
+//
+// Reference anchors (file:line under /root/reference):
+//   codes            src/panman.cpp:41-113 (getNucleotideFromCode / getCodeFromNucleotide)
+//   complement       src/panman.cpp:171-204
+//   Newick           src/panman.cpp:265-308 (stringSplit, stripString), :310-450
+//   Fitch F1-F3      src/fitchSankoff.cpp:30-56, 96-129, 131-171
+//   Sankoff S1-S3    src/fitchSankoff.cpp:359-405, 487-531, 676-703
+//   block B1         src/fitchSankoff.cpp:224-308
+//   block B2         src/fitchSankoff.cpp:707-818
+//   M1 MSA driver    src/panman.cpp:1274-1466
+//   M2 low-mem       src/panman.cpp:1467-1649 (readFastaInBatch :677-724)
+//   E1 grouping      src/panman.cpp:1445-1466, src/panman.hpp:100-151
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <sstream>
+#include <stack>
+#include <queue>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr int kSankoffInf = 100000001;      // src/common.hpp:16
+constexpr int kNoDefault = 1 << 28;         // src/panman.hpp:851 default argument
+
+enum NucType { NS = 0, ND = 1, NI = 2 };    // src/panman.hpp:46-61
+enum BlockType { BD = 0, BI = 1 };          // src/panman.hpp:63-72
+
+// ---------------------------------------------------------------- codes ----
+int code_of(char c) {
+    switch (c) {
+        case 'A': return 1;  case 'C': return 2;  case 'G': return 4;  case 'T': return 8;
+        case 'R': return 5;  case 'Y': return 10; case 'S': return 6;  case 'W': return 9;
+        case 'K': return 12; case 'M': return 3;  case 'B': return 14; case 'D': return 13;
+        case 'H': return 11; case 'V': return 7;  case 'N': return 15;
+        default: return 0;
+    }
+}
+
+char char_of(int code) {
+    static const char tab[16] = {'-', 'A', 'C', 'M', 'G', 'R', 'S', 'V',
+                                 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
+    return (code >= 0 && code < 16) ? tab[code] : '-';
+}
+
+char complement_of(char c) {
+    switch (c) {
+        case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+        case 'R': return 'Y'; case 'Y': return 'R'; case 'S': return 'S'; case 'W': return 'W';
+        case 'K': return 'M'; case 'M': return 'K'; case 'B': return 'V'; case 'D': return 'H';
+        case 'H': return 'D'; case 'V': return 'B';
+        default: return 'N';
+    }
+}
+
+// index of the highest set bit, as the reference's shift loop computes it
+int log2_state(int s) {
+    int code = 0;
+    while (s > 0) { s >>= 1; ++code; }
+    return code - 1;
+}
+
+int lowest_bit(int s) {
+    int cur = 1;
+    while (!(s & cur)) cur <<= 1;
+    return cur;
+}
+
+// ----------------------------------------------------------------- tree ----
+struct ONode {
+    std::string id;
+    ONode* parent = nullptr;
+    std::vector<ONode*> children;
+};
+
+struct OTree {
+    std::vector<ONode*> owned;
+    ONode* root = nullptr;
+    std::map<std::string, ONode*> all;   // name order, like Tree::allNodes
+    size_t internal_counter = 0;
+    ~OTree() { for (auto* n : owned) delete n; }
+    ONode* make(const std::string& id, ONode* par) {
+        ONode* n = new ONode();
+        n->id = id;
+        n->parent = par;
+        if (par) par->children.push_back(n);
+        owned.push_back(n);
+        return n;
+    }
+};
+
+// Quote-aware split that keeps ' ... ' groups whole (src/panman.cpp:265-296).
+void split_keep_quotes(const std::string& s, char delim, std::vector<std::string>& out) {
+    size_t start = 0, end = 0, hold = 0;
+    while ((end = s.find(delim, start)) != std::string::npos) {
+        if (end >= s.size()) break;
+        if (hold == 0) {
+            std::string piece = s.substr(start, end - start);
+            if (std::count(piece.begin(), piece.end(), '\'') % 2 == 1) hold = start;
+            else out.push_back(piece);
+        } else {
+            std::string piece = s.substr(hold, end - hold);
+            if (std::count(piece.begin(), piece.end(), '\'') % 2 == 0) {
+                hold = 0;
+                out.push_back(piece);
+            }
+        }
+        start = end + 1;
+    }
+    std::string tail = s.substr(start);
+    if (!tail.empty()) out.push_back(tail);
+}
+
+std::string strip_spaces(std::string s) {
+    while (!s.empty() && s.back() == ' ') s.pop_back();
+    for (size_t i = 0; i < s.size(); ++i)
+        if (s[i] != ' ') return s.substr(i);
+    return s;
+}
+
+// Newick -> tree, internal nodes named node_<k> in order of '(' (src/panman.cpp:310-450,
+// src/panman.hpp:793-795).  Branch lengths are parsed but irrelevant to this path.
+bool parse_newick(const std::string& text, OTree& t, std::string& err) {
+    std::string nwk = strip_spaces(text);
+    std::vector<std::string> pieces;
+    split_keep_quotes(nwk, ',', pieces);
+    std::vector<std::string> leaves;
+    std::vector<size_t> opens, closes;
+    long level = 0;
+    for (const auto& s : pieces) {
+        size_t no = 0, nc = 0;
+        bool stop = false, in_quote = false, quoted = false;
+        std::string leaf;
+        for (char c : s) {
+            if (in_quote) {
+                leaf += c;
+                if (c == '\'') in_quote = false;
+            } else if (c == '\'') {
+                in_quote = true; quoted = true; leaf += c;
+            } else if (c == ':') {
+                stop = true;
+            } else if (c == '(') {
+                ++no; ++level;
+            } else if (c == ')') {
+                stop = true; ++nc; --level;
+            } else if (!stop) {
+                leaf += c;
+            }
+        }
+        if (quoted && leaf.size() >= 2 && leaf.front() == '\'' && leaf.back() == '\'')
+            leaf = leaf.substr(1, leaf.size() - 2);
+        leaves.push_back(leaf);
+        opens.push_back(no);
+        closes.push_back(nc);
+    }
+    if (level != 0) { err = "incorrect Newick format"; return false; }
+    std::stack<ONode*> stack;
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        for (size_t j = 0; j < opens[i]; ++j) {
+            std::string nid = "node_" + std::to_string(++t.internal_counter);
+            ONode* n = t.make(nid, stack.empty() ? nullptr : stack.top());
+            if (stack.empty()) t.root = n;
+            t.all[nid] = n;
+            stack.push(n);
+        }
+        if (stack.empty()) { err = "leaf outside any clade"; return false; }
+        ONode* lf = t.make(leaves[i], stack.top());
+        t.all[leaves[i]] = lf;
+        for (size_t j = 0; j < closes[i]; ++j) stack.pop();
+    }
+    if (!t.root) { err = "empty tree"; return false; }
+    return true;
+}
+
+// ------------------------------------------------------ nucleotide Fitch ----
+using StateMap = std::unordered_map<std::string, int>;
+using CostMap = std::unordered_map<std::string, std::vector<int>>;
+using NucMutMap = std::unordered_map<std::string, std::pair<int, char>>;
+using BlockMutMap = std::unordered_map<std::string, std::pair<int, bool>>;
+
+// F1: src/fitchSankoff.cpp:30-56
+int fitch_up(ONode* n, StateMap& st, int ref_state) {
+    if (n->children.empty()) {
+        auto it = st.find(n->id);
+        if (it == st.end()) return st[n->id] = 0;    // absent leaf poisons the AND
+        return it->second;
+    }
+    std::vector<int> kids;
+    kids.reserve(n->children.size());
+    for (ONode* c : n->children) kids.push_back(fitch_up(c, st, ref_state));
+    if (n->parent == nullptr && ref_state != -1) return st[n->id] = ref_state;
+    int both = kids[0], either = 0;
+    for (int k : kids) { either |= k; both &= k; }
+    return st[n->id] = both ? both : either;
+}
+
+// F2: src/fitchSankoff.cpp:96-129
+void fitch_down(ONode* n, ONode* root, StateMap& st, int parent_state, int forced) {
+    if (n == root && forced != kNoDefault) {
+        st[n->id] = forced;
+    } else {
+        int own = st[n->id];
+        if (own == 0) return;
+        if (n == root) st[n->id] = lowest_bit(own);
+        else if (parent_state & own) st[n->id] = parent_state;
+        else st[n->id] = lowest_bit(own);
+    }
+    int mine = st[n->id];
+    for (ONode* c : n->children) fitch_down(c, root, st, mine, kNoDefault);
+}
+
+// F3: src/fitchSankoff.cpp:131-171
+void fitch_assign(ONode* n, StateMap& st, NucMutMap& muts, int parent_state) {
+    int own = st[n->id];
+    if (own == 0) return;
+    if (parent_state != own) {
+        if (parent_state == 1) muts[n->id] = {NI, char_of(log2_state(own))};
+        else if (own == 1) muts[n->id] = {ND, '-'};
+        else muts[n->id] = {NS, char_of(log2_state(own))};
+    }
+    for (ONode* c : n->children) fitch_assign(c, st, muts, own);
+}
+
+// ---------------------------------------------------- nucleotide Sankoff ----
+// S1: src/fitchSankoff.cpp:359-405
+std::vector<int> sankoff_up(ONode* n, CostMap& cs) {
+    if (n->children.empty()) {
+        if (cs.find(n->id) == cs.end()) cs[n->id] = std::vector<int>(16, kSankoffInf);
+        return cs[n->id];
+    }
+    std::vector<std::vector<int>> kids;
+    for (ONode* c : n->children) kids.push_back(sankoff_up(c, cs));
+    bool any_finite = false;
+    for (auto& k : kids)
+        for (int v : k)
+            if (v < kSankoffInf) { any_finite = true; break; }
+    if (!any_finite) return cs[n->id] = std::vector<int>(16, kSankoffInf);
+    std::vector<int> cost(16, 0);
+    for (int i = 0; i < 16; ++i) {
+        for (auto& k : kids) {
+            int best = kSankoffInf;
+            for (int j = 0; j < 16; ++j) best = std::min(best, (i != j) + k[j]);
+            if (best < kSankoffInf) cost[i] += best;
+        }
+    }
+    return cs[n->id] = cost;
+}
+
+// S2: src/fitchSankoff.cpp:487-531
+void sankoff_down(ONode* n, ONode* root, CostMap& cs, StateMap& st, int parent_ptr, int forced) {
+    if (n == root && forced != kNoDefault) {
+        st[n->id] = forced;
+    } else if (n == root) {
+        int best = kSankoffInf, arg = -1;
+        const auto& c = cs[n->id];
+        for (int i = 0; i < 16; ++i)
+            if (c[i] < best) { best = c[i]; arg = i; }
+        st[n->id] = arg;      // reference asserts arg != -1 (all-absent column)
+    } else {
+        st[n->id] = parent_ptr;
+    }
+    int mine = st[n->id];
+    for (ONode* c : n->children) {
+        if (mine == -1) { sankoff_down(c, root, cs, st, -1, kNoDefault); continue; }
+        const auto& k = cs[c->id];
+        int best = kSankoffInf, arg = -1;
+        for (int i = 0; i < 16; ++i) {
+            int v = (i != mine) + k[i];
+            if (v < best) { best = v; arg = i; }
+        }
+        sankoff_down(c, root, cs, st, arg, kNoDefault);
+    }
+}
+
+// S3: src/fitchSankoff.cpp:676-703
+void sankoff_assign(ONode* n, StateMap& st, NucMutMap& muts, int parent_state) {
+    int own = st[n->id];
+    if (own == -1) return;
+    if (parent_state != own) {
+        if (parent_state == 0) muts[n->id] = {NI, char_of(own)};
+        else if (own == 0) muts[n->id] = {ND, '-'};
+        else muts[n->id] = {NS, char_of(own)};
+    }
+    for (ONode* c : n->children) sankoff_assign(c, st, muts, own);
+}
+
+// -------------------------------------------------------- block Fitch B1 ----
+int block_fitch_up(ONode* n, StateMap& st) {             // :224-245
+    if (n->children.empty()) {
+        auto it = st.find(n->id);
+        if (it == st.end()) return st[n->id] = 0;
+        return it->second;
+    }
+    std::vector<int> kids;
+    for (ONode* c : n->children) kids.push_back(block_fitch_up(c, st));
+    int both = kids[0], either = 0;
+    for (int k : kids) { either |= k; both &= k; }
+    return st[n->id] = both ? both : either;
+}
+
+void block_fitch_down(ONode* n, ONode* root, StateMap& st, int parent_state, int forced) {  // :247-270
+    if (n == root && forced != kNoDefault) {
+        st[n->id] = forced;
+    } else {
+        int own = st[n->id];
+        if (own == 0) return;
+        st[n->id] = (parent_state & own) ? parent_state : lowest_bit(own);
+    }
+    int mine = st[n->id];
+    for (ONode* c : n->children) block_fitch_down(c, root, st, mine, kNoDefault);
+}
+
+void block_fitch_assign(ONode* n, StateMap& st, BlockMutMap& muts, int parent_state) {  // :272-308
+    int own = st[n->id];
+    if (own == 0) return;
+    if (parent_state != own) {
+        if (parent_state == 1) muts[n->id] = {BI, log2_state(own) == 2};
+        else if (own == 1) muts[n->id] = {BD, false};
+        else muts[n->id] = {BD, true};
+    }
+    for (ONode* c : n->children) block_fitch_assign(c, st, muts, own);
+}
+
+// ------------------------------------------------------ block Sankoff B2 ----
+std::vector<int> block_sankoff_up(ONode* n, CostMap& cs) {   // :707-735
+    if (n->children.empty()) {
+        if (cs.find(n->id) == cs.end()) cs[n->id] = {0, kSankoffInf, kSankoffInf};
+        return cs[n->id];
+    }
+    std::vector<std::vector<int>> kids;
+    for (ONode* c : n->children) kids.push_back(block_sankoff_up(c, cs));
+    std::vector<int> cost(3, 0);
+    for (int i = 0; i < 3; ++i)
+        for (auto& k : kids) {
+            int best = kSankoffInf;
+            for (int j = 0; j < 3; ++j) best = std::min(best, (i != j) + k[j]);
+            cost[i] += best;
+        }
+    return cs[n->id] = cost;
+}
+
+void block_sankoff_down(ONode* n, ONode* root, CostMap& cs, StateMap& st, int parent_ptr, int forced) {  // :737-786
+    if (n == root && forced != kNoDefault) {
+        st[n->id] = forced;
+    } else if (n == root) {
+        int best = kSankoffInf, arg = -1;
+        const auto& c = cs[n->id];
+        for (int i = 0; i < 3; ++i)
+            if (c[i] < best) { best = c[i]; arg = i; }
+        if (arg == -1) { st[n->id] = -1; return; }
+        st[n->id] = arg;
+    } else {
+        bool finite = false;
+        for (int v : cs[n->id]) if (v < kSankoffInf) finite = true;
+        if (!finite) { st[n->id] = -1; return; }
+        st[n->id] = parent_ptr;
+    }
+    int mine = st[n->id];
+    for (ONode* c : n->children) {
+        const auto& k = cs[c->id];
+        int best = kSankoffInf, arg = -1;
+        for (int i = 0; i < 3; ++i) {
+            int v = (i != mine) + k[i];
+            if (v < best) { best = v; arg = i; }
+        }
+        block_sankoff_down(c, root, cs, st, arg, kNoDefault);
+    }
+}
+
+void block_sankoff_assign(ONode* n, StateMap& st, BlockMutMap& muts, int parent_state) {  // :788-818
+    int own = st[n->id];
+    if (own == -1) return;
+    if (parent_state != own) {
+        if (parent_state == 0) muts[n->id] = {BI, own == 2};
+        else if (own == 0) muts[n->id] = {BD, false};
+        else muts[n->id] = {BD, true};
+    }
+    for (ONode* c : n->children) block_sankoff_assign(c, st, muts, own);
+}
+
+// ------------------------------------------------------------ E1 grouping ----
+// One NucMut as the reference stores it (src/panman.hpp:75-151).
+struct ONucMut {
+    int32_t pos;
+    int32_t gap;
+    uint8_t info;     // (len << 4) | type
+    uint32_t nucs;    // code k at bits 4*(5-k)
+};
+
+using PosMut = std::tuple<int, int8_t, int8_t>;   // (position, type, code)
+
+void group_runs(std::vector<PosMut>& v, std::vector<ONucMut>& out) {
+    // src/panman.cpp:1445-1466
+    std::sort(v.begin(), v.end());
+    auto emit = [&](size_t a, size_t b) {
+        ONucMut m;
+        m.pos = std::get<0>(v[a]);
+        m.gap = -1;
+        m.info = (uint8_t)(((b - a) << 4) + std::get<1>(v[a]));
+        m.nucs = 0;
+        for (size_t k = a; k < b; ++k) m.nucs += (uint32_t)std::get<2>(v[k]) << (4 * (5 - (k - a)));
+        out.push_back(m);
+    };
+    size_t start = 0;
+    for (size_t i = 1; i < v.size(); ++i) {
+        if (i - start == 6 || std::get<0>(v[i]) != std::get<0>(v[i - 1]) + 1 ||
+            std::get<1>(v[i]) != std::get<1>(v[i - 1])) {
+            emit(start, i);
+            start = i;
+        }
+    }
+    if (!v.empty()) emit(start, v.size());
+}
+
+// ------------------------------------------------------------ MSA readers ----
+struct Msa {
+    std::map<std::string, std::string> rows;
+    size_t width = 0;
+};
+
+// M1 reader (src/panman.cpp:1285-1322), '\r'-tolerant.
+bool read_msa_m1(const std::string& text, Msa& msa, std::string& err) {
+    std::istringstream in(text);
+    std::string line, seq, id;
+    size_t width = 0;
+    auto flush_named = [&](const std::string& name) {
+        if (width == 0) width = seq.size();
+        else if (width != seq.size()) { err = "sequence lengths don't match: " + name; return false; }
+        msa.rows[name] = seq;
+        return true;
+    };
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        if (line[0] == '>') {
+            if (!seq.empty()) {
+                std::vector<std::string> sp;
+                split_keep_quotes(id, '\r', sp);
+                if (!flush_named(sp.empty() ? std::string() : sp[0])) return false;
+            }
+            std::vector<std::string> sp;
+            split_keep_quotes(line, ' ', sp);
+            id = sp.empty() ? std::string() : sp[0].substr(1);
+            seq.clear();
+        } else {
+            std::vector<std::string> sp;
+            split_keep_quotes(line, '\r', sp);
+            seq += sp.empty() ? std::string() : sp[0];
+        }
+    }
+    if (!seq.empty() && !flush_named(id)) return false;
+    msa.width = width;
+    return true;
+}
+
+// ------------------------------------------------------------ M1 / M2 ------
+struct BuildOut {
+    std::string consensus;
+    std::map<std::string, std::vector<ONucMut>> node_muts;   // name order
+    std::string root_id;
+    std::string err;
+};
+
+using PerNode = std::unordered_map<std::string, std::vector<PosMut>>;
+
+void collect(const NucMutMap& muts, int pos, PerNode& into) {
+    for (auto& m : muts) into[m.first].emplace_back(pos, (int8_t)m.second.first, (int8_t)code_of(m.second.second));
+}
+
+void finish(OTree& t, PerNode& raw, BuildOut& out) {
+    for (auto& kv : raw) {
+        std::vector<ONucMut> recs;
+        group_runs(kv.second, recs);
+        out.node_muts[kv.first] = std::move(recs);
+    }
+    out.root_id = t.root->id;
+}
+
+// Column loop shared by M1/M2: run [lo,hi) columns, optionally on several threads
+// (the reference M1 loop is sequential, src/panman.cpp:1380-1381; M2 is tbb::parallel_for,
+// :1568; results are order-independent because every node's list is sorted later).
+template <class Fn>
+void run_columns(size_t lo, size_t hi, int threads, PerNode& raw, Fn&& body) {
+    if (threads <= 1) {
+        for (size_t i = lo; i < hi; ++i) body(i, raw);
+        return;
+    }
+    std::vector<PerNode> parts(threads);
+    std::atomic<size_t> next(lo);
+    std::vector<std::thread> pool;
+    for (int w = 0; w < threads; ++w)
+        pool.emplace_back([&, w] {
+            for (;;) {
+                size_t i = next.fetch_add(1);
+                if (i >= hi) break;
+                body(i, parts[w]);
+            }
+        });
+    for (auto& th : pool) th.join();
+    for (auto& p : parts)
+        for (auto& kv : p) {
+            auto& dst = raw[kv.first];
+            dst.insert(dst.end(), kv.second.begin(), kv.second.end());
+        }
+}
+
+void build_msa_fitch(OTree& t, Msa& msa, const std::string& reference, int threads, BuildOut& out) {
+    std::string consensus;
+    if (!reference.empty()) {
+        consensus = msa.rows[reference];
+    } else {
+        consensus.resize(msa.width);
+        for (size_t i = 0; i < msa.width; ++i) {
+            bool found = false;
+            for (auto& r : msa.rows)
+                if (r.second[i] != '-') { consensus[i] = r.second[i]; found = true; break; }
+            if (!found) {
+                // src/panman.cpp:1336-1361 drops the column from the rows but not from the
+                // consensus, so the loop reads past the shortened rows: undefined behaviour.
+                out.err = "all-gap column without reference (reference behaviour undefined)";
+                return;
+            }
+        }
+    }
+    PerNode raw;
+    run_columns(0, consensus.size(), threads, raw, [&](size_t i, PerNode& sink) {
+        StateMap st;
+        NucMutMap muts;
+        for (const auto& r : msa.rows) {
+            if (r.second[i] != '-') st.insert({r.first, 1 << code_of(r.second[i])});
+            else st.insert({r.first, 1});
+        }
+        int ref_state = reference.empty() ? -1 : 1 << code_of(msa.rows.at(reference)[i]);
+        fitch_up(t.root, st, ref_state);
+        int cons_state = 1 << code_of(consensus[i]);
+        fitch_down(t.root, t.root, st, cons_state, kNoDefault);
+        fitch_assign(t.root, st, muts, cons_state);
+        collect(muts, (int)i, sink);
+    });
+    out.consensus = consensus;
+    finish(t, raw, out);
+}
+
+// M2 width probe (src/panman.cpp:1479-1500): only a header that follows a non-empty
+// row sets the width, so the last row is never measured.
+size_t m2_width(const std::string& text) {
+    std::istringstream in(text);
+    std::string line, seq;
+    size_t width = 0;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        if (line[0] == '>') {
+            if (!seq.empty() && width == 0) width = seq.size();
+            seq.clear();
+        } else {
+            seq += line;
+        }
+    }
+    return width;
+}
+
+// readFastaInBatch (src/panman.cpp:677-724), without the length check it also does.
+void read_batch(const std::string& text, size_t start, size_t batch, Msa& msa) {
+    std::istringstream in(text);
+    std::string line, seq, id;
+    auto put = [&](const std::string& name) {
+        size_t take = start + batch > seq.size() ? seq.size() - start : batch;
+        msa.rows[name] = seq.substr(start, take);
+    };
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        if (line[0] == '>') {
+            if (!seq.empty()) put(id);
+            std::vector<std::string> sp;
+            split_keep_quotes(line, ' ', sp);
+            id = sp.empty() ? std::string() : sp[0].substr(1);
+            seq.clear();
+        } else {
+            seq += line;
+        }
+    }
+    if (!seq.empty()) put(id);
+}
+
+void build_msa_sankoff(OTree& t, const std::string& text, const std::string& reference,
+                       int threads, size_t batch, BuildOut& out) {
+    size_t width = m2_width(text);
+    std::string consensus(width, '\0');
+    PerNode raw;
+    for (size_t start = 0; start < width;) {
+        Msa msa;
+        read_batch(text, start, batch, msa);
+        size_t n = 0;
+        if (!msa.rows.empty()) n = msa.rows.rbegin()->second.size();
+        if (n == 0) break;
+        if (!reference.empty()) {
+            auto it = msa.rows.find(reference);
+            if (it == msa.rows.end()) { out.err = "Reference not found in the sequence"; return; }
+            for (size_t i = 0; i < n; ++i) {
+                if (it->second[i] == '-') {
+                    for (auto& r : msa.rows)
+                        if (r.second[i] != '-') { consensus[start + i] = r.second[i]; break; }
+                } else {
+                    consensus[start + i] = it->second[i];
+                }
+            }
+        } else {
+            for (size_t i = 0; i < n; ++i) {
+                bool found = false;
+                for (auto& r : msa.rows)
+                    if (r.second[i] != '-') { consensus[start + i] = r.second[i]; found = true; break; }
+                if (!found) { out.err = "all-gap column without reference (reference exits)"; return; }
+            }
+        }
+        run_columns(0, n, threads, raw, [&](size_t i, PerNode& sink) {
+            CostMap cs;
+            StateMap st;
+            NucMutMap muts;
+            for (const auto& r : msa.rows) {
+                std::vector<int> v(16, kSankoffInf);
+                v[r.second[i] != '-' ? code_of(r.second[i]) : 0] = 0;
+                cs[r.first] = v;
+            }
+            int forced = -1;
+            if (!reference.empty()) {
+                char rc = msa.rows.at(reference)[i];
+                forced = rc != '-' ? code_of(rc) : 0;
+            }
+            sankoff_up(t.root, cs);
+            int cons_code = code_of(consensus[start + i]);
+            sankoff_down(t.root, t.root, cs, st, cons_code, forced != -1 ? forced : kNoDefault);
+            sankoff_assign(t.root, st, muts, cons_code);
+            collect(muts, (int)(start + i), sink);
+        });
+        start += n;
+    }
+    out.consensus = consensus;
+    finish(t, raw, out);
+}
+
+char* dup_string(const std::string& s) {
+    char* p = (char*)std::malloc(s.size() + 1);
+    std::memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    return p;
+}
+
+// Canonical text dump shared with the product's host driver (byte-identical format).
+std::string dump_build(const BuildOut& b) {
+    std::ostringstream os;
+    if (!b.err.empty()) { os << "#error\t" << b.err << "\n"; return os.str(); }
+    os << "#consensus\t" << b.consensus << "\n";
+    os << "#blockmut\t" << b.root_id << "\t0\t-1\t1\t0\n";   // root BlockMut(0, BI, false)
+    for (auto& kv : b.node_muts) {
+        for (auto& m : kv.second) {
+            char buf[96];
+            std::snprintf(buf, sizeof buf, "\t%d\t%d\t%u\t%06x\n", m.pos, m.gap, (unsigned)m.info,
+                          (unsigned)m.nucs);
+            os << kv.first << buf;
+        }
+    }
+    return os.str();
+}
+
+// ---------------------------------------------------------- CSR trees -------
+// Bench / parity entry: a tree given as CSR with names, leaf columns as codes.
+struct CsrTree {
+    OTree t;
+    std::vector<ONode*> by_index;
+};
+
+void csr_to_tree(int32_t n, const int32_t* child_off, const int32_t* child_idx, int32_t root,
+                 const char* names, CsrTree& ct) {
+    ct.by_index.assign(n, nullptr);
+    const char* p = names;
+    std::vector<std::string> nm(n);
+    for (int32_t i = 0; i < n; ++i) { nm[i] = p; p += nm[i].size() + 1; }
+    for (int32_t i = 0; i < n; ++i) {
+        ONode* x = new ONode();
+        x->id = nm[i];
+        ct.t.owned.push_back(x);
+        ct.by_index[i] = x;
+        ct.t.all[x->id] = x;
+    }
+    for (int32_t i = 0; i < n; ++i)
+        for (int32_t e = child_off[i]; e < child_off[i + 1]; ++e) {
+            ONode* c = ct.by_index[child_idx[e]];
+            c->parent = ct.by_index[i];
+            ct.by_index[i]->children.push_back(c);
+        }
+    ct.t.root = ct.by_index[root];
+}
+
+}  // namespace
+
+// ===================================================================== C API ==
+extern "C" {
+
+void oracle_free(void* p) { std::free(p); }
+
+// M1 (mode 0: FILE_TYPE::MSA, Fitch) / M2 (mode 1: FILE_TYPE::MSA_OPTIMIZE, Sankoff).
+// Returns the canonical dump (malloc'd; release with oracle_free).
+char* oracle_msa_build(const char* newick, const char* msa_text, const char* reference, int mode,
+                       int threads) {
+    BuildOut out;
+    OTree t;
+    std::string err;
+    std::string first_line(newick);
+    size_t nl = first_line.find('\n');
+    if (nl != std::string::npos) first_line.resize(nl);
+    if (!parse_newick(first_line, t, err)) { out.err = err; return dup_string(dump_build(out)); }
+    std::string ref = reference ? reference : "";
+    if (mode == 0) {
+        Msa msa;
+        if (!read_msa_m1(msa_text, msa, err)) { out.err = err; return dup_string(dump_build(out)); }
+        build_msa_fitch(t, msa, ref, threads, out);
+    } else {
+        build_msa_sankoff(t, msa_text, ref, threads, 20000, out);
+    }
+    return dup_string(dump_build(out));
+}
+
+// One column through the per-column routines on a Newick tree (KAT driver).
+// algo: 0 nuc Fitch, 1 nuc Sankoff, 2 block Fitch, 3 block Sankoff.
+// leaves: "name=V,name=V" -- V is a nucleotide char (algo 0/1) or a state digit
+// (algo 2: 1/2/4, algo 3: 0/1/2).  Leaves not listed are absent.
+// forced: refState (algo 0, forward) / defaultState (others); -1 = none.
+// parent: the root's parent state passed to backward/assign (algo 0: a char code is
+// converted to 1<<code by the caller, i.e. pass the state).
+char* oracle_column(const char* newick, const char* leaves, int algo, int forced, int parent) {
+    OTree t;
+    std::string err;
+    std::ostringstream os;
+    if (!parse_newick(newick, t, err)) { os << "#error\t" << err << "\n"; return dup_string(os.str()); }
+    std::vector<std::pair<std::string, std::string>> kv;
+    {
+        std::vector<std::string> items;
+        split_keep_quotes(leaves, ',', items);
+        for (auto& it : items) {
+            size_t eq = it.rfind('=');
+            kv.emplace_back(it.substr(0, eq), it.substr(eq + 1));
+        }
+    }
+    StateMap st;
+    CostMap cs;
+    NucMutMap nm;
+    BlockMutMap bm;
+    if (algo == 0) {
+        for (auto& p : kv) st[p.first] = p.second[0] != '-' ? 1 << code_of(p.second[0]) : 1;
+        fitch_up(t.root, st, forced);
+        for (auto& n : t.all) os << "F\t" << n.first << "\t" << st[n.first] << "\n";
+        fitch_down(t.root, t.root, st, parent, kNoDefault);
+        for (auto& n : t.all) os << "B\t" << n.first << "\t" << st[n.first] << "\n";
+        fitch_assign(t.root, st, nm, parent);
+    } else if (algo == 1) {
+        for (auto& p : kv) {
+            std::vector<int> v(16, kSankoffInf);
+            v[p.second[0] != '-' ? code_of(p.second[0]) : 0] = 0;
+            cs[p.first] = v;
+        }
+        sankoff_up(t.root, cs);
+        for (auto& n : t.all) {
+            os << "F\t" << n.first << "\t";
+            for (int i = 0; i < 16; ++i) os << (i ? "," : "") << cs[n.first][i];
+            os << "\n";
+        }
+        sankoff_down(t.root, t.root, cs, st, parent, forced == -1 ? kNoDefault : forced);
+        for (auto& n : t.all) os << "B\t" << n.first << "\t" << st[n.first] << "\n";
+        sankoff_assign(t.root, st, nm, parent);
+    } else if (algo == 2) {
+        for (auto& p : kv) st[p.first] = std::atoi(p.second.c_str());
+        block_fitch_up(t.root, st);
+        for (auto& n : t.all) os << "F\t" << n.first << "\t" << st[n.first] << "\n";
+        block_fitch_down(t.root, t.root, st, parent, forced == -1 ? kNoDefault : forced);
+        for (auto& n : t.all) os << "B\t" << n.first << "\t" << st[n.first] << "\n";
+        block_fitch_assign(t.root, st, bm, parent);
+    } else {
+        for (auto& p : kv) {
+            std::vector<int> v(3, kSankoffInf);
+            v[std::atoi(p.second.c_str())] = 0;
+            cs[p.first] = v;
+        }
+        block_sankoff_up(t.root, cs);
+        for (auto& n : t.all) {
+            os << "F\t" << n.first << "\t";
+            for (int i = 0; i < 3; ++i) os << (i ? "," : "") << cs[n.first][i];
+            os << "\n";
+        }
+        block_sankoff_down(t.root, t.root, cs, st, parent, forced == -1 ? kNoDefault : forced);
+        for (auto& n : t.all) os << "B\t" << n.first << "\t" << st[n.first] << "\n";
+        block_sankoff_assign(t.root, st, bm, parent);
+    }
+    std::map<std::string, std::string> sorted;
+    for (auto& m : nm) sorted[m.first] = std::to_string(m.second.first) + "\t" + m.second.second;
+    for (auto& m : bm) sorted[m.first] = std::to_string(m.second.first) + "\t" + (m.second.second ? "1" : "0");
+    for (auto& m : sorted) os << "M\t" << m.first << "\t" << m.second << "\n";
+    return dup_string(os.str());
+}
+
+// Column block on a CSR tree (bench baseline + full-size parity samples).
+//   child_off[n+1], child_idx[]: children in order; names: n NUL-terminated strings.
+//   leaf_codes: row r holds `sites` 4-bit codes, one byte per site; node_row[i] is the
+//   row of leaf i, or -1 for a leaf absent from the alignment.
+//   cons: per-site consensus code; ref: per-site forced root code or NULL.
+//   algo 0 = Fitch (M1 semantics, ref -> refState=1<<code), 1 = Sankoff (M2 semantics,
+//   ref -> defaultState=code).
+//   Output: *out_recs = malloc'd uint32 quads (node, site, type, code), *out_n = count,
+//   sorted by (node, site).  Returns wall seconds of the column loop.
+double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* child_idx, int32_t root,
+                          const char* names, const uint8_t* leaf_codes, int64_t row_stride,
+                          const int32_t* node_row, int64_t sites, const uint8_t* cons,
+                          const uint8_t* ref, int algo, int threads, uint32_t** out_recs,
+                          int64_t* out_n) {
+    CsrTree ct;
+    csr_to_tree(n, child_off, child_idx, root, names, ct);
+    std::unordered_map<std::string, int32_t> index_of;
+    for (int32_t i = 0; i < n; ++i) index_of[ct.by_index[i]->id] = i;
+    std::vector<std::pair<int32_t, int32_t>> present;   // (node, row)
+    for (int32_t i = 0; i < n; ++i)
+        if (child_off[i] == child_off[i + 1] && node_row[i] >= 0) present.emplace_back(i, node_row[i]);
+
+    std::vector<std::vector<uint32_t>> parts(std::max(1, threads));
+    std::atomic<int64_t> next(0);
+    auto t0 = std::chrono::steady_clock::now();
+    auto worker = [&](int w) {
+        for (;;) {
+            int64_t s = next.fetch_add(1);
+            if (s >= sites) break;
+            NucMutMap muts;
+            if (algo == 0) {
+                StateMap st;
+                for (auto& pr : present) {
+                    int c = leaf_codes[(int64_t)pr.second * row_stride + s];
+                    st.insert({ct.by_index[pr.first]->id, 1 << c});
+                }
+                int ref_state = ref ? 1 << ref[s] : -1;
+                fitch_up(ct.t.root, st, ref_state);
+                int cs = 1 << cons[s];
+                fitch_down(ct.t.root, ct.t.root, st, cs, kNoDefault);
+                fitch_assign(ct.t.root, st, muts, cs);
+            } else {
+                CostMap costs;
+                StateMap st;
+                for (auto& pr : present) {
+                    std::vector<int> v(16, kSankoffInf);
+                    v[leaf_codes[(int64_t)pr.second * row_stride + s]] = 0;
+                    costs[ct.by_index[pr.first]->id] = v;
+                }
+                sankoff_up(ct.t.root, costs);
+                sankoff_down(ct.t.root, ct.t.root, costs, st, cons[s], ref ? (int)ref[s] : kNoDefault);
+                sankoff_assign(ct.t.root, st, muts, cons[s]);
+            }
+            for (auto& m : muts) {
+                auto& o = parts[w];
+                o.push_back((uint32_t)index_of[m.first]);
+                o.push_back((uint32_t)s);
+                o.push_back((uint32_t)m.second.first);
+                o.push_back((uint32_t)code_of(m.second.second));
+            }
+        }
+    };
+    if (threads <= 1) {
+        worker(0);
+    } else {
+        std::vector<std::thread> pool;
+        for (int w = 0; w < threads; ++w) pool.emplace_back(worker, w);
+        for (auto& th : pool) th.join();
+    }
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<std::array<uint32_t, 4>> all;
+    for (auto& p : parts)
+        for (size_t i = 0; i < p.size(); i += 4) all.push_back({p[i], p[i + 1], p[i + 2], p[i + 3]});
+    std::sort(all.begin(), all.end());
+    *out_n = (int64_t)all.size();
+    *out_recs = (uint32_t*)std::malloc(sizeof(uint32_t) * 4 * (all.size() + 1));
+    for (size_t i = 0; i < all.size(); ++i) std::memcpy(*out_recs + 4 * i, all[i].data(), 16);
+    return secs;
+}
+
+}  // extern "C"
