@@ -1,0 +1,26 @@
+# libpanman_amd.so: HIP kernels + C-ABI for gfx950 (MI355X).  No CPU fallback inside.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+SRC := $(wildcard panman_amd/csrc/*.cpp) $(wildcard panman_amd/csrc/*.hip)
+HDR := $(wildcard panman_amd/csrc/*.h) include/panman_gpu.h
+OBJ := $(patsubst panman_amd/csrc/%,build/%.o,$(SRC))
+LIB := panman_amd/libpanman_amd.so
+
+all: $(LIB) oracle
+
+build/%.o: panman_amd/csrc/% $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Fitch small-parsimony throughput on MI355X (site*node updates/s), driver contract.
+
+Workload (BASELINE.json north star / SURVEY.md §8d): synthetic random-join tree (T1,
+seed 1) with `--leaves` leaves per GPU and `--sites` alignment columns in total
+(default 1M x 30k = N*, 1 GPU).  At N GPUs the job is weak-scaled exactly as config C4:
+the tree has N x leaves leaves and the columns are sharded across ranks (S/N each), so
+per-GPU work is constant; 8 GPUs = 8M leaves x 30k sites.  One step = post-order +
+pre-order + mutation assignment + per-site score over the rank's shard, then one RCCL
+all-gather of (score, root code) per site.  Inputs are generated on the
+device before timing (resident in HBM).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import panman_amd  # noqa: E402  (after torch: one HIP runtime per process)
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md chip-level table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--leaves", type=int, default=1_000_000, help="leaves per GPU")
+    p.add_argument("--sites", type=int, default=30_000, help="alignment columns in total")
+    p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
+                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    L = args.leaves * world
+    S = args.sites
+    lo, hi = rank * S // world, (rank + 1) * S // world
+    s_local = hi - lo
+    t0 = time.time()
+    off, idx, root = panman_amd.random_join_tree(L, seed=1)
+    n_nodes = 2 * L - 1
+    n_int = L - 1
+    log(rank, f"[bench] tree: {L} leaves, {n_nodes} nodes ({time.time() - t0:.1f}s)")
+
+    eng = panman_amd.Engine(local)
+    stream = torch.cuda.current_stream()
+    eng.set_stream(stream.cuda_stream)
+    eng.tree_upload(off, idx, root)
+    eng.synth_columns(lo, s_local, seed=2)
+    torch.cuda.synchronize()
+    log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
+
+    score_all = torch.zeros(S + world, dtype=torch.int32, device="cuda")
+    root_all = torch.zeros(S + world, dtype=torch.uint8, device="cuda")
+    per = (S + world - 1) // world
+    score_loc = torch.zeros(per, dtype=torch.int32, device="cuda")
+    root_loc = torch.zeros(per, dtype=torch.uint8, device="cuda")
+
+    def step():
+        eng.run(panman_amd.MODE_FITCH)
+        eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(score_all[: per * world], score_loc)
+            dist.all_gather_into_tensor(root_all[: per * world], root_loc)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    muts = eng.mutation_count()   # sizes the record buffers (re-runs once if a shard overflowed)
+    torch.cuda.synchronize()
+
+    eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    ms, launches = eng.kernel_times(3)
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        m = torch.tensor([float(muts)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(m, op=dist.ReduceOp.SUM)
+        muts_total = int(m.item())
+    else:
+        muts_total = muts
+
+    updates = float(S) * n_nodes * args.steps
+    value = updates / elapsed
+    ms_step = elapsed * 1e3 / args.steps
+
+    # Roofline of the dominant kernel (SURVEY.md §8d contract bytes, per site of this shard):
+    #   post-order  0.5 L (leaf codes) + 2 I (set write) + 2 (I-1) (set read by parent)
+    #   pre-order   2 I (set read) + 0.5 I (final write) + 0.5 (N-1) (parent final read)
+    #               + 0.5 L (leaf re-read) + 8 B per emitted mutation record
+    up_bytes = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1))
+    down_bytes = s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
+    classes = {
+        "k_fitch_up": (ms[0] / args.steps, launches[0] / max(1, args.steps), up_bytes),
+        "k_fitch_down": (ms[1] / args.steps, launches[1] / max(1, args.steps), down_bytes),
+    }
+    dom = max(classes, key=lambda k: classes[k][0])
+    dms, dl, dbytes = classes[dom]
+    achieved = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            key = f"{L}x{s_local}"
+            if key in tr.get(dom, {}):
+                traffic = tr[dom][key] * dl   # bytes per launch x launches per step = per step
+        except Exception:
+            traffic = None
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom,
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "algorithmic_bytes_per_step": dbytes,
+        "kernel_ms_per_step": round(dms, 3),
+        "launches_per_step": dl,
+        "other_kernels_ms_per_step": {k: round(v[0], 3) for k, v in classes.items() if k != dom},
+        "score_kernel_ms_per_step": round(ms[2] / args.steps, 3),
+        "pipeline_effective_GBs": round((up_bytes + down_bytes) / (ms_step * 1e-3) / 1e9, 1),
+    }
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes)
+
+    if rank == 0:
+        out = {
+            "metric": "Fitch-Sankoff site*node updates/sec (Fitch mode)",
+            "value": value,
+            "unit": "site*node updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 bit-planes (16-bit one-hot state sets)",
+            "data": "synthetic (seeded on-device tree-evolved columns, random-join tree)",
+            "config": {
+                "workload": f"N* Fitch: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)",
+                "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
+                "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
+                "mutations_total": muts_total,
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity_sample": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, eng, off, idx, root, L, n_nodes):
+    """Reference-faithful CPU path (oracle: per-column unordered_map<string,int> +
+    recursion, src/fitchSankoff.cpp:30-171) on a bounded column sample, plus a bit-exact
+    check of the GPU kernels on the same sample at full tree size."""
+    sys.path.insert(0, ROOT)
+    import oracle as orc
+    ns = args.cpu_sites
+    codes = eng.leaf_codes(0, ns, L)
+    cons = eng.consensus(0, ns)
+    names = [f"s{i}" if i < L else f"node_{i}" for i in range(n_nodes)]
+    node_row = np.full(n_nodes, -1, np.int32)
+    node_row[:L] = np.arange(L, dtype=np.int32)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    o = orc.load()
+    secs, want = o.csr_columns(off, idx, root, names, codes, node_row, cons, None, algo=0, threads=threads)
+    cpu = {"value": ns * n_nodes / secs, "unit": "site*node updates/s", "cores": threads,
+           "kind": "port",
+           "sample": f"first {ns} of the same columns, {L} leaves x {ns} sites, {threads} threads "
+                     f"({secs:.1f}s), oracle/pm_oracle.cpp faithful per-column loop"}
+    # GPU on the identical sample columns (same kernels, separate context)
+    e2 = panman_amd.Engine(0)
+    e2.tree_upload(off, idx, root)
+    e2.leaves_upload(codes, node_row)
+    e2.sites_upload(cons)
+    e2.run(panman_amd.MODE_FITCH)
+    got = e2.mutations()
+    e2.close()
+    parity = {"sites": ns, "records": int(want.shape[0]),
+              "bit_exact": bool(got.shape == want.shape and (got == want).all())}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

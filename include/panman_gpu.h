@@ -1,0 +1,148 @@
+/* panman_gpu.h -- C-ABI of the MI355X small-parsimony engine (libpanman_amd.so).
+ *
+ * Drop-in boundary for the reference's per-column parsimony path.  The reference
+ * (faithokamoto/panman) has no FFI of its own: its kernels are C++ Tree members called
+ * once per alignment column from the construction drivers.  Each entry point below names
+ * the reference interface it replaces (paths relative to the reference root):
+ *
+ *   per-column Fitch      Tree::nucFitchForwardPass / BackwardPass / AssignMutations
+ *                         src/panman.hpp:846-857, src/fitchSankoff.cpp:30-171
+ *   per-column Sankoff    Tree::nucSankoff{Forward,Backward}Pass / AssignMutations
+ *                         src/panman.hpp:860-875, src/fitchSankoff.cpp:359-703
+ *   GPU batch entry       fitch_sankoff_on_gpu(Tree*, seqs, util*)   gpu/fitchSankoff.cuh:11
+ *   column drivers        Tree(ifstream&, ifstream&, FILE_TYPE::MSA | MSA_OPTIMIZE, ref)
+ *                         src/panman.cpp:1274-1649
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Host pointers unless a name says `_device`.
+ *   - Every function returns PM_OK (0) or a negative PM_ERR_*; pm_last_error() gives the
+ *     message.  Nothing here exits or aborts (the reference exit()s, src/panman.cpp:1297).
+ *   - One pm_ctx per GPU; a ctx is not thread-safe, independent ctxs are.
+ *   - Device work is queued on the ctx stream (pm_set_stream); functions that return
+ *     host data synchronise that stream.
+ *   - Codes are the reference's 4-bit NucCode (src/panman.hpp:27-44): A=1 C=2 G=4 T=8
+ *     R=5 Y=10 S=6 W=9 K=12 M=3 B=14 D=13 H=11 V=7 N=15, gap/other=0.
+ *     Packed code arrays hold two codes per byte, even site in the low nibble.
+ */
+#ifndef PANMAN_GPU_H
+#define PANMAN_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_OK 0
+#define PM_ERR_ARG (-1)
+#define PM_ERR_OOM (-2)
+#define PM_ERR_HIP (-3)
+#define PM_ERR_UNSUPPORTED (-4)
+#define PM_ERR_STATE (-5)
+
+#define PM_MODE_FITCH 0   /* F1-F3: 16-bit one-hot state sets, M1 semantics            */
+#define PM_MODE_SANKOFF 1 /* S1-S3: unit-cost Sankoff over 16 codes, M2 semantics      */
+
+#define PM_MUT_NS 0 /* NucMutationType::NS  src/panman.hpp:48 */
+#define PM_MUT_ND 1 /* NucMutationType::ND  src/panman.hpp:50 */
+#define PM_MUT_NI 2 /* NucMutationType::NI  src/panman.hpp:52 */
+
+typedef struct pm_ctx pm_ctx;
+
+/* Tree topology as CSR.  Replaces the Node* graph built by
+ * Tree::createTreeFromNewickString (src/panman.cpp:310-450) and the flattening in
+ * gpu/fitchSankoff.cu:40-83.  Children keep their Newick order.  A node with no
+ * children is a leaf.  Node ids are the caller's; mutation records use them. */
+typedef struct pm_tree {
+    int32_t num_nodes;
+    int32_t root;
+    const int32_t* child_offsets; /* [num_nodes + 1] */
+    const int32_t* child_index;   /* [child_offsets[num_nodes]] */
+} pm_tree;
+
+/* One mutation record: the (node, column, type, char) tuple the reference pushes into
+ * nonGapMutationsMSA (src/panman.cpp:1426-1430, 1607-1610). */
+typedef struct pm_mut {
+    uint32_t node;      /* caller node id                                    */
+    uint32_t site_info; /* (site << 8) | (type << 4) | code; type = PM_MUT_* */
+} pm_mut;
+
+/* Context / device (replaces the device setup of gpu/fitchSankoff.cu:370-440). */
+int pm_create(int device, pm_ctx** out);
+void pm_destroy(pm_ctx* ctx);
+const char* pm_last_error(const pm_ctx* ctx);
+/* Queue all work on `hip_stream` (a hipStream_t; NULL = the ctx's own stream). */
+int pm_set_stream(pm_ctx* ctx, void* hip_stream);
+/* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
+int pm_set_profiling(pm_ctx* ctx, int enable);
+
+/* Upload the topology (host arrays).  Levels, dense indices and the device copy are built
+ * here, once; replaces the recursion over Node* children in every per-column call. */
+int pm_tree_upload(pm_ctx* ctx, const pm_tree* tree);
+
+/* Upload the leaf columns.  Replaces the per-column `states` maps of the drivers
+ * (src/panman.cpp:1409-1417 Fitch, :1574-1582 Sankoff).
+ *   codes4[row * row_stride + s/2]: 4-bit code of site s for alignment row `row`.
+ *   node_row[node]: the row of leaf `node`, or -1 if the leaf is absent from the
+ *     alignment (reference: state 0 / all-INF, src/fitchSankoff.cpp:33-36, :362-368).
+ *   present (nullable): per-row bitmask of present sites (bit s%8 of byte
+ *     row * present_stride + s/8); a cleared bit makes that (leaf, site) absent, as the
+ *     PanGraph driver does for leaves lacking a block (src/panman.cpp:1026-1028). */
+int pm_leaves_upload(pm_ctx* ctx, int64_t num_sites, const uint8_t* codes4, int64_t row_stride,
+                     const int32_t* node_row, const uint8_t* present, int64_t present_stride);
+
+/* Per-site constants (packed codes, ceil(S/2) bytes each).
+ *   consensus: the root's parent state, i.e. the block consensus character
+ *     (src/panman.cpp:1424-1425, :1600-1606).
+ *   forced (nullable): Fitch: refState forcing the root forward set (:1419);
+ *     Sankoff: defaultState forcing the root (:1583-1596). */
+int pm_sites_upload(pm_ctx* ctx, const uint8_t* consensus4, const uint8_t* forced4);
+
+/* Run post-order, pre-order and mutation assignment for every uploaded site (async). */
+int pm_run(pm_ctx* ctx, int mode);
+
+/* Results (synchronise the stream). */
+int pm_mutation_count(pm_ctx* ctx, int64_t* count);
+/* Records sorted by (node, site); `cap` records fit in `out`. */
+int pm_mutations_fetch(pm_ctx* ctx, pm_mut* out, int64_t cap, int64_t* count);
+/* Per site: number of mutated edges below the root (parsimony score of the assignment)
+ * and the root's final code (255 = unresolved).  Either pointer may be NULL. */
+int pm_site_results(pm_ctx* ctx, int32_t* score, uint8_t* root_code);
+/* Same, copied device-to-device into caller buffers on the ctx stream (async), so that a
+ * collective can gather them without a host round trip. */
+int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_device);
+/* Accumulated device milliseconds and launch counts per kernel class since the last
+ * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram. */
+int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
+
+/* ---- column drivers ------------------------------------------------------------------ */
+/* Drop-in for Tree(msa, newick, FILE_TYPE::MSA (mode PM_MODE_FITCH, "M1") or
+ * FILE_TYPE::MSA_OPTIMIZE (PM_MODE_SANKOFF, "M2"), reference) -- src/panman.cpp:1274-1649:
+ * Newick + aligned FASTA text -> consensus block, root block insertion and every node's
+ * NucMut list (grouped as src/panman.cpp:1445-1466), computed on `device`.  Returns a
+ * malloc'd text dump (release with pm_free):
+ *   "#consensus\t<seq>\n" "#blockmut\t<root>\t0\t-1\t1\t0\n" then one line per NucMut,
+ *   nodes in name order: "<node>\t<nucPosition>\t<nucGapPosition>\t<mutInfo>\t<nucs %06x>\n";
+ * or "#error\t<message>\n" where the reference would exit or has undefined behaviour. */
+char* pm_msa_build(const char* newick, const char* msa_text, const char* reference, int mode, int device);
+void pm_free(void* p);
+
+/* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
+/* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes
+ * 2*leaves-1 nodes as CSR; leaves are ids [0, leaves), internal nodes follow. */
+int pm_synth_tree_random_join(int64_t leaves, uint64_t seed, int32_t* child_offsets,
+                              int32_t* child_index, int32_t* root);
+/* Evolve columns [site_begin, site_begin + num_sites) of a seeded alignment down the
+ * uploaded tree on the device and install them as the leaf columns plus the consensus
+ * (the root sequence).  Identical global sites give identical columns on every rank. */
+int pm_synth_columns(pm_ctx* ctx, int64_t site_begin, int64_t num_sites, uint64_t seed);
+/* Copy leaf codes of sites [s0, s0+ns) to host, one byte per site:
+ * out[leaf * ns + (s - s0)] for every leaf in increasing node-id order (absent = 0). */
+int pm_leaf_codes_fetch(pm_ctx* ctx, int64_t s0, int64_t ns, uint8_t* out);
+int pm_consensus_fetch(pm_ctx* ctx, int64_t s0, int64_t ns, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PANMAN_GPU_H */

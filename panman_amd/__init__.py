@@ -1,0 +1,7 @@
+"""panman_amd -- MI355X-native Fitch/Sankoff small parsimony for PanMAN (HIP, gfx950).
+
+The compute path is libpanman_amd.so (hand-written HIP kernels behind the C-ABI in
+include/panman_gpu.h); this package is its host-side binding.  No CPU fallback exists.
+"""
+from ._lib import LIB_PATH, MODE_FITCH, MODE_SANKOFF, PanmanError, header_symbols, load  # noqa: F401
+from .engine import Engine, msa_build, pack_codes, random_join_tree  # noqa: F401

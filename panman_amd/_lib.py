@@ -1,0 +1,79 @@
+"""ctypes binding of libpanman_amd.so (the HIP engine's C-ABI, include/panman_gpu.h).
+
+There is no CPU fallback: if the library is missing or a call fails, this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpanman_amd.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "panman_gpu.h")
+
+PM_OK = 0
+MODE_FITCH = 0
+MODE_SANKOFF = 1
+
+_lib = None
+
+
+class PanmanError(RuntimeError):
+    pass
+
+
+class Mut(C.Structure):
+    _fields_ = [("node", C.c_uint32), ("site_info", C.c_uint32)]
+
+
+class Tree(C.Structure):
+    _fields_ = [("num_nodes", C.c_int32), ("root", C.c_int32),
+                ("child_offsets", C.c_void_p), ("child_index", C.c_void_p)]
+
+
+_SIGS = {
+    "pm_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "pm_destroy": (None, [C.c_void_p]),
+    "pm_last_error": (C.c_char_p, [C.c_void_p]),
+    "pm_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pm_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "pm_tree_upload": (C.c_int, [C.c_void_p, C.POINTER(Tree)]),
+    "pm_leaves_upload": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
+                                   C.c_void_p, C.c_int64]),
+    "pm_sites_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pm_run": (C.c_int, [C.c_void_p, C.c_int]),
+    "pm_mutation_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "pm_mutations_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "pm_site_results": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pm_site_results_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pm_kernel_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "pm_synth_tree_random_join": (C.c_int, [C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p,
+                                            C.POINTER(C.c_int32)]),
+    "pm_synth_columns": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]),
+    "pm_leaf_codes_fetch": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
+    "pm_consensus_fetch": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
+    "pm_msa_build": (C.c_void_p, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
+    "pm_free": (None, [C.c_void_p]),
+}
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pm_[a-z_0-9]+)\s*\(", text)))
+
+
+def load():
+    """Load the HIP engine.  Raises if the extension was not built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PanmanError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib

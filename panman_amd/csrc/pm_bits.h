@@ -1,0 +1,71 @@
+// pm_bits.h -- bit-sliced state arithmetic for 32 alignment sites per 32-bit word.
+//
+// A Fitch state set (src/fitchSankoff.cpp:30-56 keeps it as `1 << code`, 16 bits) is held
+// as 16 one-hot bit-planes: bit b of plane v is set iff code v is in the set of site b.
+// A final (single) code is held as 4 code bit-planes.  Intersection / union / emptiness
+// over 32 sites are then single VALU ops per plane.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pm {
+
+// 4 code planes -> 16 one-hot planes; `m` masks present sites (absent sites -> empty set).
+__device__ __forceinline__ void onehot_from_code(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
+                                                 uint32_t m, uint32_t* out) {
+    const uint32_t n0 = ~b0, n1 = ~b1, n2 = ~b2, n3 = ~b3;
+    const uint32_t lo[4] = {n0 & n1, b0 & n1, n0 & b1, b0 & b1};
+    const uint32_t hi[4] = {n2 & n3 & m, b2 & n3 & m, n2 & b3 & m, b2 & b3 & m};
+#pragma unroll
+    for (int v = 0; v < 16; ++v) out[v] = lo[v & 3] & hi[v >> 2];
+}
+
+// one-hot planes (at most one bit per site across planes) -> 4 code planes
+__device__ __forceinline__ void code_from_onehot(const uint32_t* in, uint32_t& b0, uint32_t& b1,
+                                                 uint32_t& b2, uint32_t& b3) {
+    const uint32_t p01 = in[1] | in[3], p05 = in[5] | in[7], p09 = in[9] | in[11], p13 = in[13] | in[15];
+    b0 = p01 | p05 | p09 | p13;
+    const uint32_t q2 = in[2] | in[3], q6 = in[6] | in[7], q10 = in[10] | in[11], q14 = in[14] | in[15];
+    b1 = q2 | q6 | q10 | q14;
+    b2 = in[4] | in[5] | q6 | in[12] | in[13] | q14;
+    b3 = in[8] | in[9] | q10 | in[12] | in[13] | q14;
+}
+
+// lowest set code per site (the reference's `currentState <<= 1` scan, :107-113, :118-121)
+__device__ __forceinline__ void lowest_code(const uint32_t* s, uint32_t* out) {
+    uint32_t seen = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        out[v] = s[v] & ~seen;
+        seen |= s[v];
+    }
+}
+
+__device__ __forceinline__ uint32_t any_plane(const uint32_t* s) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) r |= s[v];
+    return r;
+}
+
+__device__ __forceinline__ uint32_t code_at(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, int bit) {
+    return ((b0 >> bit) & 1u) | (((b1 >> bit) & 1u) << 1) | (((b2 >> bit) & 1u) << 2) |
+           (((b3 >> bit) & 1u) << 3);
+}
+
+// 64-lane exclusive prefix sum; returns the wave total through `total`.
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t& total) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+}  // namespace pm

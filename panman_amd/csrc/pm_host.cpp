@@ -1,0 +1,605 @@
+// pm_host.cpp -- host side of the C-ABI: context, tree flattening, uploads, results.
+//
+// The reference keeps the tree as Node* with children vectors and rebuilds an
+// unordered_map<string,int> per column (src/panman.cpp:1409-1417).  Here the topology is
+// flattened once (pm_tree_upload): dense internal indices, height levels for the
+// post-order and depth levels for the pre-order, children encoded for the kernels.
+#include <algorithm>
+#include <random>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "pm_internal.h"
+
+namespace pm {
+
+int fail(pm_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(pm_ctx* c, hipError_t e, const char* what) {
+    return fail(c, PM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+namespace {
+
+template <class T>
+hipError_t dev_alloc(T** p, size_t count) {
+    if (count == 0) count = 1;
+    return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * count);
+}
+
+template <class T>
+void dev_free(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+template <class T>
+hipError_t upload(T** dst, const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = dev_alloc(dst, v.size());
+    if (e != hipSuccess || v.empty()) return e;
+    e = hipMemcpyAsync(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);   // host vectors may die after return
+}
+
+void free_tree(DevTree& t) {
+    dev_free(t.child_off);
+    dev_free(t.child_enc);
+    dev_free(t.parent_dense);
+    dev_free(t.internal_id);
+    dev_free(t.leaf_id);
+    dev_free(t.up_order);
+    dev_free(t.down_order);
+    dev_free(t.leaf_parent);
+    dev_free(t.leaf_down);
+    t = DevTree{};
+}
+
+void free_columns(pm_ctx* c) {
+    dev_free(c->leaf_planes);
+    dev_free(c->leaf_present);
+    dev_free(c->leaf_flag);
+    dev_free(c->cons);
+    dev_free(c->forced);
+    dev_free(c->score);
+    dev_free(c->root_code);
+    c->has_leaves = c->has_sites = c->has_forced = false;
+    c->ran = false;
+}
+
+void free_work(pm_ctx* c) {
+    dev_free(c->sets);
+    dev_free(c->finals);
+    dev_free(c->recs);
+    dev_free(c->shard_cnt);
+    c->sets_bytes = c->finals_bytes = 0;
+    c->shard_cap = 0;
+}
+
+int64_t wpad_of(const pm_ctx* c) { return (int64_t)((c->words + kWave - 1) / kWave) * kWave; }
+
+// Allocate per-shard column buffers (leaf planes, consensus, outputs) for S sites.
+int alloc_columns(pm_ctx* c, int64_t sites) {
+    free_columns(c);
+    c->num_sites = sites;
+    c->words = (int32_t)((sites + 31) / 32);
+    const int64_t wpad = wpad_of(c);
+    hipError_t e;
+    if ((e = dev_alloc(&c->leaf_planes, (size_t)c->dt.num_leaves * wpad)) != hipSuccess ||
+        (e = dev_alloc(&c->leaf_flag, (size_t)c->dt.num_leaves)) != hipSuccess ||
+        (e = dev_alloc(&c->cons, (size_t)wpad)) != hipSuccess ||
+        (e = dev_alloc(&c->forced, (size_t)wpad)) != hipSuccess ||
+        (e = dev_alloc(&c->score, (size_t)sites)) != hipSuccess ||
+        (e = dev_alloc(&c->root_code, (size_t)sites)) != hipSuccess) {
+        free_columns(c);
+        return fail(c, PM_ERR_OOM, std::string("column buffers: ") + hipGetErrorString(e));
+    }
+    (void)hipMemsetAsync(c->cons, 0, sizeof(uint4) * wpad, c->stream);
+    return PM_OK;
+}
+
+// Work buffers sized for the current shard and mode; records get a first-guess capacity
+// that pm_mutation_count grows on overflow.
+int alloc_work(pm_ctx* c, int mode) {
+    const int64_t wpad = wpad_of(c);
+    const size_t planes = mode == PM_MODE_FITCH ? 16 : 32;
+    const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
+    const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
+    hipError_t e;
+    if (need_sets > c->sets_bytes) {
+        dev_free(c->sets);
+        if ((e = hipMalloc(reinterpret_cast<void**>(&c->sets), need_sets)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("state sets: ") + hipGetErrorString(e));
+        c->sets_bytes = need_sets;
+    }
+    if (need_fin > c->finals_bytes) {
+        dev_free(c->finals);
+        if ((e = hipMalloc(reinterpret_cast<void**>(&c->finals), need_fin)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("finals: ") + hipGetErrorString(e));
+        c->finals_bytes = need_fin;
+    }
+    if (!c->shard_cnt && (e = dev_alloc(&c->shard_cnt, kShards)) != hipSuccess)
+        return fail(c, PM_ERR_OOM, "shard counters");
+    if (c->shard_cap == 0) {
+        const double nodes = (double)c->dt.num_internal + c->dt.num_leaves;
+        const double guess = std::max(65536.0, 0.01 * nodes * (double)c->num_sites);
+        const int64_t cap = (int64_t)(guess * 1.5 / kShards) + 256;
+        if ((e = dev_alloc(&c->recs, (size_t)cap * kShards)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("mutation records: ") + hipGetErrorString(e));
+        c->shard_cap = cap;
+    }
+    return PM_OK;
+}
+
+int run_once(pm_ctx* c, int mode) {
+    hipError_t e = mode == PM_MODE_FITCH ? launch_fitch(c) : launch_sankoff(c);
+    if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
+    e = launch_score(c);
+    if (e != hipSuccess) return hip_fail(c, e, "score launch");
+    c->ran = true;
+    c->last_mode = mode;
+    return PM_OK;
+}
+
+// Synchronise; if any shard overflowed, grow the record buffer to fit and run again.
+int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        counts.assign(kShards, 0);
+        hipError_t e = hipMemcpyAsync(counts.data(), c->shard_cnt, sizeof(uint32_t) * kShards,
+                                      hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "result sync");
+        const uint32_t worst = *std::max_element(counts.begin(), counts.end());
+        if ((int64_t)worst <= c->shard_cap) return PM_OK;
+        dev_free(c->recs);
+        const int64_t cap = (int64_t)worst + worst / 8 + 256;
+        if ((e = dev_alloc(&c->recs, (size_t)cap * kShards)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("mutation records: ") + hipGetErrorString(e));
+        c->shard_cap = cap;
+        int rc = run_once(c, c->last_mode);
+        if (rc != PM_OK) return rc;
+    }
+    return fail(c, PM_ERR_STATE, "mutation record buffer still overflowing");
+}
+
+}  // namespace
+
+void timer_begin(pm_ctx* c, int cls) {
+    if (!c->profiling) return;
+    auto& v = c->timers[cls];
+    if (c->timers_used[cls] == v.size()) {
+        Timer t;
+        (void)hipEventCreate(&t.a);
+        (void)hipEventCreate(&t.b);
+        v.push_back(t);
+    }
+    (void)hipEventRecord(v[c->timers_used[cls]].a, c->stream);
+}
+
+void timer_end(pm_ctx* c, int cls) {
+    if (!c->profiling) return;
+    (void)hipEventRecord(c->timers[cls][c->timers_used[cls]].b, c->stream);
+    ++c->timers_used[cls];
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+int pm_create(int device, pm_ctx** out) {
+    if (!out) return PM_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return PM_ERR_HIP;
+    if (device < 0 || device >= n) return PM_ERR_ARG;
+    if ((e = hipSetDevice(device)) != hipSuccess) return PM_ERR_HIP;
+    pm_ctx* c = new pm_ctx();
+    c->device = device;
+    if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete c;
+        return PM_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return PM_OK;
+}
+
+void pm_destroy(pm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_work(c);
+    free_columns(c);
+    free_tree(c->dt);
+    for (auto& v : c->timers)
+        for (auto& t : v) {
+            (void)hipEventDestroy(t.a);
+            (void)hipEventDestroy(t.b);
+        }
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* pm_last_error(const pm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pm_set_stream(pm_ctx* c, void* s) {
+    if (!c) return PM_ERR_ARG;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    return PM_OK;
+}
+
+int pm_set_profiling(pm_ctx* c, int enable) {
+    if (!c) return PM_ERR_ARG;
+    c->profiling = enable != 0;
+    for (auto& u : c->timers_used) u = 0;
+    return PM_OK;
+}
+
+int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
+    if (!c || !t || !t->child_offsets || t->num_nodes < 2) return fail(c, PM_ERR_ARG, "bad tree");
+    (void)hipSetDevice(c->device);
+    const int32_t N = t->num_nodes;
+    const int32_t* off = t->child_offsets;
+    const int32_t* idx = t->child_index;
+    if (off[0] != 0 || t->root < 0 || t->root >= N) return fail(c, PM_ERR_ARG, "bad tree header");
+    for (int32_t i = 0; i < N; ++i)
+        if (off[i + 1] < off[i]) return fail(c, PM_ERR_ARG, "child offsets not monotone");
+    const int32_t E = off[N];
+    if (E != N - 1) return fail(c, PM_ERR_ARG, "a tree on N nodes has N-1 edges");
+    std::vector<int32_t> parent(N, -2);
+    parent[t->root] = -1;
+    for (int32_t i = 0; i < N; ++i)
+        for (int32_t e = off[i]; e < off[i + 1]; ++e) {
+            const int32_t ch = idx[e];
+            if (ch < 0 || ch >= N || parent[ch] != -2) return fail(c, PM_ERR_ARG, "child index invalid or repeated");
+            parent[ch] = i;
+        }
+    if (off[t->root + 1] == off[t->root]) return fail(c, PM_ERR_ARG, "root must be internal");
+    // BFS from the root: depth + connectivity.
+    std::vector<int32_t> bfs;
+    bfs.reserve(N);
+    std::vector<int32_t> depth(N, -1);
+    bfs.push_back(t->root);
+    depth[t->root] = 0;
+    for (size_t h = 0; h < bfs.size(); ++h) {
+        const int32_t u = bfs[h];
+        for (int32_t e = off[u]; e < off[u + 1]; ++e) {
+            depth[idx[e]] = depth[u] + 1;
+            bfs.push_back(idx[e]);
+        }
+    }
+    if ((int32_t)bfs.size() != N) return fail(c, PM_ERR_ARG, "tree is not connected");
+    std::vector<int32_t> height(N, 0);
+    for (int32_t k = N - 1; k >= 0; --k) {
+        const int32_t u = bfs[k];
+        int32_t h = 0;
+        for (int32_t e = off[u]; e < off[u + 1]; ++e) h = std::max(h, height[idx[e]] + 1);
+        height[u] = off[u + 1] > off[u] ? h : 0;
+    }
+
+    HostTree ht;
+    ht.num_nodes = N;
+    ht.root = t->root;
+    ht.dense_of.assign(N, 0);
+    for (int32_t i = 0; i < N; ++i) {
+        if (off[i + 1] > off[i]) {
+            ht.dense_of[i] = (int32_t)ht.internal_id.size();
+            ht.internal_id.push_back(i);
+        } else {
+            ht.dense_of[i] = -(int32_t)ht.leaf_id.size() - 1;
+            ht.leaf_id.push_back(i);
+        }
+    }
+    const int32_t I = (int32_t)ht.internal_id.size();
+    const int32_t L = (int32_t)ht.leaf_id.size();
+    ht.child_off.assign(I + 1, 0);
+    ht.child_enc.reserve(E);
+    std::vector<int32_t> parent_dense(I, -1), leaf_parent(L, -1);
+    for (int32_t d = 0; d < I; ++d) {
+        const int32_t u = ht.internal_id[d];
+        for (int32_t e = off[u]; e < off[u + 1]; ++e) {
+            const int32_t ch = idx[e];
+            ht.child_enc.push_back(ht.dense_of[ch]);
+            if (ht.dense_of[ch] >= 0) parent_dense[ht.dense_of[ch]] = d;
+            else leaf_parent[-ht.dense_of[ch] - 1] = d;
+        }
+        ht.child_off[d + 1] = (int32_t)ht.child_enc.size();
+    }
+    // post-order levels: internal nodes by height 1..H
+    int32_t H = 0, D = 0;
+    for (int32_t d = 0; d < I; ++d) {
+        H = std::max(H, height[ht.internal_id[d]]);
+        D = std::max(D, depth[ht.internal_id[d]]);
+    }
+    int32_t DL = 0;
+    for (int32_t l = 0; l < L; ++l) DL = std::max(DL, depth[ht.leaf_id[l]]);
+    auto bucket = [](int32_t levels, int32_t count, auto key, std::vector<int32_t>& offs, std::vector<int32_t>& order) {
+        offs.assign(levels + 1, 0);
+        for (int32_t i = 0; i < count; ++i) ++offs[key(i) + 1];
+        for (int32_t k = 0; k < levels; ++k) offs[k + 1] += offs[k];
+        order.assign(count, 0);
+        std::vector<int32_t> cur(offs.begin(), offs.end() - 1);
+        for (int32_t i = 0; i < count; ++i) order[cur[key(i)]++] = i;
+    };
+    std::vector<int32_t> up_order, down_order, leaf_down;
+    bucket(H, I, [&](int32_t d) { return height[ht.internal_id[d]] - 1; }, ht.up_level_off, up_order);
+    bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
+    bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
+
+    free_work(c);
+    free_columns(c);
+    free_tree(c->dt);
+    DevTree dt;
+    dt.num_internal = I;
+    dt.num_leaves = L;
+    dt.root_dense = ht.dense_of[t->root];
+    hipError_t e;
+    if ((e = upload(&dt.child_off, ht.child_off, c->stream)) != hipSuccess ||
+        (e = upload(&dt.child_enc, ht.child_enc, c->stream)) != hipSuccess ||
+        (e = upload(&dt.parent_dense, parent_dense, c->stream)) != hipSuccess ||
+        (e = upload(&dt.internal_id, ht.internal_id, c->stream)) != hipSuccess ||
+        (e = upload(&dt.leaf_id, ht.leaf_id, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_order, up_order, c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_order, down_order, c->stream)) != hipSuccess ||
+        (e = upload(&dt.leaf_parent, leaf_parent, c->stream)) != hipSuccess ||
+        (e = upload(&dt.leaf_down, leaf_down, c->stream)) != hipSuccess) {
+        free_tree(dt);
+        return hip_fail(c, e, "tree upload");
+    }
+    c->dt = dt;
+    c->ht = std::move(ht);
+    c->has_tree = true;
+    return PM_OK;
+}
+
+int pm_leaves_upload(pm_ctx* c, int64_t S, const uint8_t* codes4, int64_t row_stride, const int32_t* node_row,
+                     const uint8_t* present, int64_t present_stride) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->has_tree) return fail(c, PM_ERR_STATE, "upload the tree first");
+    if (S <= 0 || S >= (int64_t)1 << 24 || !codes4 || !node_row || row_stride < (S + 1) / 2)
+        return fail(c, PM_ERR_ARG, "bad leaf matrix arguments (0 < sites < 2^24)");
+    if (present && present_stride < (S + 7) / 8) return fail(c, PM_ERR_ARG, "bad presence stride");
+    (void)hipSetDevice(c->device);
+    const int32_t L = c->dt.num_leaves;
+    std::vector<int32_t> row_of_leaf(L);
+    std::vector<uint8_t> flag(L);
+    int32_t rows = 0;
+    for (int32_t l = 0; l < L; ++l) {
+        row_of_leaf[l] = node_row[c->ht.leaf_id[l]];
+        flag[l] = row_of_leaf[l] < 0 ? kLeafAbsent : (present ? kLeafPartial : kLeafPresent);
+        rows = std::max(rows, row_of_leaf[l] + 1);
+    }
+    int rc = alloc_columns(c, S);
+    if (rc != PM_OK) return rc;
+    const int64_t wpad = wpad_of(c);
+    hipError_t e;
+    if (present && (e = dev_alloc(&c->leaf_present, (size_t)L * wpad)) != hipSuccess)
+        return fail(c, PM_ERR_OOM, "presence planes");
+    uint8_t* d_codes = nullptr;
+    uint8_t* d_present = nullptr;
+    int32_t* d_rows = nullptr;
+    const size_t code_bytes = (size_t)rows * row_stride;
+    const size_t pres_bytes = present ? (size_t)rows * present_stride : 0;
+    if ((e = dev_alloc(&d_codes, code_bytes)) != hipSuccess || (e = upload(&d_rows, row_of_leaf, c->stream)) != hipSuccess ||
+        (present && (e = dev_alloc(&d_present, pres_bytes)) != hipSuccess)) {
+        dev_free(d_codes);
+        dev_free(d_rows);
+        dev_free(d_present);
+        return fail(c, PM_ERR_OOM, "leaf staging");
+    }
+    e = hipMemcpyAsync(d_codes, codes4, code_bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && present) e = hipMemcpyAsync(d_present, present, pres_bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->leaf_flag, flag.data(), L, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_pack_codes(c, d_codes, row_stride, d_rows, d_present, present_stride);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d_codes);
+    dev_free(d_rows);
+    dev_free(d_present);
+    if (e != hipSuccess) return hip_fail(c, e, "leaf upload");
+    c->has_leaves = true;
+    return PM_OK;
+}
+
+int pm_sites_upload(pm_ctx* c, const uint8_t* consensus4, const uint8_t* forced4) {
+    if (!c || !consensus4) return fail(c, PM_ERR_ARG, "consensus required");
+    if (!c->has_leaves) return fail(c, PM_ERR_STATE, "upload the leaves first");
+    (void)hipSetDevice(c->device);
+    const size_t bytes = (size_t)(c->num_sites + 1) / 2;
+    uint8_t* d = nullptr;
+    hipError_t e = dev_alloc(&d, bytes);
+    if (e != hipSuccess) return fail(c, PM_ERR_OOM, "site staging");
+    e = hipMemcpyAsync(d, consensus4, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_pack_sites(c, d, c->cons);
+    if (e == hipSuccess && forced4) {
+        e = hipMemcpyAsync(d, forced4, bytes, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = launch_pack_sites(c, d, c->forced);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d);
+    if (e != hipSuccess) return hip_fail(c, e, "site upload");
+    c->has_forced = forced4 != nullptr;
+    c->has_sites = true;
+    return PM_OK;
+}
+
+int pm_run(pm_ctx* c, int mode) {
+    if (!c) return PM_ERR_ARG;
+    if (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF) return fail(c, PM_ERR_ARG, "unknown mode");
+    if (!c->has_tree || !c->has_leaves || !c->has_sites) return fail(c, PM_ERR_STATE, "tree, leaves and sites first");
+    (void)hipSetDevice(c->device);
+    int rc = alloc_work(c, mode);
+    if (rc != PM_OK) return rc;
+    return run_once(c, mode);
+}
+
+int pm_mutation_count(pm_ctx* c, int64_t* count) {
+    if (!c || !count) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    std::vector<uint32_t> counts;
+    int rc = settle(c, counts);
+    if (rc != PM_OK) return rc;
+    int64_t n = 0;
+    for (uint32_t k : counts) n += k;
+    *count = n;
+    return PM_OK;
+}
+
+int pm_mutations_fetch(pm_ctx* c, pm_mut* out, int64_t cap, int64_t* count) {
+    if (!c || !count) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    std::vector<uint32_t> counts;
+    int rc = settle(c, counts);
+    if (rc != PM_OK) return rc;
+    int64_t n = 0;
+    for (uint32_t k : counts) n += k;
+    *count = n;
+    if (!out) return PM_OK;
+    if (cap < n) return fail(c, PM_ERR_ARG, "output capacity too small");
+    int64_t at = 0;
+    for (int s = 0; s < kShards; ++s) {
+        if (!counts[s]) continue;
+        hipError_t e = hipMemcpyAsync(out + at, c->recs + (size_t)s * c->shard_cap, sizeof(pm_mut) * counts[s],
+                                      hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "record download");
+        at += counts[s];
+    }
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "record download");
+    std::sort(out, out + n, [](const pm_mut& a, const pm_mut& b) {
+        return a.node != b.node ? a.node < b.node : a.site_info < b.site_info;
+    });
+    return PM_OK;
+}
+
+int pm_site_results(pm_ctx* c, int32_t* score, uint8_t* root_code) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    std::vector<uint32_t> counts;
+    int rc = settle(c, counts);
+    if (rc != PM_OK) return rc;
+    hipError_t e = hipSuccess;
+    if (score) e = hipMemcpyAsync(score, c->score, sizeof(int32_t) * c->num_sites, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && root_code)
+        e = hipMemcpyAsync(root_code, c->root_code, c->num_sites, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? PM_OK : hip_fail(c, e, "site results");
+}
+
+int pm_site_results_device(pm_ctx* c, void* score_device, void* root_device) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    hipError_t e = hipSuccess;
+    if (score_device)
+        e = hipMemcpyAsync(score_device, c->score, sizeof(int32_t) * c->num_sites, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess && root_device)
+        e = hipMemcpyAsync(root_device, c->root_code, c->num_sites, hipMemcpyDeviceToDevice, c->stream);
+    return e == hipSuccess ? PM_OK : hip_fail(c, e, "site results (device)");
+}
+
+int pm_kernel_times(pm_ctx* c, double* ms, int64_t* launches, int classes) {
+    if (!c || !ms || !launches) return PM_ERR_ARG;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "timer sync");
+    for (int k = 0; k < classes; ++k) {
+        ms[k] = 0.0;
+        launches[k] = 0;
+        if (k >= kClasses) continue;
+        for (size_t i = 0; i < c->timers_used[k]; ++i) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, c->timers[k][i].a, c->timers[k][i].b) == hipSuccess) ms[k] += t;
+        }
+        launches[k] = (int64_t)c->timers_used[k];
+        c->timers_used[k] = 0;
+    }
+    return PM_OK;
+}
+
+int pm_synth_columns(pm_ctx* c, int64_t site_begin, int64_t S, uint64_t seed) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->has_tree) return fail(c, PM_ERR_STATE, "upload the tree first");
+    if (S <= 0 || S >= (int64_t)1 << 24 || site_begin < 0) return fail(c, PM_ERR_ARG, "bad site range");
+    (void)hipSetDevice(c->device);
+    int rc = alloc_columns(c, S);
+    if (rc != PM_OK) return rc;
+    rc = alloc_work(c, PM_MODE_FITCH);   // the generator stages internal sequences in `finals`
+    if (rc != PM_OK) return rc;
+    std::vector<uint8_t> flag(c->dt.num_leaves, kLeafPresent);
+    hipError_t e = hipMemcpyAsync(c->leaf_flag, flag.data(), flag.size(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_synth(c, site_begin, seed);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "synthetic columns");
+    c->has_leaves = c->has_sites = true;
+    c->has_forced = false;
+    return PM_OK;
+}
+
+int pm_leaf_codes_fetch(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* out) {
+    if (!c || !out || s0 < 0 || ns <= 0) return fail(c, PM_ERR_ARG, "bad range");
+    if (!c->has_leaves || s0 + ns > c->num_sites) return fail(c, PM_ERR_STATE, "range outside the uploaded sites");
+    (void)hipSetDevice(c->device);
+    uint8_t* d = nullptr;
+    const size_t bytes = (size_t)c->dt.num_leaves * ns;
+    hipError_t e = dev_alloc(&d, bytes);
+    if (e != hipSuccess) return fail(c, PM_ERR_OOM, "fetch staging");
+    e = launch_unpack_leaf_codes(c, s0, ns, d);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d);
+    return e == hipSuccess ? PM_OK : hip_fail(c, e, "leaf fetch");
+}
+
+int pm_consensus_fetch(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* out) {
+    if (!c || !out || s0 < 0 || ns <= 0) return fail(c, PM_ERR_ARG, "bad range");
+    if (!c->has_sites || s0 + ns > c->num_sites) return fail(c, PM_ERR_STATE, "range outside the uploaded sites");
+    (void)hipSetDevice(c->device);
+    uint8_t* d = nullptr;
+    hipError_t e = dev_alloc(&d, (size_t)ns);
+    if (e != hipSuccess) return fail(c, PM_ERR_OOM, "fetch staging");
+    e = launch_unpack_sites(c, c->cons, s0, ns, d);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, ns, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d);
+    return e == hipSuccess ? PM_OK : hip_fail(c, e, "consensus fetch");
+}
+
+int pm_synth_tree_random_join(int64_t leaves, uint64_t seed, int32_t* child_offsets, int32_t* child_index,
+                              int32_t* root) {
+    // SURVEY.md §8d family T1: repeatedly join two uniformly chosen pool items.
+    if (leaves < 2 || leaves > (int64_t)1 << 30 || !child_offsets || !child_index || !root) return PM_ERR_ARG;
+    std::mt19937_64 rng(seed);
+    std::vector<int32_t> pool(leaves);
+    std::iota(pool.begin(), pool.end(), 0);
+    const int64_t N = 2 * leaves - 1;
+    for (int64_t i = 0; i <= leaves; ++i) child_offsets[i] = 0;
+    int32_t next = (int32_t)leaves;
+    int64_t e = 0;
+    while (pool.size() > 1) {
+        size_t m = pool.size();
+        size_t a = rng() % m;
+        std::swap(pool[a], pool[m - 1]);
+        const int32_t x = pool[m - 1];
+        pool.pop_back();
+        --m;
+        size_t b = rng() % m;
+        std::swap(pool[b], pool[m - 1]);
+        const int32_t y = pool[m - 1];
+        pool.pop_back();
+        child_index[e++] = x;
+        child_index[e++] = y;
+        child_offsets[next + 1] = (int32_t)e;
+        pool.push_back(next++);
+    }
+    (void)N;
+    *root = pool[0];
+    return PM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// pm_internal.h -- context layout shared by the host side and the kernel launchers.
+//
+// HBM layout (one pm_ctx = one GPU = one shard of S sites, W = ceil(S/32) words):
+//   leaf planes   [L][W] uint4     4 code bit-planes of 32 sites (16 B / 32 sites)
+//   leaf present  [L][W] uint32    only for leaves with partially present columns
+//   Fitch sets    [I][W][16] u32   16 one-hot bit-planes of 32 sites (64 B / 32 sites)
+//   Sankoff sets  [I][W][32] u32   Z0 (optimal codes) + Z1 (one above optimal) planes
+//   finals        [I][W] uint4     4 code bit-planes of the internal node's final state
+//   consensus     [W] uint4        root's parent state; forced [W] uint4 (optional)
+//   records       [shards][cap]    pm_mut, sharded write cursors (one atomic per wave)
+// Internal nodes are addressed by a dense index (0..I-1), leaves by their rank among
+// leaf node ids (0..L-1).  A child is encoded as its dense internal index (>= 0) or
+// -(leaf rank + 1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/panman_gpu.h"
+
+namespace pm {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kShards = 1024;
+constexpr int kClasses = 3;
+
+enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
+
+struct DevTree {
+    int32_t num_internal = 0;
+    int32_t num_leaves = 0;
+    int32_t root_dense = -1;          // dense index of the root (internal)
+    int32_t* child_off = nullptr;     // [I+1] over dense internal index
+    int32_t* child_enc = nullptr;     // [E]
+    int32_t* parent_dense = nullptr;  // [I] parent dense index, -1 for the root
+    int32_t* internal_id = nullptr;   // [I] caller node id
+    int32_t* leaf_id = nullptr;       // [L] caller node id
+    int32_t* up_order = nullptr;      // [I] dense indices grouped by height (post-order levels)
+    int32_t* down_order = nullptr;    // [I] dense indices grouped by depth (pre-order levels)
+    int32_t* leaf_parent = nullptr;   // [L] parent dense index (synthetic generator)
+    int32_t* leaf_down = nullptr;     // [L] leaf ranks grouped by depth (synthetic generator)
+};
+
+struct HostTree {
+    int32_t num_nodes = 0;
+    int32_t root = -1;
+    std::vector<int32_t> dense_of;        // [N] dense internal index or -(leaf rank + 1)
+    std::vector<int32_t> internal_id;     // [I]
+    std::vector<int32_t> leaf_id;         // [L]
+    std::vector<int32_t> up_level_off;    // [H+1] offsets into up_order (level 0 = height 1)
+    std::vector<int32_t> down_level_off;  // [D+1] offsets into down_order (level 0 = root)
+    std::vector<int32_t> leaf_level_off;  // [D+1] offsets into leaf_down by depth
+    std::vector<int32_t> child_off;       // dense CSR (host copy)
+    std::vector<int32_t> child_enc;
+};
+
+struct Timer {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace pm
+
+struct pm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    std::string err;
+
+    pm::HostTree ht;
+    pm::DevTree dt;
+    bool has_tree = false;
+
+    // column shard
+    int64_t num_sites = 0;
+    int32_t words = 0;
+    uint4* leaf_planes = nullptr;     // [L][W]
+    uint32_t* leaf_present = nullptr; // [L][W] (allocated only when needed)
+    uint8_t* leaf_flag = nullptr;     // [L]
+    uint4* cons = nullptr;            // [W]
+    uint4* forced = nullptr;          // [W]
+    bool has_forced = false;
+    bool has_leaves = false;
+    bool has_sites = false;
+
+    // work buffers
+    uint32_t* sets = nullptr;         // [I][W][16 or 32]
+    size_t sets_bytes = 0;
+    uint4* finals = nullptr;          // [I][W]
+    size_t finals_bytes = 0;
+    pm_mut* recs = nullptr;           // [kShards][shard_cap]
+    int64_t shard_cap = 0;
+    uint32_t* shard_cnt = nullptr;    // [kShards]
+    int32_t* score = nullptr;         // [S]
+    uint8_t* root_code = nullptr;     // [S]
+    bool ran = false;
+    int last_mode = -1;
+
+    // profiling
+    bool profiling = false;
+    std::vector<pm::Timer> timers[pm::kClasses];
+    size_t timers_used[pm::kClasses] = {0, 0, 0};
+};
+
+namespace pm {
+
+int fail(pm_ctx* c, int code, const std::string& msg);
+int hip_fail(pm_ctx* c, hipError_t e, const char* what);
+
+void timer_begin(pm_ctx* c, int cls);
+void timer_end(pm_ctx* c, int cls);
+
+// kernel launchers (pm_fitch.hip / pm_sankoff.hip / pm_synth.hip)
+hipError_t launch_fitch(pm_ctx* c);
+hipError_t launch_sankoff(pm_ctx* c);
+hipError_t launch_score(pm_ctx* c);
+hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_stride, const int32_t* d_row_of_leaf,
+                             const uint8_t* d_present, int64_t present_stride);
+hipError_t launch_pack_sites(pm_ctx* c, const uint8_t* d_codes4, uint4* dst);
+hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
+hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
+hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
+
+}  // namespace pm
