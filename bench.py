@@ -137,15 +137,15 @@ def main():
     dom = max(classes, key=lambda k: classes[k][0])
     dms, dl, dbytes = classes[dom]
     achieved = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
+    # PMC-derived HBM bytes per launch of the same kernel on the same workload, if profiled
+    # (tools/pmc_traffic.py; rocprofv3 summaries live in profiles/)
     traffic = None
     if os.path.exists(args.traffic):
         try:
-            tr = json.load(open(args.traffic))
-            key = f"{L}x{s_local}"
-            if key in tr.get(dom, {}):
-                traffic = tr[dom][key] * dl   # bytes per launch x launches per step = per step
-        except Exception:
+            traffic = json.load(open(args.traffic)).get(dom, {}).get(f"{L}x{s_local}")
+        except (OSError, ValueError):
             traffic = None
+    per_launch = dbytes / dl if dl else 0.0
     roofline = {
         "bound": "hbm",
         "kernel": dom,
@@ -154,9 +154,10 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "algorithmic_bytes_per_step": dbytes,
-        "kernel_ms_per_step": round(dms, 3),
+        "algorithmic_bytes_per_launch": per_launch,
+        "avg_launch_ms": round(dms / dl, 4) if dl else None,
         "launches_per_step": dl,
+        "kernel_ms_per_step": round(dms, 3),
         "other_kernels_ms_per_step": {k: round(v[0], 3) for k, v in classes.items() if k != dom},
         "score_kernel_ms_per_step": round(ms[2] / args.steps, 3),
         "pipeline_effective_GBs": round((up_bytes + down_bytes) / (ms_step * 1e-3) / 1e9, 1),

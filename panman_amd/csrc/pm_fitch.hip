@@ -194,11 +194,25 @@ __global__ __launch_bounds__(kBlock) void k_fitch_down(DownArgs a) {
     uint32_t count = __builtin_popcount(self_diff);
     const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
+    // The first kCached leaf children keep their planes and masks in registers for the
+    // emission pass (binary trees: every leaf child); further ones are reloaded.
+    constexpr int kCached = 2;
+    uint4 cl[kCached];
+    uint32_t cd[kCached];
+    int32_t cid[kCached];
+    int ncached = 0;
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         if (c >= 0) continue;
         uint4 L;
-        count += __builtin_popcount(leaf_diff(a, -c - 1, word, valid, F, L));
+        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
+        count += __builtin_popcount(d);
+        if (ncached < kCached) {
+#pragma unroll
+            for (int k = 0; k < kCached; ++k)
+                if (k == ncached) { cl[k] = L; cd[k] = d; cid[k] = e; }
+            ++ncached;
+        }
     }
 
     if (is_root) {
@@ -220,12 +234,22 @@ __global__ __launch_bounds__(kBlock) void k_fitch_down(DownArgs a) {
     int64_t pos = (int64_t)base + excl;
 
     pos += emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0) continue;
-        uint4 L;
-        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
-        if (d) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
+#pragma unroll
+    for (int k = 0; k < kCached; ++k) {
+        if (k >= ncached) break;
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[cid[k]]);
+        if (cd[k]) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], cd[k], word, F, cl[k].x, cl[k].y,
+                               cl[k].z, cl[k].w);
+    }
+    if (ncached == kCached) {
+        int seen = 0;
+        for (int32_t e = e0; e < e1; ++e) {
+            const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+            if (c >= 0 || seen++ < kCached) continue;
+            uint4 L;
+            const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
+            if (d) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
+        }
     }
 }
 
