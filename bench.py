@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import panman_amd  # noqa: E402  (after torch: one HIP runtime per process)
+from panman_amd.shard import gather_site_results, shard_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md chip-level table)
 
@@ -63,7 +64,7 @@ def main():
 
     L = args.leaves * world
     S = args.sites
-    lo, hi = rank * S // world, (rank + 1) * S // world
+    lo, hi = shard_range(rank, world, S)
     s_local = hi - lo
     t0 = time.time()
     off, idx, root = panman_amd.random_join_tree(L, seed=1)
@@ -79,18 +80,14 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
 
-    score_all = torch.zeros(S + world, dtype=torch.int32, device="cuda")
-    root_all = torch.zeros(S + world, dtype=torch.uint8, device="cuda")
-    per = (S + world - 1) // world
-    score_loc = torch.zeros(per, dtype=torch.int32, device="cuda")
-    root_loc = torch.zeros(per, dtype=torch.uint8, device="cuda")
+    score_loc = torch.zeros(s_local, dtype=torch.int32, device="cuda")
+    root_loc = torch.zeros(s_local, dtype=torch.uint8, device="cuda")
 
     def step():
         eng.run(panman_amd.MODE_FITCH)
         eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
         if world > 1:
-            dist.all_gather_into_tensor(score_all[: per * world], score_loc)
-            dist.all_gather_into_tensor(root_all[: per * world], root_loc)
+            gather_site_results(score_loc, root_loc, S)
 
     for _ in range(max(1, args.warmup)):
         step()

@@ -33,7 +33,7 @@ def load() -> "Oracle":
         lib.oracle_csr_columns.argtypes = [
             C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_char_p,
             C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
-            C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64)]
+            C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
         _lib = lib
     return Oracle(_lib)
 
@@ -75,8 +75,9 @@ class Oracle:
         return out
 
     def csr_columns(self, child_off, child_idx, root, names, leaf_codes, node_row, cons,
-                    ref=None, algo=0, threads=1):
-        """Faithful per-column loop on a CSR tree.  Returns (seconds, records[n,4])."""
+                    ref=None, algo=0, threads=1, with_root=False):
+        """Faithful per-column loop on a CSR tree.  Returns (seconds, records[n,4]) or, with
+        with_root, (seconds, records, root_code[S]) -- root final code per site, 255 = none."""
         child_off = np.ascontiguousarray(child_off, dtype=np.int32)
         child_idx = np.ascontiguousarray(child_idx, dtype=np.int32)
         leaf_codes = np.ascontiguousarray(leaf_codes, dtype=np.uint8)
@@ -91,11 +92,14 @@ class Oracle:
             refp = ref.ctypes.data
         recs = C.POINTER(C.c_uint32)()
         cnt = C.c_int64(0)
+        root_codes = np.zeros(sites, np.uint8)
         secs = self.lib.oracle_csr_columns(
             n, child_off.ctypes.data, child_idx.ctypes.data, int(root), blob,
             leaf_codes.ctypes.data, leaf_codes.strides[0], node_row.ctypes.data, sites,
-            cons.ctypes.data, refp, algo, threads, C.byref(recs), C.byref(cnt))
+            cons.ctypes.data, refp, algo, threads, C.byref(recs), C.byref(cnt), root_codes.ctypes.data)
         k = cnt.value
         out = np.ctypeslib.as_array(recs, shape=(max(k, 1) * 4,))[: k * 4].reshape(k, 4).copy()
         self.lib.oracle_free(C.cast(recs, C.c_void_p))
+        if with_root:
+            return secs, out, root_codes
         return secs, out

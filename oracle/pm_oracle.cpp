@@ -840,7 +840,7 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
                           const char* names, const uint8_t* leaf_codes, int64_t row_stride,
                           const int32_t* node_row, int64_t sites, const uint8_t* cons,
                           const uint8_t* ref, int algo, int threads, uint32_t** out_recs,
-                          int64_t* out_n) {
+                          int64_t* out_n, uint8_t* out_root /* nullable: root final code per site, 255 = unresolved */) {
     CsrTree ct;
     csr_to_tree(n, child_off, child_idx, root, names, ct);
     std::unordered_map<std::string, int32_t> index_of;
@@ -868,6 +868,10 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
                 int cs = 1 << cons[s];
                 fitch_down(ct.t.root, ct.t.root, st, cs, kNoDefault);
                 fitch_assign(ct.t.root, st, muts, cs);
+                if (out_root) {
+                    const int r = st[ct.t.root->id];
+                    out_root[s] = r ? (uint8_t)log2_state(r) : (uint8_t)255;
+                }
             } else {
                 CostMap costs;
                 StateMap st;
@@ -879,6 +883,10 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
                 sankoff_up(ct.t.root, costs);
                 sankoff_down(ct.t.root, ct.t.root, costs, st, cons[s], ref ? (int)ref[s] : kNoDefault);
                 sankoff_assign(ct.t.root, st, muts, cons[s]);
+                if (out_root) {
+                    const int r = st[ct.t.root->id];
+                    out_root[s] = r >= 0 ? (uint8_t)r : (uint8_t)255;
+                }
             }
             for (auto& m : muts) {
                 auto& o = parts[w];

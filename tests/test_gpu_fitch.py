@@ -69,11 +69,12 @@ def _compare(engine, oracle, off, idx, root, codes, present, cons, forced):
     engine.sites_upload(cons, forced)
     engine.run(panman_amd.MODE_FITCH)
     got = engine.mutations()
-    _, want = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, forced, algo=0,
-                                 threads=8)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, forced,
+                                            algo=0, threads=8, with_root=True)
     assert got.shape == want.shape, (got.shape, want.shape)
     assert (got == want).all()
     score, rootc = engine.site_results()
+    assert (rootc == want_root).all()
     nonroot = want[want[:, 0] != root]
     assert (score == np.bincount(nonroot[:, 1], minlength=codes.shape[1])).all()
     return got
