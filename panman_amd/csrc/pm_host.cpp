@@ -330,7 +330,14 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         for (int32_t i = 0; i < count; ++i) order[cur[key(i)]++] = i;
     };
     std::vector<int32_t> up_order, down_order, leaf_down;
-    bucket(H, I, [&](int32_t d) { return height[ht.internal_id[d]] - 1; }, ht.up_level_off, up_order);
+    bucket(H * kDegreeClasses, I,
+           [&](int32_t d) {
+               return (height[ht.internal_id[d]] - 1) * kDegreeClasses +
+                      degree_class(ht.child_off[d + 1] - ht.child_off[d]);
+           },
+           ht.up_class_off, up_order);
+    ht.up_level_off.assign(H + 1, 0);
+    for (int32_t h = 0; h <= H; ++h) ht.up_level_off[h] = ht.up_class_off[h * kDegreeClasses];
     bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 

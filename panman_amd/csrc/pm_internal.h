@@ -28,6 +28,8 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
 constexpr int kClasses = 3;
+constexpr int kDegreeClasses = 4;
+inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
 
@@ -53,6 +55,8 @@ struct HostTree {
     std::vector<int32_t> internal_id;     // [I]
     std::vector<int32_t> leaf_id;         // [L]
     std::vector<int32_t> up_level_off;    // [H+1] offsets into up_order (level 0 = height 1)
+    std::vector<int32_t> up_class_off;    // [4H+1] within a level, nodes by out-degree class
+                                          // (<=3, <=15, <=255, more): Sankoff counter widths
     std::vector<int32_t> down_level_off;  // [D+1] offsets into down_order (level 0 = root)
     std::vector<int32_t> leaf_level_off;  // [D+1] offsets into leaf_down by depth
     std::vector<int32_t> child_off;       // dense CSR (host copy)

@@ -1,6 +1,160 @@
-// pm_sankoff.hip -- placeholder until the Sankoff kernels land: the product fails loudly.
-#include "pm_internal.h"
+// pm_sankoff.hip -- unit-cost Sankoff over the 16 codes for every column at once (gfx950).
+//
+// Restates src/fitchSankoff.cpp:359-405 (forward), :487-531 (backward), :676-703
+// (assignment), as driven by the low-mem MSA driver (src/panman.cpp:1568-1613).
+//
+// Exact compression of the reference's 16 x int32 cost vectors: with unit costs a child
+// contributes  min_k((i != k) + c[k]) = min(c) + [i not optimal in c]  to its parent, and
+// the backward argmin given parent state s only asks whether s is optimal, whether s is
+// exactly one above optimal, and which codes are optimal.  So a node keeps two 16-bit sets
+// per site: Z0 = optimal codes, Z1 = codes one above optimal (INF <=> Z0 == 0).  Forward:
+// count, per code, the finite children that hold it optimal (bit-sliced counters, B bits
+// per code); Z0 = codes of maximum count, Z1 = codes of maximum - 1.  B is chosen per
+// node by out-degree class so binary nodes pay for 2-bit counters only.
+#include "pm_kernels.h"
 
 namespace pm {
-hipError_t launch_sankoff(pm_ctx*) { return hipErrorNotSupported; }
+namespace {
+
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    if (item >= a.count) return;
+    const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+
+    uint32_t cnt[16][B];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+#pragma unroll
+        for (int b = 0; b < B; ++b) cnt[v][b] = 0;
+    uint32_t finite = 0, z[16];
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        if (c >= 0) load_set16<8>(a.sets, c, a.tiles, tile, lane, z);   // child's Z0
+        else leaf_set16(a, -c - 1, word, z);                            // leaf: {code}, absent: INF
+        finite |= any_plane(z);   // an all-INF child adds nothing (:398-400)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            uint32_t x = z[v];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint32_t t = cnt[v][b] & x;
+                cnt[v][b] ^= x;
+                x = t;
+            }
+        }
+    }
+    // maximum count per site, most significant bit first
+    uint32_t cand[16], mx[B];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cand[v] = ~0u;
+#pragma unroll
+    for (int b = B - 1; b >= 0; --b) {
+        uint32_t hit = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) hit |= cand[v] & cnt[v][b];
+        mx[b] = hit;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) cand[v] &= cnt[v][b] | ~hit;
+    }
+    // max - 1 (max >= 1 wherever a child is finite)
+    uint32_t mm1[B], borrow = ~0u;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        mm1[b] = mx[b] ^ borrow;
+        borrow &= ~mx[b];
+    }
+    uint32_t z0[16], z1[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t eq = finite;
+#pragma unroll
+        for (int b = 0; b < B; ++b) eq &= ~(cnt[v][b] ^ mm1[b]);
+        z0[v] = cand[v] & finite;
+        z1[v] = eq;
+    }
+    store_set16<8>(a.sets, n, a.tiles, tile, lane, z0, 0);
+    store_set16<8>(a.sets, n, a.tiles, tile, lane, z1, 4);
+}
+
+}  // namespace
+
+hipError_t launch_sankoff(pm_ctx* c) {
+    const HostTree& ht = c->ht;
+    const DevTree& dt = c->dt;
+    const int32_t tiles = (c->words + kWave - 1) / kWave;
+    const int64_t wpad = (int64_t)tiles * kWave;
+    const int H = (int)ht.up_level_off.size() - 1;
+    for (int h = 0; h < H; ++h)
+        if (ht.up_class_off[h * kDegreeClasses + 4] > ht.up_class_off[h * kDegreeClasses + 3])
+            return hipErrorNotSupported;   // > 255 children: wider counters not built yet
+
+    UpArgs up{};
+    up.child_off = dt.child_off;
+    up.child_enc = dt.child_enc;
+    up.leaf_flag = c->leaf_flag;
+    up.leaf_planes = c->leaf_planes;
+    up.leaf_present = c->leaf_present;
+    up.sets = reinterpret_cast<uint4*>(c->sets);
+    up.forced = nullptr;   // Sankoff forces the root in the backward pass only
+    up.root_dense = dt.root_dense;
+    up.tiles = tiles;
+    up.wpad = wpad;
+    for (int h = 0; h < H; ++h) {
+        for (int k = 0; k < 3; ++k) {
+            const int32_t b = ht.up_class_off[h * kDegreeClasses + k];
+            const int32_t e = ht.up_class_off[h * kDegreeClasses + k + 1];
+            if (e == b) continue;
+            up.order = dt.up_order + b;
+            up.count = e - b;
+            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+            timer_begin(c, 0);
+            if (k == 0) hipLaunchKernelGGL(k_sankoff_up<2>, grid, dim3(kBlock), 0, c->stream, up);
+            else if (k == 1) hipLaunchKernelGGL(k_sankoff_up<4>, grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL(k_sankoff_up<8>, grid, dim3(kBlock), 0, c->stream, up);
+            timer_end(c, 0);
+        }
+    }
+
+    hipError_t err = hipMemsetAsync(c->shard_cnt, 0, sizeof(uint32_t) * kShards, c->stream);
+    if (err != hipSuccess) return err;
+    DownArgs dn{};
+    dn.child_off = dt.child_off;
+    dn.child_enc = dt.child_enc;
+    dn.parent_dense = dt.parent_dense;
+    dn.internal_id = dt.internal_id;
+    dn.leaf_id = dt.leaf_id;
+    dn.leaf_flag = c->leaf_flag;
+    dn.leaf_planes = c->leaf_planes;
+    dn.leaf_present = c->leaf_present;
+    dn.sets = reinterpret_cast<const uint4*>(c->sets);
+    dn.finals = c->finals;
+    dn.cons = c->cons;
+    dn.root_dense = dt.root_dense;
+    dn.tiles = tiles;
+    dn.wpad = wpad;
+    dn.words = c->words;
+    dn.sites = c->num_sites;
+    dn.recs = c->recs;
+    dn.shard_cap = c->shard_cap;
+    dn.shard_cnt = c->shard_cnt;
+    dn.root_code = c->root_code;
+    dn.forced = c->has_forced ? c->forced : nullptr;
+    const int D = (int)ht.down_level_off.size() - 1;
+    for (int d = 0; d < D; ++d) {
+        dn.order = dt.down_order + ht.down_level_off[d];
+        dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
+        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        timer_begin(c, 1);
+        hipLaunchKernelGGL(k_down<Mode::kSankoff>, grid, dim3(kBlock), 0, c->stream, dn);
+        timer_end(c, 1);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace pm

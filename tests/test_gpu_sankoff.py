@@ -1,0 +1,98 @@
+"""GPU parity for the Sankoff path (S1-S3 + M2): HIP kernels through the C-ABI vs the
+CPU oracle, bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import panman_amd
+from _trees import CODE, names_for, parse_newick, random_tree
+from test_gpu_fitch import _random_columns, _random_msa
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kats.json")
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = panman_amd.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("kat", [k for k in json.load(open(GOLDEN))["column"] if k["algo"] == "sankoff"],
+                         ids=lambda k: k["id"])
+def test_sankoff_kats_on_gpu(engine, kat):
+    names, off, idx, root = parse_newick(kat["newick"])
+    vals = dict(kv.split("=") for kv in kat["leaves"].split(","))
+    node_row = np.full(len(names), -1, np.int32)
+    rows = []
+    for i, nm in enumerate(names):
+        if off[i] == off[i + 1] and nm in vals:
+            node_row[i] = len(rows)
+            rows.append([CODE[vals[nm]]])
+    engine.tree_upload(off, idx, root)
+    engine.leaves_upload(np.array(rows, np.uint8), node_row)
+    forced = None if kat["forced"] == -1 else np.array([kat["forced"]], np.uint8)
+    engine.sites_upload(np.array([kat["parent"]], np.uint8), forced)
+    engine.run(panman_amd.MODE_SANKOFF)
+    got = {names[m[0]]: [int(m[2]), "-ACMGRSVTWYHKDBN"[m[3]] if m[2] != 1 else "-"]
+           for m in engine.mutations()}
+    assert got == {k: list(v) for k, v in kat["expect"]["muts"].items()}
+    _, rootc = engine.site_results()
+    r = kat["expect"]["final"][names[root]]
+    assert rootc[0] == (255 if r == -1 else r)
+
+
+def _compare(engine, oracle, off, idx, root, codes, present, cons, forced):
+    n = off.shape[0] - 1
+    leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
+    node_row = np.full(n, -1, np.int32)
+    for r, lid in enumerate(leaf_ids):
+        if present[r]:
+            node_row[lid] = r
+    engine.tree_upload(off, idx, root)
+    engine.leaves_upload(codes, node_row)
+    engine.sites_upload(cons, forced)
+    engine.run(panman_amd.MODE_SANKOFF)
+    got = engine.mutations()
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, forced,
+                                            algo=1, threads=8, with_root=True)
+    assert got.shape == want.shape, (got.shape, want.shape)
+    assert (got == want).all()
+    score, rootc = engine.site_results()
+    assert (rootc == want_root).all()
+    assert (score == np.bincount(want[want[:, 0] != root][:, 1], minlength=codes.shape[1])).all()
+
+
+@pytest.mark.parametrize("sites", [1, 33, 700, 2049])
+def test_sankoff_random_binary_vs_oracle(engine, oracle, sites):
+    rng = np.random.default_rng(sites)
+    off, idx, root = panman_amd.random_join_tree(200, seed=sites)
+    codes, present = _random_columns(rng, 200, sites)
+    cons = rng.integers(0, 16, size=sites).astype(np.uint8)
+    _compare(engine, oracle, off, idx, root, codes, present, cons, None)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_sankoff_random_polytomy_vs_oracle(engine, oracle, seed):
+    rng = np.random.default_rng(200 + seed)
+    max_children = [3, 6, 15, 40, 300][seed]
+    off, idx, root = random_tree(400, rng, max_children=max_children, unary=0.1)
+    sites = 257
+    codes, present = _random_columns(rng, 400, sites, absent_frac=0.3)
+    cons = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=sites)
+    forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
+    _compare(engine, oracle, off, idx, root, codes, present, cons, forced)
+
+
+@pytest.mark.parametrize("with_ref", [False, True])
+def test_msa_driver_m2_vs_oracle(oracle, with_ref):
+    rng = np.random.default_rng(17 + with_ref)
+    nwk, msa = _random_msa(rng, 60, 150, with_ref)
+    ref = "ref" if with_ref else ""
+    want = oracle.msa_build(nwk, msa, ref, mode=1)
+    got = panman_amd.msa_build(nwk, msa, ref, panman_amd.MODE_SANKOFF)
+    assert not want.startswith("#error"), want
+    assert got == want
