@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--mode", choices=["fitch", "sankoff"], default="fitch")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -83,8 +84,10 @@ def main():
     score_loc = torch.zeros(s_local, dtype=torch.int32, device="cuda")
     root_loc = torch.zeros(s_local, dtype=torch.uint8, device="cuda")
 
+    mode = panman_amd.MODE_FITCH if args.mode == "fitch" else panman_amd.MODE_SANKOFF
+
     def step():
-        eng.run(panman_amd.MODE_FITCH)
+        eng.run(mode)
         eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
         if world > 1:
             gather_site_results(score_loc, root_loc, S)
@@ -125,11 +128,21 @@ def main():
     #   post-order  0.5 L (leaf codes) + 2 I (set write) + 2 (I-1) (set read by parent)
     #   pre-order   2 I (set read) + 0.5 I (final write) + 0.5 (N-1) (parent final read)
     #               + 0.5 L (leaf re-read) + 8 B per emitted mutation record
-    up_bytes = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1))
-    down_bytes = s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
+    if mode == panman_amd.MODE_FITCH:
+        up_bytes = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1))
+        down_bytes = s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
+        names = ("k_fitch_up", "k_down<Fitch>")
+        prof_names = {"k_fitch_up": "k_fitch_up", "k_down<Fitch>": "k_down"}
+    else:
+        # this layout's Sankoff state: Z0 + Z1 planes (4 B/site), parent reads Z0 (2 B/site);
+        # the survey's 16 x u16 cost-vector model (1.5 L + 97 I) is reported beside it
+        up_bytes = s_local * (0.5 * L + 4.0 * n_int + 2.0 * (n_int - 1))
+        down_bytes = s_local * (4.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
+        names = ("k_sankoff_up", "k_down<Sankoff>")
+        prof_names = {"k_sankoff_up": "k_sankoff_up", "k_down<Sankoff>": "k_down"}
     classes = {
-        "k_fitch_up": (ms[0] / args.steps, launches[0] / max(1, args.steps), up_bytes),
-        "k_fitch_down": (ms[1] / args.steps, launches[1] / max(1, args.steps), down_bytes),
+        names[0]: (ms[0] / args.steps, launches[0] / max(1, args.steps), up_bytes),
+        names[1]: (ms[1] / args.steps, launches[1] / max(1, args.steps), down_bytes),
     }
     dom = max(classes, key=lambda k: classes[k][0])
     dms, dl, dbytes = classes[dom]
@@ -139,7 +152,7 @@ def main():
     traffic = None
     if os.path.exists(args.traffic):
         try:
-            traffic = json.load(open(args.traffic)).get(dom, {}).get(f"{L}x{s_local}")
+            traffic = json.load(open(args.traffic)).get(prof_names[dom], {}).get(f"{args.mode}:{L}x{s_local}")
         except (OSError, ValueError):
             traffic = None
     per_launch = dbytes / dl if dl else 0.0
@@ -159,15 +172,17 @@ def main():
         "score_kernel_ms_per_step": round(ms[2] / args.steps, 3),
         "pipeline_effective_GBs": round((up_bytes + down_bytes) / (ms_step * 1e-3) / 1e9, 1),
     }
+    if mode == panman_amd.MODE_SANKOFF:
+        roofline["survey_contract_GBs"] = round(s_local * (1.5 * L + 97.0 * n_int) / (ms_step * 1e-3) / 1e9, 1)
 
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes)
+        cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode)
 
     if rank == 0:
         out = {
-            "metric": "Fitch-Sankoff site*node updates/sec (Fitch mode)",
+            "metric": f"Fitch-Sankoff site*node updates/sec ({args.mode} mode)",
             "value": value,
             "unit": "site*node updates/s",
             "n_gpus": world,
@@ -177,10 +192,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32 bit-planes (16-bit one-hot state sets)",
+            "dtype": "u32 bit-planes (16-bit one-hot state sets)" if mode == panman_amd.MODE_FITCH
+            else "u32 bit-planes (Z0/Z1 optimal-code sets, exact unit-cost Sankoff)",
             "data": "synthetic (seeded on-device tree-evolved columns, random-join tree)",
             "config": {
-                "workload": f"N* Fitch: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)",
+                "workload": f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)",
                 "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
                 "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
                 "mutations_total": muts_total,
@@ -194,7 +210,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, eng, off, idx, root, L, n_nodes):
+def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     """Reference-faithful CPU path (oracle: per-column unordered_map<string,int> +
     recursion, src/fitchSankoff.cpp:30-171) on a bounded column sample, plus a bit-exact
     check of the GPU kernels on the same sample at full tree size."""
@@ -208,7 +224,7 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes):
     node_row[:L] = np.arange(L, dtype=np.int32)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     o = orc.load()
-    secs, want = o.csr_columns(off, idx, root, names, codes, node_row, cons, None, algo=0, threads=threads)
+    secs, want = o.csr_columns(off, idx, root, names, codes, node_row, cons, None, algo=mode, threads=threads)
     cpu = {"value": ns * n_nodes / secs, "unit": "site*node updates/s", "cores": threads,
            "kind": "port",
            "sample": f"first {ns} of the same columns, {L} leaves x {ns} sites, {threads} threads "
@@ -218,7 +234,7 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes):
     e2.tree_upload(off, idx, root)
     e2.leaves_upload(codes, node_row)
     e2.sites_upload(cons)
-    e2.run(panman_amd.MODE_FITCH)
+    e2.run(mode)
     got = e2.mutations()
     e2.close()
     parity = {"sites": ns, "records": int(want.shape[0]),

@@ -137,6 +137,8 @@ int alloc_work(pm_ctx* c, int mode) {
 }
 
 int run_once(pm_ctx* c, int mode) {
+    if (mode == PM_MODE_SANKOFF && c->max_degree > 4095)
+        return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
     hipError_t e = mode == PM_MODE_FITCH ? launch_fitch(c) : launch_sankoff(c);
     if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
     e = launch_score(c);
@@ -363,6 +365,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
     c->dt = dt;
     c->ht = std::move(ht);
+    c->max_degree = 0;
+    for (int32_t d = 0; d < I; ++d) c->max_degree = std::max(c->max_degree, c->ht.child_off[d + 1] - c->ht.child_off[d]);
     c->has_tree = true;
     return PM_OK;
 }

@@ -78,6 +78,7 @@ struct pm_ctx {
     pm::HostTree ht;
     pm::DevTree dt;
     bool has_tree = false;
+    int32_t max_degree = 0;
 
     // column shard
     int64_t num_sites = 0;

@@ -90,9 +90,7 @@ hipError_t launch_sankoff(pm_ctx* c) {
     const int32_t tiles = (c->words + kWave - 1) / kWave;
     const int64_t wpad = (int64_t)tiles * kWave;
     const int H = (int)ht.up_level_off.size() - 1;
-    for (int h = 0; h < H; ++h)
-        if (ht.up_class_off[h * kDegreeClasses + 4] > ht.up_class_off[h * kDegreeClasses + 3])
-            return hipErrorNotSupported;   // > 255 children: wider counters not built yet
+    if (c->max_degree > 4095) return hipErrorNotSupported;   // 12-bit counters cover 4095 children
 
     UpArgs up{};
     up.child_off = dt.child_off;
@@ -106,7 +104,7 @@ hipError_t launch_sankoff(pm_ctx* c) {
     up.tiles = tiles;
     up.wpad = wpad;
     for (int h = 0; h < H; ++h) {
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < kDegreeClasses; ++k) {
             const int32_t b = ht.up_class_off[h * kDegreeClasses + k];
             const int32_t e = ht.up_class_off[h * kDegreeClasses + k + 1];
             if (e == b) continue;
@@ -116,7 +114,8 @@ hipError_t launch_sankoff(pm_ctx* c) {
             timer_begin(c, 0);
             if (k == 0) hipLaunchKernelGGL(k_sankoff_up<2>, grid, dim3(kBlock), 0, c->stream, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up<4>, grid, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_sankoff_up<8>, grid, dim3(kBlock), 0, c->stream, up);
+            else if (k == 2) hipLaunchKernelGGL(k_sankoff_up<8>, grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL(k_sankoff_up<12>, grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
     }

@@ -96,3 +96,34 @@ def test_msa_driver_m2_vs_oracle(oracle, with_ref):
     got = panman_amd.msa_build(nwk, msa, ref, panman_amd.MODE_SANKOFF)
     assert not want.startswith("#error"), want
     assert got == want
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+@pytest.mark.parametrize("width", [16, 300, 1500])
+def test_star_polytomy_vs_oracle(engine, oracle, mode, width):
+    """One node with `width` children (SARS-like trees have nodes with thousands)."""
+    rng = np.random.default_rng(width)
+    n = width + 2
+    # root(0) -> [star(1), leaf]; star -> width leaves
+    off = np.zeros(n + 1, np.int32)
+    off[1] = 2
+    off[2:] = 2 + width
+    idx = np.array([1, n - 1] + list(range(2, 2 + width)), np.int32)
+    leaves = width + 1
+    codes, present = _random_columns(rng, leaves, 97, absent_frac=0.1)
+    codes[rng.random(codes.shape) < 0.6] = 4   # a majority state
+    cons = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=97)
+    node_row = np.full(n, -1, np.int32)
+    leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
+    for r, lid in enumerate(leaf_ids):
+        if present[r]:
+            node_row[lid] = r
+    engine.tree_upload(off, idx, 0)
+    engine.leaves_upload(codes, node_row)
+    engine.sites_upload(cons)
+    engine.run(mode)
+    got = engine.mutations()
+    _, want, want_root = oracle.csr_columns(off, idx, 0, names_for(off), codes, node_row, cons, None,
+                                            algo=mode, threads=8, with_root=True)
+    assert got.shape == want.shape and (got == want).all()
+    assert (engine.site_results()[1] == want_root).all()
