@@ -103,8 +103,8 @@ def test_msa_driver_m2_vs_oracle(oracle, with_ref):
 def test_star_polytomy_vs_oracle(engine, oracle, mode, width):
     """One node with `width` children (SARS-like trees have nodes with thousands)."""
     rng = np.random.default_rng(width)
-    n = width + 2
-    # root(0) -> [star(1), leaf]; star -> width leaves
+    n = width + 3
+    # root(0) -> [star(1), leaf n-1]; star -> leaves 2..width+1
     off = np.zeros(n + 1, np.int32)
     off[1] = 2
     off[2:] = 2 + width
