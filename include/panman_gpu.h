@@ -42,6 +42,15 @@ extern "C" {
 
 #define PM_MODE_FITCH 0   /* F1-F3: 16-bit one-hot state sets, M1 semantics            */
 #define PM_MODE_SANKOFF 1 /* S1-S3: unit-cost Sankoff over 16 codes, M2 semantics      */
+/* Block-level parsimony (columns = blocks; codes 0 block absent, 1 forward, 2 reverse):
+ * B1 Tree::blockFitch*New   src/fitchSankoff.cpp:224-308 (leaf not in the column: state 0)
+ * B2 Tree::blockSankoff*    src/fitchSankoff.cpp:707-818 (leaf not in the column: absent
+ *    block, cost {0, INF, INF}).  Root parent state = consensus code (0 in the PanGraph
+ *    driver, src/panman.cpp:906-909, :952-956); `forced` = defaultState of the backward
+ *    pass.  Records: PM_MUT_NI -> BlockMut(BI, inversion = code == 2), PM_MUT_ND ->
+ *    BlockMut(BD, false), PM_MUT_NS -> BlockMut(BD, inversion = true). */
+#define PM_MODE_BLOCK_FITCH 2
+#define PM_MODE_BLOCK_SANKOFF 3
 
 #define PM_MUT_NS 0 /* NucMutationType::NS  src/panman.hpp:48 */
 #define PM_MUT_ND 1 /* NucMutationType::ND  src/panman.hpp:50 */

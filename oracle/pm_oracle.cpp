@@ -833,7 +833,8 @@ char* oracle_column(const char* newick, const char* leaves, int algo, int forced
 //   row of leaf i, or -1 for a leaf absent from the alignment.
 //   cons: per-site consensus code; ref: per-site forced root code or NULL.
 //   algo 0 = Fitch (M1 semantics, ref -> refState=1<<code), 1 = Sankoff (M2 semantics,
-//   ref -> defaultState=code).
+//   ref -> defaultState=code), 2 = block Fitch, 3 = block Sankoff (codes 0 absent block,
+//   1 forward, 2 reverse; ref -> defaultValue; records carry (blockMutInfo, inversion)).
 //   Output: *out_recs = malloc'd uint32 quads (node, site, type, code), *out_n = count,
 //   sorted by (node, site).  Returns wall seconds of the column loop.
 double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* child_idx, int32_t root,
@@ -872,7 +873,7 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
                     const int r = st[ct.t.root->id];
                     out_root[s] = r ? (uint8_t)log2_state(r) : (uint8_t)255;
                 }
-            } else {
+            } else if (algo == 1) {
                 CostMap costs;
                 StateMap st;
                 for (auto& pr : present) {
@@ -887,13 +888,46 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
                     const int r = st[ct.t.root->id];
                     out_root[s] = r >= 0 ? (uint8_t)r : (uint8_t)255;
                 }
+            } else if (algo == 2) {
+                // block Fitch (B1), driven like src/panman.cpp:873-911
+                StateMap st;
+                BlockMutMap bm;
+                for (auto& pr : present)
+                    st[ct.by_index[pr.first]->id] = 1 << leaf_codes[(int64_t)pr.second * row_stride + s];
+                block_fitch_up(ct.t.root, st);
+                block_fitch_down(ct.t.root, ct.t.root, st, 1 << cons[s], ref ? 1 << ref[s] : kNoDefault);
+                block_fitch_assign(ct.t.root, st, bm, 1 << cons[s]);
+                for (auto& m : bm) muts[m.first] = {m.second.first, m.second.second ? '1' : '0'};
+                if (out_root) {
+                    const int r = st[ct.t.root->id];
+                    out_root[s] = r ? (uint8_t)log2_state(r) : (uint8_t)255;
+                }
+            } else {
+                // block Sankoff (B2), driven like src/panman.cpp:912-960
+                CostMap costs;
+                StateMap st;
+                BlockMutMap bm;
+                for (auto& pr : present) {
+                    std::vector<int> v(3, kSankoffInf);
+                    v[leaf_codes[(int64_t)pr.second * row_stride + s]] = 0;
+                    costs[ct.by_index[pr.first]->id] = v;
+                }
+                block_sankoff_up(ct.t.root, costs);
+                block_sankoff_down(ct.t.root, ct.t.root, costs, st, cons[s], ref ? (int)ref[s] : kNoDefault);
+                block_sankoff_assign(ct.t.root, st, bm, cons[s]);
+                for (auto& m : bm) muts[m.first] = {m.second.first, m.second.second ? '1' : '0'};
+                if (out_root) {
+                    const int r = st[ct.t.root->id];
+                    out_root[s] = r >= 0 ? (uint8_t)r : (uint8_t)255;
+                }
             }
             for (auto& m : muts) {
                 auto& o = parts[w];
                 o.push_back((uint32_t)index_of[m.first]);
                 o.push_back((uint32_t)s);
                 o.push_back((uint32_t)m.second.first);
-                o.push_back((uint32_t)code_of(m.second.second));
+                // nucleotide: code of the char; block: inversion flag
+                o.push_back(algo >= 2 ? (uint32_t)(m.second.second == '1') : (uint32_t)code_of(m.second.second));
             }
         }
     };

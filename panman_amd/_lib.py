@@ -15,6 +15,8 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "panman_gpu.h")
 PM_OK = 0
 MODE_FITCH = 0
 MODE_SANKOFF = 1
+MODE_BLOCK_FITCH = 2
+MODE_BLOCK_SANKOFF = 3
 
 _lib = None
 

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_site_score(const pm_mut* recs, const
 
 }  // namespace
 
-hipError_t launch_fitch(pm_ctx* c) {
+hipError_t launch_fitch(pm_ctx* c, bool block) {
     const HostTree& ht = c->ht;
     const DevTree& dt = c->dt;
     const int32_t tiles = (c->words + kWave - 1) / kWave;
@@ -94,7 +94,8 @@ hipError_t launch_fitch(pm_ctx* c) {
     up.leaf_planes = c->leaf_planes;
     up.leaf_present = c->leaf_present;
     up.sets = reinterpret_cast<uint4*>(c->sets);
-    up.forced = c->has_forced ? c->forced : nullptr;
+    up.forced = (c->has_forced && !block) ? c->forced : nullptr;   // refState (M1); blocks force in backward
+    up.absent_code0 = false;
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
@@ -131,14 +132,16 @@ hipError_t launch_fitch(pm_ctx* c) {
     dn.shard_cap = c->shard_cap;
     dn.shard_cnt = c->shard_cnt;
     dn.root_code = c->root_code;
-    dn.forced = nullptr;
+    dn.forced = (c->has_forced && block) ? c->forced : nullptr;
+    dn.absent_code0 = false;
     const int D = (int)ht.down_level_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.order = dt.down_order + ht.down_level_off[d];
         dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
-        hipLaunchKernelGGL(k_down<Mode::kFitch>, grid, dim3(kBlock), 0, c->stream, dn);
+        if (block) hipLaunchKernelGGL(k_down<Mode::kBlockFitch>, grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL(k_down<Mode::kFitch>, grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
     return hipGetLastError();

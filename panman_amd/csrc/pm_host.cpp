@@ -107,7 +107,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
 // that pm_mutation_count grows on overflow.
 int alloc_work(pm_ctx* c, int mode) {
     const int64_t wpad = wpad_of(c);
-    const size_t planes = mode == PM_MODE_FITCH ? 16 : 32;
+    const size_t planes = (mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH) ? 16 : 32;
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
     const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
     hipError_t e;
@@ -137,9 +137,11 @@ int alloc_work(pm_ctx* c, int mode) {
 }
 
 int run_once(pm_ctx* c, int mode) {
-    if (mode == PM_MODE_SANKOFF && c->max_degree > 4095)
+    const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
+    const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
+    if (sankoff && c->max_degree > 4095)
         return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
-    hipError_t e = mode == PM_MODE_FITCH ? launch_fitch(c) : launch_sankoff(c);
+    hipError_t e = sankoff ? launch_sankoff(c, block) : launch_fitch(c, block);
     if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
     e = launch_score(c);
     if (e != hipSuccess) return hip_fail(c, e, "score launch");
@@ -443,7 +445,7 @@ int pm_sites_upload(pm_ctx* c, const uint8_t* consensus4, const uint8_t* forced4
 
 int pm_run(pm_ctx* c, int mode) {
     if (!c) return PM_ERR_ARG;
-    if (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF) return fail(c, PM_ERR_ARG, "unknown mode");
+    if (mode < PM_MODE_FITCH || mode > PM_MODE_BLOCK_SANKOFF) return fail(c, PM_ERR_ARG, "unknown mode");
     if (!c->has_tree || !c->has_leaves || !c->has_sites) return fail(c, PM_ERR_STATE, "tree, leaves and sites first");
     (void)hipSetDevice(c->device);
     int rc = alloc_work(c, mode);

@@ -120,8 +120,8 @@ void timer_begin(pm_ctx* c, int cls);
 void timer_end(pm_ctx* c, int cls);
 
 // kernel launchers (pm_fitch.hip / pm_sankoff.hip / pm_synth.hip)
-hipError_t launch_fitch(pm_ctx* c);
-hipError_t launch_sankoff(pm_ctx* c);
+hipError_t launch_fitch(pm_ctx* c, bool block);
+hipError_t launch_sankoff(pm_ctx* c, bool block);
 hipError_t launch_score(pm_ctx* c);
 hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_stride, const int32_t* d_row_of_leaf,
                              const uint8_t* d_present, int64_t present_stride);

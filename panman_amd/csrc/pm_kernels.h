@@ -10,7 +10,7 @@
 
 namespace pm {
 
-enum class Mode { kFitch, kSankoff };
+enum class Mode { kFitch, kSankoff, kBlockFitch };
 
 struct UpArgs {
     const int32_t* order;
@@ -25,6 +25,7 @@ struct UpArgs {
     int32_t root_dense;
     int32_t tiles;
     int64_t wpad;
+    bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
 };
 
 // Load 16 planes (quads q0..q0+3) of a record of Q quads.
@@ -57,11 +58,13 @@ __device__ __forceinline__ void leaf_set16(const Args& a, int32_t leaf, int64_t 
     if (flag == kLeafAbsent) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) s[v] = 0;
+        if (a.absent_code0) s[0] = ~0u;
         return;
     }
     const uint4 L = a.leaf_planes[(size_t)leaf * a.wpad + word];
     const uint32_t m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
     onehot_from_code(L.x, L.y, L.z, L.w, m, s);
+    if (a.absent_code0) s[0] |= ~m;
 }
 
 struct DownArgs {
@@ -87,7 +90,8 @@ struct DownArgs {
     int64_t shard_cap;
     uint32_t* shard_cnt;
     uint8_t* root_code;
-    const uint4* forced;   // Sankoff defaultState per site (nullable)
+    const uint4* forced;   // Sankoff / block defaultState per site (nullable)
+    bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
 };
 
 __device__ __forceinline__ uint32_t valid_mask(const DownArgs& a, int64_t word) {
@@ -100,10 +104,21 @@ __device__ __forceinline__ uint32_t valid_mask(const DownArgs& a, int64_t word) 
 __device__ __forceinline__ uint32_t leaf_diff(const DownArgs& a, int32_t leaf, int64_t word, uint32_t valid,
                                               const uint32_t* F, uint4& L) {
     const uint8_t flag = a.leaf_flag[leaf];
-    if (flag == kLeafAbsent) return 0u;
+    if (flag == kLeafAbsent) {
+        if (!a.absent_code0) return 0u;
+        L = make_uint4(0, 0, 0, 0);
+        return valid & (F[0] | F[1] | F[2] | F[3]);
+    }
     L = a.leaf_planes[(size_t)leaf * a.wpad + word];
     uint32_t m = valid;
-    if (flag == kLeafPartial) m &= a.leaf_present[(size_t)leaf * a.wpad + word];
+    if (flag == kLeafPartial) {
+        const uint32_t p = a.leaf_present[(size_t)leaf * a.wpad + word];
+        if (a.absent_code0) {   // missing sites are state 0
+            L.x &= p; L.y &= p; L.z &= p; L.w &= p;
+        } else {
+            m &= p;
+        }
+    }
     return m & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
 }
 
@@ -154,16 +169,22 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     }
     onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
     uint32_t pres;
-    if constexpr (M == Mode::kFitch) {
+    if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
         pres = any_plane(own);   // state 0: subtree absent, skipped (:101-103, :136-138)
         lowest_code(own, fin);
-        if (!is_root) {
+        const bool generic = !is_root || M == Mode::kBlockFitch;   // block root: parent & own rule (:249-264)
+        if (generic) {
             // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:115-123)
             uint32_t hit = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) hit |= P[v] & own[v];
 #pragma unroll
             for (int v = 0; v < 16; ++v) fin[v] = (P[v] & hit) | (fin[v] & ~hit);
+        }
+        if (M == Mode::kBlockFitch && is_root && a.forced) {   // defaultValue (:249-250)
+            const uint4 f = a.forced[word];
+            onehot_from_code(f.x, f.y, f.z, f.w, ~0u, fin);
+            pres = ~0u;
         }
     } else {
         if (is_root) {

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
 
 }  // namespace
 
-hipError_t launch_sankoff(pm_ctx* c) {
+hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const HostTree& ht = c->ht;
     const DevTree& dt = c->dt;
     const int32_t tiles = (c->words + kWave - 1) / kWave;
@@ -100,6 +100,7 @@ hipError_t launch_sankoff(pm_ctx* c) {
     up.leaf_present = c->leaf_present;
     up.sets = reinterpret_cast<uint4*>(c->sets);
     up.forced = nullptr;   // Sankoff forces the root in the backward pass only
+    up.absent_code0 = block;
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
@@ -144,6 +145,7 @@ hipError_t launch_sankoff(pm_ctx* c) {
     dn.shard_cnt = c->shard_cnt;
     dn.root_code = c->root_code;
     dn.forced = c->has_forced ? c->forced : nullptr;
+    dn.absent_code0 = block;
     const int D = (int)ht.down_level_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.order = dt.down_order + ht.down_level_off[d];
