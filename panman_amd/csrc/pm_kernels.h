@@ -151,7 +151,7 @@ __device__ __forceinline__ uint32_t emit(pm_mut* out, int64_t pos, int64_t cap, 
 // parent code 0 -> NI, child code 0 -> ND, else NS.
 template <Mode M>
 __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
-    constexpr int Q = M == Mode::kFitch ? 4 : 8;
+    constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;   // whole wave leaves together
