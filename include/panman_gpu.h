@@ -121,7 +121,7 @@ int pm_site_results(pm_ctx* ctx, int32_t* score, uint8_t* root_code);
  * collective can gather them without a host round trip. */
 int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_device);
 /* Accumulated device milliseconds and launch counts per kernel class since the last
- * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram. */
+ * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram, 3 replay. */
 int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
 
 /* ---- column drivers ------------------------------------------------------------------ */
@@ -135,6 +135,56 @@ int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
  * or "#error\t<message>\n" where the reference would exit or has undefined behaviour. */
 char* pm_msa_build(const char* newick, const char* msa_text, const char* reference, int mode, int device);
 void pm_free(void* p);
+
+/* ---- root-to-leaf mutation replay (FASTA extraction) ---------------------------------- */
+/* PanMAT fields used by printFASTAUltraFast (src/panman.hpp:520-543 Block / GapList,
+ * :429-517 BlockMut, :75-313 NucMut, Tree::circularSequences / rotationIndexes /
+ * sequenceInverted).  Per-node lists are CSR in list order; arrays are host memory. */
+typedef struct pm_panmat {
+    int32_t num_nodes;
+    int32_t root;
+    const int32_t* child_offsets;    /* [num_nodes + 1] */
+    const int32_t* child_index;
+    const char* names;               /* num_nodes NUL-terminated identifiers, back to back */
+    int32_t num_blocks;
+    const int32_t* block_primary;    /* [num_blocks] primaryBlockId */
+    const int64_t* block_seq_offsets;/* [num_blocks + 1] into block_seq */
+    const uint32_t* block_seq;       /* consensusSeq: 8 codes per word, MSB first, code 0 ends */
+    int32_t num_gaps;
+    const int32_t* gap_primary;      /* [num_gaps] */
+    const int64_t* gap_offsets;      /* [num_gaps + 1] into gap_position / gap_length */
+    const uint32_t* gap_position;
+    const uint32_t* gap_length;
+    const int64_t* block_mut_offsets;/* [num_nodes + 1] */
+    const int32_t* block_mut_primary;
+    const uint8_t* block_mut_info;   /* 1 = insertion (BI), 0 = deletion / inversion */
+    const uint8_t* block_mut_inversion;
+    const int64_t* nuc_mut_offsets;  /* [num_nodes + 1] */
+    const int32_t* nuc_mut_primary;
+    const int32_t* nuc_mut_secondary;
+    const int32_t* nuc_mut_position;
+    const int32_t* nuc_mut_gap_position; /* -1 = main position */
+    const uint8_t* nuc_mut_info;     /* (length << 4) | type */
+    const uint32_t* nuc_mut_nucs;    /* code i at bits 4 * (5 - i) */
+    const int32_t* circular_offset;  /* nullable [num_nodes]; < 0 = not circular */
+    const int32_t* rotation_index;   /* nullable [num_nodes] */
+    const uint8_t* sequence_inverted;/* nullable [num_nodes] */
+} pm_panmat;
+
+/* Drop-in for Tree::printFASTAUltraFast(fout, aligned) (src/fasta.cpp:1981-2099): one
+ * record per leaf, ">name\n" + 70-column lines + "\n", leaves in node-id order (the
+ * reference's order is TBB-scheduled).  `*text` is malloc'd (release with pm_free).
+ * Replay runs on the GPU (consensus expansion + path mutations per leaf); block order,
+ * strands, rotation, circular offset and line wrapping are applied by the host formatter. */
+int pm_fasta(pm_ctx* ctx, const pm_panmat* panmat, int aligned, char** text, int64_t* length);
+/* The same in stages: prepare (host flattening + upload), run (GPU replay, async on the
+ * ctx stream; profiling class 3), format (download + text). */
+int pm_replay_prepare(pm_ctx* ctx, const pm_panmat* panmat);
+int pm_replay_run(pm_ctx* ctx);
+int pm_replay_format(pm_ctx* ctx, int aligned, char** text, int64_t* length);
+/* Canonical aligned columns per leaf of the prepared PanMAT (gap slots before each main
+ * position, block sentinels included) and the number of leaves. */
+int pm_replay_shape(pm_ctx* ctx, int64_t* leaves, int64_t* columns, int64_t* edits);
 
 /* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
 /* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes

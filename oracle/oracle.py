@@ -34,6 +34,8 @@ def load() -> "Oracle":
             C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_char_p,
             C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
             C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
+        lib.oracle_fasta.restype = C.c_void_p
+        lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int]
         _lib = lib
     return Oracle(_lib)
 
@@ -56,6 +58,13 @@ class Oracle:
         """M1 (mode 0, Fitch) / M2 (mode 1, low-mem Sankoff) canonical dump."""
         p = self.lib.oracle_msa_build(newick.encode(), msa_text.encode(), reference.encode(),
                                       mode, threads)
+        return _take_string(self.lib, p)
+
+    def fasta(self, panmat, aligned: bool) -> str:
+        """printFASTAUltraFast records of every leaf, sorted by name (panman_amd.panmat.PanMAT)."""
+        st, keep = panmat.as_struct()
+        p = self.lib.oracle_fasta(C.byref(st), int(aligned))
+        del keep
         return _take_string(self.lib, p)
 
     def column(self, newick: str, leaves: str, algo: str, forced: int, parent: int) -> dict:

@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <set>
 #include <sstream>
 #include <stack>
@@ -723,6 +724,178 @@ void csr_to_tree(int32_t n, const int32_t* child_off, const int32_t* child_idx, 
 
 }  // namespace
 
+// ------------------------------------------------------------- R1-R3 replay ----
+// Restatement of Tree::printFASTAUltraFast (src/fasta.cpp:1981-2099) with
+// getNodesFromTipToRoot (:1753-1764), getBlockSequence (:1766-1787),
+// printFASTAUltraFastHelper (:1789-1979) and printSequenceLinesNew (:155-254).
+
+struct RBlockMut { int32_t primary; int32_t secondary; bool info; bool inversion; };
+struct RNucMut { int32_t pos; int32_t gap; int32_t primary; int32_t secondary; uint8_t info; uint32_t nucs;
+                 int length() const { return info >> 4; }
+                 uint32_t type() const { return info & 0x7; }
+                 int code(int i) const { return (nucs >> (4 * (5 - i))) & 0xF; } };
+struct RNode { std::string id; RNode* parent = nullptr; std::vector<RNode*> children;
+               std::vector<RBlockMut> bmuts; std::vector<RNucMut> nmuts; };
+struct RBlock { int32_t primary; std::vector<uint32_t> seq; };
+struct RGap { int32_t primary; std::vector<uint32_t> pos, len; };
+using Seq = std::vector<std::vector<std::pair<char, std::vector<char>>>>;
+
+struct RTree {
+    std::vector<std::unique_ptr<RNode>> nodes;
+    std::map<std::string, RNode*> all;
+    std::vector<RBlock> blocks;
+    std::vector<RGap> gaps;
+    std::unordered_map<std::string, int> circular, rotation;
+    std::unordered_map<std::string, bool> inverted;
+};
+
+std::string print_lines(const Seq& seq, std::unordered_map<int, int>& block_len, const std::vector<bool>& exists,
+                        const std::vector<bool>& strand, size_t width, bool aligned, int offset) {
+    std::string line;
+    for (size_t i = 0; i < exists.size(); ++i) {
+        if (exists[i]) {
+            if (strand[i]) {
+                for (size_t j = 0; j < seq[i].size(); ++j) {
+                    for (char g : seq[i][j].second) {
+                        if (g != '-') line += g;
+                        else if (aligned) line += '-';
+                    }
+                    const char m = seq[i][j].first;
+                    if (m != '-' && m != 'x') line += m;
+                    else if (aligned && m != 'x') line += '-';
+                }
+            } else {
+                for (size_t j = seq[i].size(); j-- > 0;) {
+                    const char m = seq[i][j].first;
+                    if (m != '-' && m != 'x') line += complement_of(m);
+                    else if (aligned && m != 'x') line += '-';
+                    const auto& g = seq[i][j].second;
+                    for (size_t k = g.size(); k-- > 0;) {
+                        if (g[k] != '-') line += complement_of(g[k]);
+                        else if (aligned) line += '-';
+                    }
+                }
+            }
+        } else if (aligned) {
+            line.append((size_t)block_len[(int)i], '-');   // indexed by print position (:207-210)
+        }
+    }
+    size_t start = 0;
+    if (offset != 0) {
+        for (size_t i = 0; i < line.size(); ++i) {
+            if (line[i] != '-') {
+                if (start == (size_t)offset) { start = i; break; }
+                ++start;
+            }
+        }
+    }
+    std::string out;
+    size_t col = 0;
+    auto put = [&](char ch) {
+        out += ch;
+        if (++col == width) { out += '\n'; col = 0; }
+    };
+    for (size_t i = start; i < line.size(); ++i) put(line[i]);
+    for (size_t i = 0; i < start; ++i) put(line[i]);
+    return out;
+}
+
+std::string leaf_record(RTree& t, RNode* leaf, bool aligned) {
+    std::vector<RNode*> path;
+    for (RNode* n = leaf; n; n = n->parent) path.push_back(n);
+    std::reverse(path.begin(), path.end());
+    const size_t nb = t.blocks.size() + 1;
+    std::vector<bool> present(nb, false);
+    for (RNode* n : path)
+        for (auto& m : n->bmuts) {
+            if (m.info) present[m.primary] = true;
+            else if (!m.inversion) present[m.primary] = false;
+        }
+    std::unordered_map<int, int> block_len;
+    Seq seq(nb);
+    std::vector<bool> exists(nb, false), strand(nb, true);
+    int32_t max_id = 0;
+    for (auto& b : t.blocks) {
+        block_len[b.primary] = 0;
+        max_id = std::max(max_id, b.primary);
+        int len = 0;
+        bool end = false;
+        for (size_t j = 0; j < b.seq.size() && !end; ++j)
+            for (int k = 0; k < 8; ++k) {
+                const int code = (b.seq[j] >> (4 * (7 - k))) & 15;
+                if (code == 0) { end = true; break; }
+                if (present[b.primary]) seq[b.primary].push_back({char_of(code), {}});
+                ++len;
+            }
+        if (present[b.primary]) seq[b.primary].push_back({'x', {}});
+        else block_len[b.primary] += len;
+    }
+    seq.resize(max_id + 1);
+    exists.resize(max_id + 1);
+    strand.resize(max_id + 1);
+    for (auto& g : t.gaps) {
+        if (present[g.primary]) {
+            for (size_t j = 0; j < g.pos.size(); ++j) seq[g.primary][g.pos[j]].second.resize(g.len[j], '-');
+        } else {
+            int len = 0;
+            for (auto l : g.len) len += (int)l;
+            block_len[g.primary] += len;
+        }
+    }
+    for (RNode* n : path) {
+        for (auto& m : n->bmuts) {
+            if (!present[m.primary]) continue;
+            if (m.info) { exists[m.primary] = true; strand[m.primary] = !m.inversion; }
+            else if (m.inversion) { strand[m.primary] = !strand[m.primary]; }
+            else { exists[m.primary] = false; strand[m.primary] = true; }
+        }
+        for (auto& m : n->nmuts) {
+            if (!present[m.primary]) continue;
+            const uint32_t type = m.type();
+            auto& blk = seq[m.primary];
+            if (type < 3) {
+                for (int j = 0; j < m.length(); ++j) {
+                    const char v = type == ND ? '-' : char_of(m.code(j));   // NS / NI write the code
+                    if (m.gap != -1) blk[m.pos].second[m.gap + j] = v;
+                    else blk[m.pos + j].first = v;
+                }
+            } else if (type <= 5) {
+                const char v = type == 5 ? '-' : char_of(m.code(0));
+                if (m.gap != -1) blk[m.pos].second[m.gap] = v;
+                else blk[m.pos].first = v;
+            }
+        }
+    }
+    int offset = 0;
+    if (!aligned) {
+        auto it = t.circular.find(leaf->id);
+        if (it != t.circular.end()) offset = it->second;
+    }
+    auto rit = t.rotation.find(leaf->id);
+    if (rit != t.rotation.end() && rit->second != 0) {
+        int ctr = -1;
+        size_t at = 0;
+        for (size_t i = 0; i < exists.size(); ++i) {
+            if (exists[i]) ++ctr;
+            if (ctr == rit->second) { at = i; break; }
+        }
+        std::rotate(seq.begin(), seq.begin() + at, seq.end());
+        std::vector<bool> e2(exists), s2(strand);
+        std::rotate(e2.begin(), e2.begin() + at, e2.end());
+        std::rotate(s2.begin(), s2.begin() + at, s2.end());
+        exists = e2;
+        strand = s2;
+    }
+    auto iit = t.inverted.find(leaf->id);
+    if (iit != t.inverted.end() && iit->second) {
+        std::reverse(seq.begin(), seq.end());
+        std::vector<bool> e2(exists.rbegin(), exists.rend()), s2(strand.rbegin(), strand.rend());
+        exists = e2;
+        strand = s2;
+    }
+    return ">" + leaf->id + "\n" + print_lines(seq, block_len, exists, strand, 70, aligned, offset) + "\n";
+}
+
 // ===================================================================== C API ==
 extern "C" {
 
@@ -947,6 +1120,82 @@ double oracle_csr_columns(int32_t n, const int32_t* child_off, const int32_t* ch
     *out_recs = (uint32_t*)std::malloc(sizeof(uint32_t) * 4 * (all.size() + 1));
     for (size_t i = 0; i < all.size(); ++i) std::memcpy(*out_recs + 4 * i, all[i].data(), 16);
     return secs;
+}
+
+// PanMAT description shared with the product's pm_panmat (same field order / types).
+struct OraclePanmat {
+    int32_t num_nodes;
+    int32_t root;
+    const int32_t* child_offsets;
+    const int32_t* child_index;
+    const char* names;                 // num_nodes NUL-terminated strings back to back
+    int32_t num_blocks;
+    const int32_t* block_primary;
+    const int64_t* block_seq_offsets;
+    const uint32_t* block_seq;
+    int32_t num_gaps;
+    const int32_t* gap_primary;
+    const int64_t* gap_offsets;
+    const uint32_t* gap_position;
+    const uint32_t* gap_length;
+    const int64_t* block_mut_offsets;
+    const int32_t* block_mut_primary;
+    const uint8_t* block_mut_info;
+    const uint8_t* block_mut_inversion;
+    const int64_t* nuc_mut_offsets;
+    const int32_t* nuc_mut_primary;
+    const int32_t* nuc_mut_secondary;
+    const int32_t* nuc_mut_position;
+    const int32_t* nuc_mut_gap_position;
+    const uint8_t* nuc_mut_info;
+    const uint32_t* nuc_mut_nucs;
+    const int32_t* circular_offset;    // nullable, [num_nodes]; < 0 = none
+    const int32_t* rotation_index;     // nullable
+    const uint8_t* sequence_inverted;  // nullable
+};
+
+// FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name.
+char* oracle_fasta(const OraclePanmat* p, int aligned) {
+    RTree t;
+    const char* nm = p->names;
+    for (int32_t i = 0; i < p->num_nodes; ++i) {
+        auto n = std::make_unique<RNode>();
+        n->id = nm;
+        nm += n->id.size() + 1;
+        t.nodes.push_back(std::move(n));
+    }
+    for (int32_t i = 0; i < p->num_nodes; ++i) {
+        RNode* n = t.nodes[i].get();
+        t.all[n->id] = n;
+        for (int32_t e = p->child_offsets[i]; e < p->child_offsets[i + 1]; ++e) {
+            RNode* c = t.nodes[p->child_index[e]].get();
+            c->parent = n;
+            n->children.push_back(c);
+        }
+        for (int64_t k = p->block_mut_offsets[i]; k < p->block_mut_offsets[i + 1]; ++k)
+            n->bmuts.push_back({p->block_mut_primary[k], -1, p->block_mut_info[k] != 0, p->block_mut_inversion[k] != 0});
+        for (int64_t k = p->nuc_mut_offsets[i]; k < p->nuc_mut_offsets[i + 1]; ++k)
+            n->nmuts.push_back({p->nuc_mut_position[k], p->nuc_mut_gap_position[k], p->nuc_mut_primary[k],
+                                p->nuc_mut_secondary[k], p->nuc_mut_info[k], p->nuc_mut_nucs[k]});
+        if (p->circular_offset && p->circular_offset[i] >= 0) t.circular[n->id] = p->circular_offset[i];
+        if (p->rotation_index && p->rotation_index[i] != 0) t.rotation[n->id] = p->rotation_index[i];
+        if (p->sequence_inverted && p->sequence_inverted[i]) t.inverted[n->id] = true;
+    }
+    for (int32_t b = 0; b < p->num_blocks; ++b)
+        t.blocks.push_back({p->block_primary[b], std::vector<uint32_t>(p->block_seq + p->block_seq_offsets[b],
+                                                                      p->block_seq + p->block_seq_offsets[b + 1])});
+    for (int32_t g = 0; g < p->num_gaps; ++g) {
+        RGap gl{p->gap_primary[g], {}, {}};
+        for (int64_t k = p->gap_offsets[g]; k < p->gap_offsets[g + 1]; ++k) {
+            gl.pos.push_back(p->gap_position[k]);
+            gl.len.push_back(p->gap_length[k]);
+        }
+        t.gaps.push_back(gl);
+    }
+    std::string out;
+    for (auto& kv : t.all)
+        if (kv.second->children.empty()) out += leaf_record(t, kv.second, aligned != 0);
+    return dup_string(out);
 }
 
 }  // extern "C"

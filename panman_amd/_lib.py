@@ -57,6 +57,11 @@ _SIGS = {
     "pm_consensus_fetch": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     "pm_msa_build": (C.c_void_p, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
     "pm_free": (None, [C.c_void_p]),
+    "pm_fasta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pm_replay_prepare": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pm_replay_run": (C.c_int, [C.c_void_p]),
+    "pm_replay_format": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 
 

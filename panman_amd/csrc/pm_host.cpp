@@ -223,6 +223,7 @@ void pm_destroy(pm_ctx* c) {
     free_work(c);
     free_columns(c);
     free_tree(c->dt);
+    free_replay(c);
     for (auto& v : c->timers)
         for (auto& t : v) {
             (void)hipEventDestroy(t.a);

@@ -27,7 +27,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
-constexpr int kClasses = 3;
+constexpr int kClasses = 4;
 constexpr int kDegreeClasses = 4;
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
@@ -69,6 +69,8 @@ struct Timer {
 
 }  // namespace pm
 
+namespace pm { struct ReplayState; }
+
 struct pm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -108,7 +110,10 @@ struct pm_ctx {
     // profiling
     bool profiling = false;
     std::vector<pm::Timer> timers[pm::kClasses];
-    size_t timers_used[pm::kClasses] = {0, 0, 0};
+    size_t timers_used[pm::kClasses] = {0, 0, 0, 0};
+
+    // replay (pm_replay.cpp)
+    pm::ReplayState* replay = nullptr;
 };
 
 namespace pm {
@@ -129,5 +134,25 @@ hipError_t launch_pack_sites(pm_ctx* c, const uint8_t* d_codes4, uint4* dst);
 hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
+void free_replay(pm_ctx* c);
+
+// replay kernels (pm_replay.hip)
+struct ReplayDev {
+    int32_t leaves = 0;
+    int64_t row_stride = 0;      // bytes per leaf row (multiple of 16)
+    int64_t columns = 0;
+    int32_t max_depth = 0;
+    int32_t presence_words = 0;  // u32 words of block-presence bits per leaf
+    char* rows = nullptr;        // [leaves][row_stride]
+    const char* cons_row = nullptr;   // [row_stride]
+    const int32_t* parent = nullptr;  // [N]
+    const int32_t* leaf_node = nullptr;   // [leaves]
+    const uint32_t* presence = nullptr;   // [leaves][presence_words]
+    const int64_t* edit_off = nullptr;    // [N+1]
+    const uint32_t* edit_col = nullptr;
+    const uint8_t* edit_chr = nullptr;
+    const int32_t* edit_blk = nullptr;
+};
+hipError_t launch_replay(pm_ctx* c, const ReplayDev& d);
 
 }  // namespace pm

@@ -1,0 +1,465 @@
+// pm_replay.cpp -- host side of FASTA replay: flatten a PanMAT for the GPU and format
+// the replayed rows as the reference prints them.
+//
+// Reference: Tree::printFASTAUltraFast (src/fasta.cpp:1981-2099), getBlockSequence
+// (:1766-1787), printFASTAUltraFastHelper (:1789-1979), printSequenceLinesNew (:155-254),
+// getComplementCharacter (src/panman.cpp:171-204).
+//
+// Canonical row of a leaf: blocks in primary-id order; inside a block, for each position
+// j = 0..len (len = the sentinel 'x'): its gap slots, then its main character.  The GPU
+// fills every leaf's row from the consensus and applies path mutations; the formatter
+// walks blocks in print order (rotation, inversion), forward or reverse-complemented,
+// drops '-' (unaligned) and the 'x' sentinels, rotates by the circular offset and wraps
+// at 70 columns.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pm_internal.h"
+
+namespace pm {
+
+struct ReplayState {
+    // topology
+    int32_t num_nodes = 0;
+    std::vector<std::string> names;
+    std::vector<int32_t> parent;
+    std::vector<int32_t> leaves;                 // leaf node ids, increasing
+    // blocks, indexed by primary id (0..max_id)
+    int32_t max_id = -1;
+    std::vector<uint8_t> is_block;               // [max_id+1]
+    std::vector<int64_t> col_start, width;       // canonical columns per block
+    std::vector<int64_t> absent_len;             // blockLengths when absent (len + sum of gap lengths)
+    int64_t columns = 0;
+    // per leaf (host, for the formatter)
+    std::vector<std::vector<uint8_t>> present;   // [leaf][max_id+1]
+    std::vector<std::vector<uint8_t>> exists, strand;
+    std::vector<int32_t> circular, rotation;
+    std::vector<uint8_t> inverted;
+    int64_t edits = 0;
+    // device
+    ReplayDev dev{};
+    char* d_rows = nullptr;
+    char* d_cons = nullptr;
+    int32_t* d_parent = nullptr;
+    int32_t* d_leaf = nullptr;
+    uint32_t* d_presence = nullptr;
+    int64_t* d_eoff = nullptr;
+    uint32_t* d_ecol = nullptr;
+    uint8_t* d_echr = nullptr;
+    int32_t* d_eblk = nullptr;
+    bool ran = false;
+};
+
+namespace {
+
+char nuc_char(int code) {
+    static const char tab[16] = {'-', 'A', 'C', 'M', 'G', 'R', 'S', 'V', 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
+    return tab[code & 15];
+}
+
+char complement(char c) {
+    switch (c) {
+        case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+        case 'R': return 'Y'; case 'Y': return 'R'; case 'S': return 'S'; case 'W': return 'W';
+        case 'K': return 'M'; case 'M': return 'K'; case 'B': return 'V'; case 'D': return 'H';
+        case 'H': return 'D'; case 'V': return 'B';
+        default: return 'N';
+    }
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+template <class T>
+hipError_t dput(T** dst, const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), sizeof(T) * std::max<size_t>(v.size(), 1));
+    if (e != hipSuccess || v.empty()) return e;
+    return hipMemcpyAsync(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
+}
+
+int prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
+    const int32_t N = p->num_nodes;
+    if (N < 1 || p->root < 0 || p->root >= N || !p->child_offsets || !p->names)
+        return fail(c, PM_ERR_ARG, "bad PanMAT topology");
+    r.num_nodes = N;
+    r.names.resize(N);
+    const char* nm = p->names;
+    for (int32_t i = 0; i < N; ++i) {
+        r.names[i] = nm;
+        nm += r.names[i].size() + 1;
+    }
+    r.parent.assign(N, -2);
+    r.parent[p->root] = -1;
+    for (int32_t i = 0; i < N; ++i)
+        for (int32_t e = p->child_offsets[i]; e < p->child_offsets[i + 1]; ++e) {
+            const int32_t ch = p->child_index[e];
+            if (ch < 0 || ch >= N || r.parent[ch] != -2) return fail(c, PM_ERR_ARG, "bad child index");
+            r.parent[ch] = i;
+        }
+    for (int32_t i = 0; i < N; ++i) {
+        if (r.parent[i] == -2) return fail(c, PM_ERR_ARG, "node unreachable from the root");
+        if (p->child_offsets[i] == p->child_offsets[i + 1]) r.leaves.push_back(i);
+    }
+
+    // ---- blocks (vector order defines blockLengths resets; ids must be unique)
+    const int32_t B = p->num_blocks;
+    for (int32_t b = 0; b < B; ++b) r.max_id = std::max(r.max_id, p->block_primary[b]);
+    if (B == 0) return fail(c, PM_ERR_ARG, "PanMAT has no blocks");
+    const int32_t M = r.max_id + 1;
+    r.is_block.assign(M, 0);
+    std::vector<int32_t> len(M, 0);
+    std::vector<std::vector<uint8_t>> codes(M);
+    for (int32_t b = 0; b < B; ++b) {
+        const int32_t id = p->block_primary[b];
+        if (id < 0 || r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "duplicate or negative primary block id");
+        r.is_block[id] = 1;
+        bool end = false;
+        for (int64_t w = p->block_seq_offsets[b]; w < p->block_seq_offsets[b + 1] && !end; ++w)
+            for (int k = 0; k < 8; ++k) {
+                const int code = (p->block_seq[w] >> (4 * (7 - k))) & 15;
+                if (code == 0) { end = true; break; }
+                codes[id].push_back((uint8_t)code);
+            }
+        len[id] = (int32_t)codes[id].size();
+    }
+    // gap slots: resize semantics (last entry wins) for present blocks; absent blocks
+    // accumulate every listed length (src/fasta.cpp:2067-2088)
+    std::vector<std::vector<int32_t>> slots(M);
+    std::vector<int64_t> gap_sum(M, 0);
+    for (int32_t id = 0; id < M; ++id)
+        if (r.is_block[id]) slots[id].assign(len[id] + 1, 0);
+    for (int32_t g = 0; g < p->num_gaps; ++g) {
+        const int32_t id = p->gap_primary[g];
+        if (id < 0 || id >= M || !r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "gap list for a missing block");
+        for (int64_t k = p->gap_offsets[g]; k < p->gap_offsets[g + 1]; ++k) {
+            const uint32_t pos = p->gap_position[k];
+            if (pos > (uint32_t)len[id]) return fail(c, PM_ERR_ARG, "gap position beyond the block");
+            slots[id][pos] = (int32_t)p->gap_length[k];
+            gap_sum[id] += p->gap_length[k];
+        }
+    }
+    r.col_start.assign(M, 0);
+    r.width.assign(M, 0);
+    r.absent_len.assign(M, 0);
+    std::vector<std::vector<int64_t>> main_col(M), gap_col(M);   // column of main j / first slot of j
+    std::string cons;
+    for (int32_t id = 0; id < M; ++id) {
+        r.col_start[id] = (int64_t)cons.size();
+        if (!r.is_block[id]) continue;
+        main_col[id].resize(len[id] + 1);
+        gap_col[id].resize(len[id] + 1);
+        for (int32_t j = 0; j <= len[id]; ++j) {
+            gap_col[id][j] = (int64_t)cons.size();
+            cons.append((size_t)slots[id][j], '-');
+            main_col[id][j] = (int64_t)cons.size();
+            cons += j < len[id] ? nuc_char(codes[id][j]) : 'x';
+        }
+        r.width[id] = (int64_t)cons.size() - r.col_start[id];
+        r.absent_len[id] = len[id] + gap_sum[id];
+    }
+    r.columns = (int64_t)cons.size();
+    if (r.columns >= ((int64_t)1 << 32)) return fail(c, PM_ERR_UNSUPPORTED, "more than 2^32 aligned columns");
+
+    // ---- per-node edits (column, char, block), last write per column within a node wins
+    std::vector<int64_t> eoff(N + 1, 0);
+    std::vector<uint32_t> ecol;
+    std::vector<uint8_t> echr;
+    std::vector<int32_t> eblk;
+    std::vector<std::pair<uint32_t, size_t>> tmp;
+    for (int32_t v = 0; v < N; ++v) {
+        const size_t first = ecol.size();
+        for (int64_t k = p->nuc_mut_offsets[v]; k < p->nuc_mut_offsets[v + 1]; ++k) {
+            const int32_t id = p->nuc_mut_primary[k];
+            const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
+            int32_t n = (int32_t)(info >> 4);
+            if (type > 5) continue;           // no-op types
+            if (type >= 3) n = 1;             // NSNPS / NSNPI / NSNPD: one code
+            if (id < 0 || id >= M || !r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "mutation on a missing block");
+            if (n > 6) return fail(c, PM_ERR_UNSUPPORTED, "nucleotide run longer than 6");
+            const int32_t pos = p->nuc_mut_position[k], gap = p->nuc_mut_gap_position[k];
+            for (int32_t j = 0; j < n; ++j) {
+                const int code = (p->nuc_mut_nucs[k] >> (4 * (5 - j))) & 15;
+                const bool del = type == 1 || type == 5;
+                int64_t col;
+                if (gap != -1) {
+                    if (pos < 0 || pos > len[id] || gap + j >= slots[id][pos] || gap < 0)
+                        return fail(c, PM_ERR_ARG, "gap-slot mutation outside the slot range");
+                    col = gap_col[id][pos] + gap + j;
+                } else {
+                    if (pos < 0 || pos + j > len[id]) return fail(c, PM_ERR_ARG, "mutation beyond the block");
+                    col = main_col[id][pos + j];   // pos + j == len rewrites the sentinel, as the reference does
+                }
+                ecol.push_back((uint32_t)col);
+                echr.push_back((uint8_t)(del ? '-' : nuc_char(code)));
+                eblk.push_back(id);
+            }
+        }
+        // dedup within the node: keep the last edit per column
+        tmp.clear();
+        for (size_t e = first; e < ecol.size(); ++e) tmp.emplace_back(ecol[e], e);
+        std::stable_sort(tmp.begin(), tmp.end(), [](auto& a, auto& b) { return a.first < b.first; });
+        std::vector<uint32_t> c2;
+        std::vector<uint8_t> h2;
+        std::vector<int32_t> b2;
+        for (size_t i = 0; i < tmp.size(); ++i) {
+            if (i + 1 < tmp.size() && tmp[i + 1].first == tmp[i].first) continue;
+            c2.push_back(ecol[tmp[i].second]);
+            h2.push_back(echr[tmp[i].second]);
+            b2.push_back(eblk[tmp[i].second]);
+        }
+        ecol.resize(first);
+        echr.resize(first);
+        eblk.resize(first);
+        ecol.insert(ecol.end(), c2.begin(), c2.end());
+        echr.insert(echr.end(), h2.begin(), h2.end());
+        eblk.insert(eblk.end(), b2.begin(), b2.end());
+        eoff[v + 1] = (int64_t)ecol.size();
+    }
+    r.edits = (int64_t)ecol.size();
+
+    // ---- per-leaf block state (getBlockSequence + the block-mutation pass of the helper)
+    const int32_t L = (int32_t)r.leaves.size();
+    const int32_t words = (M + 31) / 32;
+    std::vector<uint32_t> presence((size_t)L * words, 0);
+    r.present.assign(L, {});
+    r.exists.assign(L, {});
+    r.strand.assign(L, {});
+    int32_t max_depth = 0;
+    const int64_t nb_slots = (int64_t)B + 1;   // blockSequence has blocks.size()+1 entries
+    for (int32_t li = 0; li < L; ++li) {
+        std::vector<int32_t> path;
+        for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path.push_back(n);
+        std::reverse(path.begin(), path.end());
+        max_depth = std::max(max_depth, (int32_t)path.size());
+        std::vector<uint8_t> pres(std::max<int64_t>(M, nb_slots), 0), ex(M, 0), st(M, 1);
+        for (int32_t n : path)
+            for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
+                const int32_t id = p->block_mut_primary[k];
+                if (id < 0 || id >= (int32_t)pres.size()) return fail(c, PM_ERR_ARG, "block mutation id out of range");
+                if (p->block_mut_info[k]) pres[id] = 1;
+                else if (!p->block_mut_inversion[k]) pres[id] = 0;
+            }
+        for (int32_t n : path)
+            for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
+                const int32_t id = p->block_mut_primary[k];
+                if (id >= M || !pres[id]) continue;
+                if (p->block_mut_info[k]) { ex[id] = 1; st[id] = !p->block_mut_inversion[k]; }
+                else if (p->block_mut_inversion[k]) st[id] = !st[id];
+                else { ex[id] = 0; st[id] = 1; }
+            }
+        pres.resize(M);
+        for (int32_t id = 0; id < M; ++id)
+            if (pres[id]) presence[(size_t)li * words + id / 32] |= 1u << (id % 32);
+        r.present[li] = std::move(pres);
+        r.exists[li] = std::move(ex);
+        r.strand[li] = std::move(st);
+    }
+    r.circular.assign(L, -1);
+    r.rotation.assign(L, 0);
+    r.inverted.assign(L, 0);
+    for (int32_t li = 0; li < L; ++li) {
+        const int32_t v = r.leaves[li];
+        if (p->circular_offset) r.circular[li] = p->circular_offset[v];
+        if (p->rotation_index) r.rotation[li] = p->rotation_index[v];
+        if (p->sequence_inverted) r.inverted[li] = p->sequence_inverted[v];
+    }
+
+    // ---- device
+    const int64_t stride = (r.columns + 15) / 16 * 16;
+    std::vector<char> cons_row(stride, '-');
+    std::memcpy(cons_row.data(), cons.data(), cons.size());
+    hipError_t e;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&r.d_rows), (size_t)std::max<int64_t>(L, 1) * stride)) != hipSuccess)
+        return fail(c, PM_ERR_OOM, "replay rows");
+    if ((e = dput(&r.d_cons, cons_row, c->stream)) != hipSuccess || (e = dput(&r.d_parent, r.parent, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, presence, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_eoff, eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, ecol, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_echr, echr, c->stream)) != hipSuccess || (e = dput(&r.d_eblk, eblk, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(c, e, "replay upload");
+    ReplayDev& d = r.dev;
+    d.leaves = L;
+    d.row_stride = stride;
+    d.columns = r.columns;
+    d.max_depth = max_depth;
+    d.presence_words = words;
+    d.rows = r.d_rows;
+    d.cons_row = r.d_cons;
+    d.parent = r.d_parent;
+    d.leaf_node = r.d_leaf;
+    d.presence = r.d_presence;
+    d.edit_off = r.d_eoff;
+    d.edit_col = r.d_ecol;
+    d.edit_chr = r.d_echr;
+    d.edit_blk = r.d_eblk;
+    return PM_OK;
+}
+
+// printSequenceLinesNew for one leaf, from its replayed canonical row.
+void format_leaf(const ReplayState& r, int32_t li, const char* row, bool aligned, std::string& out) {
+    const int32_t M = r.max_id + 1;
+    std::vector<int32_t> order(M);
+    for (int32_t i = 0; i < M; ++i) order[i] = i;
+    const auto& ex = r.exists[li];
+    if (r.rotation[li] != 0) {   // rotate to the rotationIndexes-th existing block (:1950-1964)
+        int32_t ctr = -1, at = 0;
+        for (int32_t i = 0; i < M; ++i) {
+            if (ex[i]) ++ctr;
+            if (ctr == r.rotation[li]) { at = i; break; }
+        }
+        std::rotate(order.begin(), order.begin() + at, order.end());
+    }
+    if (r.inverted[li]) std::reverse(order.begin(), order.end());
+    std::string line;
+    for (int32_t i = 0; i < M; ++i) {
+        const int32_t id = order[i];
+        if (ex[id]) {
+            const char* seg = row + r.col_start[id];
+            const int64_t w = r.width[id];
+            if (r.strand[li][id]) {
+                for (int64_t k = 0; k < w; ++k) {
+                    const char ch = seg[k];
+                    if (ch == 'x') continue;
+                    if (ch != '-') line += ch;
+                    else if (aligned) line += '-';
+                }
+            } else {
+                for (int64_t k = w - 1; k >= 0; --k) {
+                    const char ch = seg[k];
+                    if (ch == 'x') continue;
+                    if (ch != '-') line += complement(ch);
+                    else if (aligned) line += '-';
+                }
+            }
+        } else if (aligned) {
+            // blockLengths is indexed by print position i, not by the block printed there
+            const int64_t dash = (r.is_block[i] && !r.present[li][i]) ? r.absent_len[i] : 0;
+            line.append((size_t)dash, '-');
+        }
+    }
+    size_t start = 0;
+    const int32_t offset = aligned ? 0 : std::max(0, r.circular[li]);
+    if (offset != 0) {
+        for (size_t i = 0; i < line.size(); ++i)
+            if (line[i] != '-') {
+                if (start == (size_t)offset) { start = i; break; }
+                ++start;
+            }
+    }
+    out += '>';
+    out += r.names[r.leaves[li]];
+    out += '\n';
+    size_t col = 0;
+    auto put = [&](char ch) {
+        out += ch;
+        if (++col == 70) { out += '\n'; col = 0; }
+    };
+    for (size_t i = start; i < line.size(); ++i) put(line[i]);
+    for (size_t i = 0; i < start; ++i) put(line[i]);
+    out += '\n';
+}
+
+}  // namespace
+
+void free_replay(pm_ctx* c) {
+    if (!c->replay) return;
+    ReplayState* r = c->replay;
+    dfree(r->d_rows);
+    dfree(r->d_cons);
+    dfree(r->d_parent);
+    dfree(r->d_leaf);
+    dfree(r->d_presence);
+    dfree(r->d_eoff);
+    dfree(r->d_ecol);
+    dfree(r->d_echr);
+    dfree(r->d_eblk);
+    delete r;
+    c->replay = nullptr;
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) {
+    if (!c || !p) return PM_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    free_replay(c);
+    c->replay = new ReplayState();
+    int rc = prepare(c, p, *c->replay);
+    if (rc != PM_OK) free_replay(c);
+    return rc;
+}
+
+int pm_replay_run(pm_ctx* c) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->replay) return fail(c, PM_ERR_STATE, "prepare a PanMAT first");
+    (void)hipSetDevice(c->device);
+    hipError_t e = launch_replay(c, c->replay->dev);
+    if (e == hipErrorNotSupported) return fail(c, PM_ERR_UNSUPPORTED, "tree deeper than 8192 nodes");
+    if (e != hipSuccess) return hip_fail(c, e, "replay launch");
+    c->replay->ran = true;
+    return PM_OK;
+}
+
+int pm_replay_shape(pm_ctx* c, int64_t* leaves, int64_t* columns, int64_t* edits) {
+    if (!c || !c->replay) return PM_ERR_ARG;
+    if (leaves) *leaves = (int64_t)c->replay->leaves.size();
+    if (columns) *columns = c->replay->columns;
+    if (edits) *edits = c->replay->edits;
+    return PM_OK;
+}
+
+int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
+    if (!c || !text || !length) return PM_ERR_ARG;
+    if (!c->replay || !c->replay->ran) return fail(c, PM_ERR_STATE, "run the replay first");
+    (void)hipSetDevice(c->device);
+    const ReplayState& r = *c->replay;
+    const int32_t L = (int32_t)r.leaves.size();
+    const int64_t stride = r.dev.row_stride;
+    std::vector<char> rows((size_t)L * stride);
+    hipError_t e = hipMemcpyAsync(rows.data(), r.d_rows, rows.size(), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "replay download");
+    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::string> parts(T);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t)
+        pool.emplace_back([&, t] {
+            const int32_t a = (int32_t)((int64_t)L * t / T), b = (int32_t)((int64_t)L * (t + 1) / T);
+            for (int32_t li = a; li < b; ++li) format_leaf(r, li, rows.data() + (size_t)li * stride, aligned != 0, parts[t]);
+        });
+    for (auto& th : pool) th.join();
+    size_t total = 0;
+    for (auto& s : parts) total += s.size();
+    char* out = static_cast<char*>(std::malloc(total + 1));
+    if (!out) return fail(c, PM_ERR_OOM, "FASTA text");
+    size_t at = 0;
+    for (auto& s : parts) {
+        std::memcpy(out + at, s.data(), s.size());
+        at += s.size();
+    }
+    out[total] = 0;
+    *text = out;
+    *length = (int64_t)total;
+    return PM_OK;
+}
+
+int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* length) {
+    int rc = pm_replay_prepare(c, p);
+    if (rc == PM_OK) rc = pm_replay_run(c);
+    if (rc == PM_OK) rc = pm_replay_format(c, aligned, text, length);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+"""In-memory PanMAT (the reference's Tree fields used by FASTA replay) as flat arrays,
+and its C view `pm_panmat` (include/panman_gpu.h).  Reference types: Block
+src/panman.hpp:520-534, GapList :537-543, BlockMut :429-517, NucMut :75-313, Tree
+circularSequences / rotationIndexes / sequenceInverted (src/panman.hpp:634-983)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+CODE = {c: i for i, c in enumerate("-ACMGRSVTWYHKDBN")}
+
+
+def encode_block(seq: str) -> list[int]:
+    """Block(primaryBlockId, seq): 8 codes per uint32, MSB nibble first (src/panman.cpp:246-257)."""
+    words = []
+    for i in range(0, len(seq), 8):
+        w = 0
+        for j, ch in enumerate(seq[i:i + 8]):
+            w ^= CODE.get(ch, 0) << (4 * (7 - j))
+        words.append(w)
+    return words
+
+
+class PanmatStruct(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_int32), ("root", C.c_int32),
+        ("child_offsets", C.c_void_p), ("child_index", C.c_void_p), ("names", C.c_char_p),
+        ("num_blocks", C.c_int32), ("block_primary", C.c_void_p), ("block_seq_offsets", C.c_void_p),
+        ("block_seq", C.c_void_p),
+        ("num_gaps", C.c_int32), ("gap_primary", C.c_void_p), ("gap_offsets", C.c_void_p),
+        ("gap_position", C.c_void_p), ("gap_length", C.c_void_p),
+        ("block_mut_offsets", C.c_void_p), ("block_mut_primary", C.c_void_p), ("block_mut_info", C.c_void_p),
+        ("block_mut_inversion", C.c_void_p),
+        ("nuc_mut_offsets", C.c_void_p), ("nuc_mut_primary", C.c_void_p), ("nuc_mut_secondary", C.c_void_p),
+        ("nuc_mut_position", C.c_void_p), ("nuc_mut_gap_position", C.c_void_p), ("nuc_mut_info", C.c_void_p),
+        ("nuc_mut_nucs", C.c_void_p),
+        ("circular_offset", C.c_void_p), ("rotation_index", C.c_void_p), ("sequence_inverted", C.c_void_p),
+    ]
+
+
+class PanMAT:
+    """Tree + blocks + gaps + per-node mutation lists, in list order."""
+
+    def __init__(self, names, child_offsets, child_index, root):
+        self.names = list(names)
+        self.child_offsets = np.ascontiguousarray(child_offsets, np.int32)
+        self.child_index = np.ascontiguousarray(child_index, np.int32)
+        self.root = int(root)
+        n = len(self.names)
+        self.blocks: list[tuple[int, list[int]]] = []
+        self.gaps: list[tuple[int, list[tuple[int, int]]]] = []
+        self.block_muts: list[list[tuple[int, int, int]]] = [[] for _ in range(n)]
+        self.nuc_muts: list[list[tuple[int, int, int, int, int, int]]] = [[] for _ in range(n)]
+        self.circular = np.full(n, -1, np.int32)
+        self.rotation = np.zeros(n, np.int32)
+        self.inverted = np.zeros(n, np.uint8)
+
+    @property
+    def num_nodes(self):
+        return len(self.names)
+
+    def index(self, name):
+        return self.names.index(name)
+
+    def add_block(self, primary: int, seq: str):
+        self.blocks.append((primary, encode_block(seq)))
+
+    def add_gaps(self, primary: int, slots: list[tuple[int, int]]):
+        self.gaps.append((primary, list(slots)))
+
+    def add_block_mut(self, node: int, primary: int, insertion: bool, inversion: bool):
+        self.block_muts[node].append((primary, int(insertion), int(inversion)))
+
+    def add_nuc_mut(self, node: int, primary: int, pos: int, gap: int, mtype: int, codes: list[int],
+                    secondary: int = -1):
+        info = (len(codes) << 4) + mtype
+        nucs = 0
+        for i, c in enumerate(codes):
+            nucs += c << (4 * (5 - i))
+        self.nuc_muts[node].append((primary, secondary, pos, gap, info, nucs))
+
+    def add_nuc_mut_raw(self, node: int, primary: int, pos: int, gap: int, info: int, nucs: int):
+        self.nuc_muts[node].append((primary, -1, pos, gap, info, nucs))
+
+    def leaves(self):
+        off = self.child_offsets
+        return [i for i in range(self.num_nodes) if off[i] == off[i + 1]]
+
+    def as_struct(self):
+        """Returns (PanmatStruct, keepalive) -- keep the second alive while the struct is used."""
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+            if a.size == 0:
+                a = np.zeros(1, dt)
+            keep.append(a)
+            return a.ctypes.data
+
+        blob = b"".join(n.encode() + b"\0" for n in self.names)
+        keep.append(blob)
+        seq_off = np.zeros(len(self.blocks) + 1, np.int64)
+        seq = []
+        for i, (_, w) in enumerate(self.blocks):
+            seq += w
+            seq_off[i + 1] = len(seq)
+        g_off = np.zeros(len(self.gaps) + 1, np.int64)
+        gpos, glen = [], []
+        for i, (_, slots) in enumerate(self.gaps):
+            for p, l in slots:
+                gpos.append(p)
+                glen.append(l)
+            g_off[i + 1] = len(gpos)
+        b_off = np.zeros(self.num_nodes + 1, np.int64)
+        bm = []
+        for i, lst in enumerate(self.block_muts):
+            bm += lst
+            b_off[i + 1] = len(bm)
+        n_off = np.zeros(self.num_nodes + 1, np.int64)
+        nm = []
+        for i, lst in enumerate(self.nuc_muts):
+            nm += lst
+            n_off[i + 1] = len(nm)
+        bm = np.array(bm, np.int64).reshape(-1, 3)
+        nm = np.array(nm, np.int64).reshape(-1, 6)
+        s = PanmatStruct(
+            self.num_nodes, self.root, arr(self.child_offsets, np.int32), arr(self.child_index, np.int32), blob,
+            len(self.blocks), arr([p for p, _ in self.blocks], np.int32), arr(seq_off, np.int64),
+            arr(seq, np.uint32),
+            len(self.gaps), arr([p for p, _ in self.gaps], np.int32), arr(g_off, np.int64), arr(gpos, np.uint32),
+            arr(glen, np.uint32),
+            arr(b_off, np.int64), arr(bm[:, 0], np.int32), arr(bm[:, 1], np.uint8), arr(bm[:, 2], np.uint8),
+            arr(n_off, np.int64), arr(nm[:, 0], np.int32), arr(nm[:, 1], np.int32), arr(nm[:, 2], np.int32),
+            arr(nm[:, 3], np.int32), arr(nm[:, 4], np.uint8), arr(nm[:, 5] & 0xFFFFFFFF, np.uint32),
+            arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8))
+        return s, keep
+
+
+def from_msa_dump(dump: str, names, child_offsets, child_index, root) -> PanMAT:
+    """PanMAT built by the MSA drivers (canonical dump of pm_msa_build / oracle_msa_build)."""
+    pm = PanMAT(names, child_offsets, child_index, root)
+    index = {n: i for i, n in enumerate(pm.names)}
+    for line in dump.splitlines():
+        f = line.split("\t")
+        if f[0] == "#error":
+            raise ValueError(f[1])
+        if f[0] == "#consensus":
+            pm.add_block(0, f[1])
+        elif f[0] == "#blockmut":
+            pm.add_block_mut(index[f[1]], int(f[2]), bool(int(f[4])), bool(int(f[5])))
+        else:
+            pm.add_nuc_mut_raw(index[f[0]], 0, int(f[1]), int(f[2]), int(f[3]), int(f[4], 16))
+    return pm
