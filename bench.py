@@ -41,7 +41,11 @@ def parse():
     p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--mode", choices=["fitch", "sankoff"], default="fitch")
+    p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
+    p.add_argument("--replay-leaves", type=int, default=1000)
+    p.add_argument("--replay-blocks", type=int, default=500)
+    p.add_argument("--replay-block-len", type=int, default=10_000)
+    p.add_argument("--cpu-leaves", type=int, default=16, help="leaves replayed on the CPU baseline")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
@@ -54,6 +58,8 @@ def log(rank, *a):
 
 def main():
     args = parse()
+    if args.mode == "replay":
+        return replay_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -240,6 +246,101 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     parity = {"sites": ns, "records": int(want.shape[0]),
               "bit_exact": bool(got.shape == want.shape and (got == want).all())}
     return cpu, parity
+
+
+def replay_main(args):
+    """FASTA replay (R1-R3) on config C5 (E. coli-like PanMAT, synthetic): leaf*column/s of
+    the GPU replay (consensus expansion + path mutations), inputs resident in HBM; host
+    formatting and the end-to-end rate are reported beside it."""
+    import ctypes as C
+
+    from panman_amd.synth import c5_panmat
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != 1:
+        raise SystemExit("replay mode runs on one GPU (leaf shards are independent replicas)")
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    pm = c5_panmat(leaves=args.replay_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len)
+    eng = panman_amd.Engine(0)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.replay_prepare(pm)
+    leaves, cols, edits = eng.replay_shape()
+    print(f"[bench] replay PanMAT {leaves} leaves x {cols} columns, {edits} edits ({time.time() - t0:.1f}s)",
+          file=sys.stderr, flush=True)
+    for _ in range(max(1, args.warmup)):
+        eng.replay_run()
+    torch.cuda.synchronize()
+    eng.set_profiling(True)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        eng.replay_run()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    ms, launches = eng.kernel_times(4)
+    eng.set_profiling(False)
+    units = float(leaves) * cols
+    value = units * args.steps / elapsed
+    # path mutation records per leaf (8 B each in the SURVEY.md §8d replay model)
+    a = pm._arrays
+    per_node = np.diff(a["nuc_mut_offsets"])
+    parent = np.full(pm.num_nodes, -1, np.int64)
+    off = pm.child_offsets
+    for v in range(pm.num_nodes):
+        parent[pm.child_index[off[v]:off[v + 1]]] = v
+    acc = per_node.astype(np.int64).copy()
+    order = []   # BFS so parents come first
+    q = [pm.root]
+    while q:
+        v = q.pop()
+        order.append(v)
+        q.extend(pm.child_index[off[v]:off[v + 1]].tolist())
+    for v in order:
+        if parent[v] >= 0:
+            acc[v] += acc[parent[v]]
+    path_recs = float(acc[[i for i in range(pm.num_nodes) if off[i] == off[i + 1]]].sum())
+    alg_bytes = units * 1.5 + 8.0 * path_recs
+    kms = ms[3] / args.steps
+    achieved = alg_bytes / (kms * 1e-3) / 1e9
+    # host formatting (aligned FASTA of every leaf)
+    tf = time.perf_counter()
+    ptr, n = C.c_void_p(), C.c_int64(0)
+    eng._check(eng.lib.pm_replay_format(eng.ctx, 1, C.byref(ptr), C.byref(n)), "pm_replay_format")
+    fmt_s = time.perf_counter() - tf
+    text = C.string_at(ptr, n.value)
+    eng.lib.pm_free(ptr)
+    cpu = parity = None
+    if not args.no_cpu:
+        import oracle as orc
+        k = args.cpu_leaves
+        want, secs = orc.load().fasta(pm, True, leaf_limit=k, timed=True)
+        names = sorted(nm for nm, i in zip(pm.names, range(pm.num_nodes)) if off[i] == off[i + 1])[:k]
+        got = []
+        for nm in names:
+            at = text.find(b">" + nm.encode() + b"\n")
+            end = text.find(b">", at + 1)
+            got.append(text[at: end if end >= 0 else len(text)].decode())
+        parity = {"leaves": k, "bit_exact": "".join(got) == want}
+        cpu = {"value": k * cols / secs, "unit": "leaf*column/s", "cores": 1, "kind": "port",
+               "sample": f"first {k} leaves by name, aligned FASTA, oracle printFASTAUltraFast restatement "
+                         f"({secs:.1f}s, 1 thread; the reference's tbb::parallel_for_each body)"}
+    out = {
+        "metric": "FASTA replay leaf*column/s (aligned, GPU replay kernels)",
+        "value": value, "unit": "leaf*column/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8 (ASCII IUPAC)",
+        "data": "synthetic C5-like PanMAT (seeded: random-join tree, blocks, gap slots, block and nuc mutations)",
+        "config": {"workload": f"C5 replay: {leaves} leaves x {cols} aligned columns, "
+                               f"{args.replay_blocks} blocks, {edits} edits",
+                   "leaves": leaves, "columns": cols, "path_mutation_records": path_recs},
+        "roofline": {"bound": "hbm", "kernel": "k_replay_fill+k_replay_apply", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "algorithmic_bytes_per_launch": alg_bytes / 2,
+                     "avg_launch_ms": round(kms / 2, 4), "launches_per_step": launches[3] / args.steps},
+        "host_format_s": round(fmt_s, 3),
+        "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
+        "cpu_baseline": cpu, "parity_sample": parity,
+    }
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

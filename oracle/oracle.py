@@ -35,7 +35,7 @@ def load() -> "Oracle":
             C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
             C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
         lib.oracle_fasta.restype = C.c_void_p
-        lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int]
+        lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
         _lib = lib
     return Oracle(_lib)
 
@@ -60,12 +60,15 @@ class Oracle:
                                       mode, threads)
         return _take_string(self.lib, p)
 
-    def fasta(self, panmat, aligned: bool) -> str:
-        """printFASTAUltraFast records of every leaf, sorted by name (panman_amd.panmat.PanMAT)."""
+    def fasta(self, panmat, aligned: bool, leaf_limit: int = 0, timed: bool = False):
+        """printFASTAUltraFast records of every leaf (or the first `leaf_limit` by name),
+        sorted by name (panman_amd.panmat.PanMAT).  timed=True -> (text, seconds)."""
         st, keep = panmat.as_struct()
-        p = self.lib.oracle_fasta(C.byref(st), int(aligned))
+        secs = C.c_double(0.0)
+        p = self.lib.oracle_fasta(C.byref(st), int(aligned), int(leaf_limit), C.byref(secs))
         del keep
-        return _take_string(self.lib, p)
+        text = _take_string(self.lib, p)
+        return (text, secs.value) if timed else text
 
     def column(self, newick: str, leaves: str, algo: str, forced: int, parent: int) -> dict:
         p = self.lib.oracle_column(newick.encode(), leaves.encode(), self.ALGO[algo], forced, parent)

@@ -1154,8 +1154,9 @@ struct OraclePanmat {
     const uint8_t* sequence_inverted;  // nullable
 };
 
-// FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name.
-char* oracle_fasta(const OraclePanmat* p, int aligned) {
+// FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name; at most
+// `leaf_limit` leaves (<= 0: all) and, when `seconds` is set, the replay wall time.
+char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* seconds) {
     RTree t;
     const char* nm = p->names;
     for (int32_t i = 0; i < p->num_nodes; ++i) {
@@ -1193,8 +1194,15 @@ char* oracle_fasta(const OraclePanmat* p, int aligned) {
         t.gaps.push_back(gl);
     }
     std::string out;
-    for (auto& kv : t.all)
-        if (kv.second->children.empty()) out += leaf_record(t, kv.second, aligned != 0);
+    int done = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    for (auto& kv : t.all) {
+        if (!kv.second->children.empty()) continue;
+        if (leaf_limit > 0 && done >= leaf_limit) break;
+        out += leaf_record(t, kv.second, aligned != 0);
+        ++done;
+    }
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return dup_string(out);
 }
 

@@ -56,6 +56,12 @@ class PanMAT:
         self.rotation = np.zeros(n, np.int32)
         self.inverted = np.zeros(n, np.uint8)
 
+    def set_arrays(self, **arrays):
+        """Bulk form: block_primary, block_seq_offsets, block_seq, gap_primary, gap_offsets,
+        gap_position, gap_length, block_mut_offsets/_primary/_info/_inversion,
+        nuc_mut_offsets/_primary/_secondary/_position/_gap_position/_info/_nucs (numpy)."""
+        self._arrays = arrays
+
     @property
     def num_nodes(self):
         return len(self.names)
@@ -100,6 +106,21 @@ class PanMAT:
 
         blob = b"".join(n.encode() + b"\0" for n in self.names)
         keep.append(blob)
+        a = getattr(self, "_arrays", None)
+        if a is not None:
+            return PanmatStruct(
+                self.num_nodes, self.root, arr(self.child_offsets, np.int32), arr(self.child_index, np.int32), blob,
+                len(a["block_primary"]), arr(a["block_primary"], np.int32), arr(a["block_seq_offsets"], np.int64),
+                arr(a["block_seq"], np.uint32),
+                len(a["gap_primary"]), arr(a["gap_primary"], np.int32), arr(a["gap_offsets"], np.int64),
+                arr(a["gap_position"], np.uint32), arr(a["gap_length"], np.uint32),
+                arr(a["block_mut_offsets"], np.int64), arr(a["block_mut_primary"], np.int32),
+                arr(a["block_mut_info"], np.uint8), arr(a["block_mut_inversion"], np.uint8),
+                arr(a["nuc_mut_offsets"], np.int64), arr(a["nuc_mut_primary"], np.int32),
+                arr(a["nuc_mut_secondary"], np.int32), arr(a["nuc_mut_position"], np.int32),
+                arr(a["nuc_mut_gap_position"], np.int32), arr(a["nuc_mut_info"], np.uint8),
+                arr(a["nuc_mut_nucs"], np.uint32),
+                arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8)), keep
         seq_off = np.zeros(len(self.blocks) + 1, np.int64)
         seq = []
         for i, (_, w) in enumerate(self.blocks):

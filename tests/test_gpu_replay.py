@@ -77,3 +77,11 @@ def test_msa_to_fasta_round_trip_on_gpu(engine, oracle):
     pnames, poff, pidx, proot = parse_newick(nwk)
     pm = from_msa_dump(dump, pnames, poff, pidx, proot)
     assert parse_records(engine.fasta(pm, True)) == rows
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_c5_like_panmat_vs_oracle(engine, oracle, aligned):
+    """Bulk generator (bench workload family C5) at reduced size, every leaf compared."""
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=120, blocks=40, mean_len=1500, seed=11)
+    assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))
