@@ -40,6 +40,7 @@ _SIGS = {
     "pm_last_error": (C.c_char_p, [C.c_void_p]),
     "pm_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pm_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "pm_set_option": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
     "pm_tree_upload": (C.c_int, [C.c_void_p, C.POINTER(Tree)]),
     "pm_leaves_upload": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
                                    C.c_void_p, C.c_int64]),

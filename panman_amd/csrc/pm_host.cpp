@@ -57,6 +57,16 @@ void free_tree(DevTree& t) {
     dev_free(t.down_order);
     dev_free(t.leaf_parent);
     dev_free(t.leaf_down);
+    dev_free(t.rg_node_off);
+    dev_free(t.rg_node_dense);
+    dev_free(t.rg_node_pslot);
+    dev_free(t.rg_node_flags);
+    dev_free(t.rg_child_off);
+    dev_free(t.rg_child);
+    dev_free(t.rg_stage_off);
+    dev_free(t.rg_stage);
+    dev_free(t.rg_up_order);
+    dev_free(t.rg_down_order);
     t = DevTree{};
 }
 
@@ -141,7 +151,8 @@ int run_once(pm_ctx* c, int mode) {
     const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
     if (sankoff && c->max_degree > 4095)
         return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
-    hipError_t e = sankoff ? launch_sankoff(c, block) : launch_fitch(c, block);
+    hipError_t e = sankoff ? launch_sankoff(c, block)
+                           : (mode == PM_MODE_FITCH && c->fused) ? launch_fitch_fused(c) : launch_fitch(c, block);
     if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
     e = launch_score(c);
     if (e != hipSuccess) return hip_fail(c, e, "score launch");
@@ -169,6 +180,145 @@ int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
         if (rc != PM_OK) return rc;
     }
     return fail(c, PM_ERR_STATE, "mutation record buffer still overflowing");
+}
+
+// Partition the internal nodes into connected subtree regions of at most kRegionSlots
+// internal nodes and kRegionStage leaf children (greedy, children before parents: cut the
+// heaviest child subtrees until the node fits).  Nodes with more than 4 children or more
+// leaf children than fit the stage form singleton "wide" regions that stream their leaves.
+struct Regions {
+    std::vector<int32_t> node_off{0}, node_dense, node_pslot, node_flags, child_off{0}, child, stage_off{0}, stage;
+    std::vector<int32_t> up_order, down_order, up_level_off, down_level_off;
+};
+
+void build_regions(const std::vector<int32_t>& bfs, const int32_t* off, const int32_t* idx, int32_t root,
+                   const HostTree& ht, Regions& rg) {
+    const int32_t N = (int32_t)bfs.size();
+    std::vector<int32_t> W(N, 0), LF(N, 0);
+    std::vector<uint8_t> cut(N, 0), wide(N, 0);
+    for (int32_t k = N - 1; k >= 0; --k) {
+        const int32_t v = bfs[k];
+        const int32_t deg = off[v + 1] - off[v];
+        if (deg == 0) continue;
+        int32_t leaf_kids = 0;
+        std::vector<std::pair<int32_t, int32_t>> kids;   // (weight, child)
+        for (int32_t e = off[v]; e < off[v + 1]; ++e) {
+            const int32_t c = idx[e];
+            if (off[c + 1] == off[c]) ++leaf_kids;
+            else kids.emplace_back(W[c], c);
+        }
+        if (deg > 4 || leaf_kids > kRegionStage) {
+            wide[v] = 1;
+            for (auto& kc : kids) cut[kc.second] = 1;
+            W[v] = kRegionSlots + 1;   // the parent always cuts a wide node
+            LF[v] = kRegionStage + 1;
+            continue;
+        }
+        int32_t w = 1, lf = leaf_kids;
+        for (auto& kc : kids) { w += W[kc.second]; lf += LF[kc.second]; }
+        std::sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.first > b.first; });
+        for (auto& kc : kids) {
+            if (w <= kRegionSlots && lf <= kRegionStage) break;
+            cut[kc.second] = 1;
+            w -= W[kc.second];
+            lf -= LF[kc.second];
+        }
+        W[v] = w;
+        LF[v] = lf;
+    }
+    cut[root] = 1;
+    // enumerate regions in BFS order of their roots (parents' regions first)
+    std::vector<int32_t> region_of(N, -1), reg_root, reg_depth, reg_parent;
+    for (int32_t k = 0; k < N; ++k) {
+        const int32_t v = bfs[k];
+        if (off[v + 1] == off[v] || !cut[v]) continue;
+        const int32_t r = (int32_t)reg_root.size();
+        reg_root.push_back(v);
+        // post-order of the region's internal nodes
+        std::vector<int32_t> post;
+        std::vector<std::pair<int32_t, int32_t>> st{{v, off[v]}};
+        while (!st.empty()) {
+            auto& top = st.back();
+            const int32_t u = top.first;
+            if (top.second < off[u + 1]) {
+                const int32_t c = idx[top.second++];
+                if (off[c + 1] > off[c] && !cut[c]) st.emplace_back(c, off[c]);
+            } else {
+                post.push_back(u);
+                st.pop_back();
+            }
+        }
+        for (size_t i = 0; i < post.size(); ++i) region_of[post[i]] = r;
+        int32_t nstage = 0;
+        for (size_t i = 0; i < post.size(); ++i) {
+            const int32_t u = post[i];
+            rg.node_dense.push_back(ht.dense_of[u]);
+            int32_t pslot = -1;
+            if (u != v) {
+                const int32_t par = [&] {   // parent of u inside the region
+                    for (size_t j = i + 1; j < post.size(); ++j)
+                        for (int32_t e = off[post[j]]; e < off[post[j] + 1]; ++e)
+                            if (idx[e] == u) return (int32_t)j;
+                    return (int32_t)-1;
+                }();
+                pslot = par;
+            }
+            rg.node_pslot.push_back(pslot);
+            int32_t flags = 0;
+            for (int32_t e = off[u]; e < off[u + 1]; ++e) {
+                const int32_t c = idx[e];
+                if (off[c + 1] == off[c]) {
+                    const int32_t rank = -ht.dense_of[c] - 1;
+                    if (wide[u]) rg.child.push_back((rank << 2) | 1);
+                    else {
+                        rg.stage.push_back(rank);
+                        rg.child.push_back((nstage++ << 2) | 0);
+                    }
+                } else if (cut[c]) {
+                    rg.child.push_back((ht.dense_of[c] << 2) | 3);
+                    flags |= 1;
+                } else {
+                    int32_t sl = 0;
+                    for (size_t j = 0; j < i; ++j)
+                        if (post[j] == c) sl = (int32_t)j;
+                    rg.child.push_back((sl << 2) | 2);
+                }
+            }
+            rg.node_flags.push_back(flags);
+            rg.child_off.push_back((int32_t)rg.child.size());
+        }
+        rg.node_off.push_back((int32_t)rg.node_dense.size());
+        rg.stage_off.push_back((int32_t)rg.stage.size());
+    }
+    const int32_t R = (int32_t)reg_root.size();
+    // region depth (BFS order) and height (reverse)
+    std::vector<int32_t> depth(R, 0), height(R, 0);
+    std::vector<int32_t> parent_node(N, -1);
+    for (int32_t v = 0; v < N; ++v)
+        for (int32_t e = off[v]; e < off[v + 1]; ++e) parent_node[idx[e]] = v;
+    for (int32_t r = 0; r < R; ++r) {
+        const int32_t v = reg_root[r];
+        depth[r] = v == root ? 0 : depth[region_of[parent_node[v]]] + 1;
+    }
+    for (int32_t r = R - 1; r >= 0; --r) {
+        const int32_t v = reg_root[r];
+        if (v != root) {
+            const int32_t pr = region_of[parent_node[v]];
+            height[pr] = std::max(height[pr], height[r] + 1);
+        }
+    }
+    auto bucket = [&](const std::vector<int32_t>& key, std::vector<int32_t>& offs, std::vector<int32_t>& order) {
+        int32_t levels = 0;
+        for (int32_t x : key) levels = std::max(levels, x + 1);
+        offs.assign(levels + 1, 0);
+        for (int32_t x : key) ++offs[x + 1];
+        for (int32_t k = 0; k < levels; ++k) offs[k + 1] += offs[k];
+        order.assign(key.size(), 0);
+        std::vector<int32_t> cur(offs.begin(), offs.end() - 1);
+        for (int32_t r = 0; r < (int32_t)key.size(); ++r) order[cur[key[r]]++] = r;
+    };
+    bucket(height, rg.up_level_off, rg.up_order);
+    bucket(depth, rg.down_level_off, rg.down_order);
 }
 
 }  // namespace
@@ -239,6 +389,15 @@ int pm_set_stream(pm_ctx* c, void* s) {
     if (!c) return PM_ERR_ARG;
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
     return PM_OK;
+}
+
+int pm_set_option(pm_ctx* c, int option, int64_t value) {
+    if (!c) return PM_ERR_ARG;
+    if (option == PM_OPT_FUSED) {
+        c->fused = value != 0;
+        return PM_OK;
+    }
+    return fail(c, PM_ERR_ARG, "unknown option");
 }
 
 int pm_set_profiling(pm_ctx* c, int enable) {
@@ -346,6 +505,11 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 
+    Regions rg;
+    build_regions(bfs, off, idx, t->root, ht, rg);
+    ht.rg_up_level_off = rg.up_level_off;
+    ht.rg_down_level_off = rg.down_level_off;
+
     free_work(c);
     free_columns(c);
     free_tree(c->dt);
@@ -362,10 +526,21 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_order, up_order, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_order, down_order, c->stream)) != hipSuccess ||
         (e = upload(&dt.leaf_parent, leaf_parent, c->stream)) != hipSuccess ||
-        (e = upload(&dt.leaf_down, leaf_down, c->stream)) != hipSuccess) {
+        (e = upload(&dt.leaf_down, leaf_down, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_node_dense, rg.node_dense, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_node_pslot, rg.node_pslot, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_node_flags, rg.node_flags, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_child_off, rg.child_off, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_child, rg.child, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_stage_off, rg.stage_off, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_stage, rg.stage, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_up_order, rg.up_order, c->stream)) != hipSuccess ||
+        (e = upload(&dt.rg_down_order, rg.down_order, c->stream)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
+    dt.num_regions = (int32_t)rg.up_order.size();
     c->dt = dt;
     c->ht = std::move(ht);
     c->max_degree = 0;

@@ -46,7 +46,22 @@ struct DevTree {
     int32_t* down_order = nullptr;    // [I] dense indices grouped by depth (pre-order levels)
     int32_t* leaf_parent = nullptr;   // [L] parent dense index (synthetic generator)
     int32_t* leaf_down = nullptr;     // [L] leaf ranks grouped by depth (synthetic generator)
+    // subtree regions for the fused Fitch kernels (pm_fused.hip)
+    int32_t num_regions = 0;
+    int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
+    int32_t* rg_node_dense = nullptr;   // [E1] dense internal index
+    int32_t* rg_node_pslot = nullptr;   // [E1] slot of the parent inside the region, -1 = region root
+    int32_t* rg_node_flags = nullptr;   // [E1] bit 0: has children in other regions (publish final)
+    int32_t* rg_child_off = nullptr;    // [E1+1]
+    int32_t* rg_child = nullptr;        // [E2] (value << 2) | kind: 0 staged leaf, 1 direct leaf, 2 slot, 3 other region
+    int32_t* rg_stage_off = nullptr;    // [R+1]
+    int32_t* rg_stage = nullptr;        // [E3] leaf ranks staged in LDS
+    int32_t* rg_up_order = nullptr;     // [R] regions by height
+    int32_t* rg_down_order = nullptr;   // [R] regions by depth
 };
+
+constexpr int kRegionSlots = 6;   // internal nodes per region (LDS: 4 KiB each per wave)
+constexpr int kRegionStage = 8;   // staged leaves per region (LDS: 1 KiB + 256 B each)
 
 struct HostTree {
     int32_t num_nodes = 0;
@@ -61,6 +76,8 @@ struct HostTree {
     std::vector<int32_t> leaf_level_off;  // [D+1] offsets into leaf_down by depth
     std::vector<int32_t> child_off;       // dense CSR (host copy)
     std::vector<int32_t> child_enc;
+    std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
+    std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
 };
 
 struct Timer {
@@ -81,6 +98,7 @@ struct pm_ctx {
     pm::DevTree dt;
     bool has_tree = false;
     int32_t max_degree = 0;
+    bool fused = true;                // Fitch: subtree-region kernels (PM_OPT_FUSED)
 
     // column shard
     int64_t num_sites = 0;
@@ -126,6 +144,7 @@ void timer_end(pm_ctx* c, int cls);
 
 // kernel launchers (pm_fitch.hip / pm_sankoff.hip / pm_synth.hip)
 hipError_t launch_fitch(pm_ctx* c, bool block);
+hipError_t launch_fitch_fused(pm_ctx* c);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
 hipError_t launch_score(pm_ctx* c);
 hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_stride, const int32_t* d_row_of_leaf,

@@ -94,14 +94,16 @@ struct DownArgs {
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
 };
 
-__device__ __forceinline__ uint32_t valid_mask(const DownArgs& a, int64_t word) {
+template <class Args>
+__device__ __forceinline__ uint32_t valid_mask(const Args& a, int64_t word) {
     if (word >= a.words) return 0u;
     const int64_t left = a.sites - word * 32;
     return left >= 32 ? ~0u : ((1u << left) - 1u);
 }
 
 // Leaf mutation mask against the parent's final codes F (leaf final = own code).
-__device__ __forceinline__ uint32_t leaf_diff(const DownArgs& a, int32_t leaf, int64_t word, uint32_t valid,
+template <class Args>
+__device__ __forceinline__ uint32_t leaf_diff(const Args& a, int32_t leaf, int64_t word, uint32_t valid,
                                               const uint32_t* F, uint4& L) {
     const uint8_t flag = a.leaf_flag[leaf];
     if (flag == kLeafAbsent) {
