@@ -57,7 +57,10 @@ struct Lds {
     uint32_t mask[kRegionStage * kWave];    // staged leaf presence
 };
 
-__device__ __forceinline__ void stage_leaves(const FusedArgs& a, int32_t r, int lane, int64_t word, Lds& s) {
+// One region per workgroup (one wave); the device functions address it directly.
+__shared__ Lds s;
+
+__device__ __forceinline__ void stage_leaves(const FusedArgs& a, int32_t r, int lane, int64_t word) {
     const int32_t s0 = __builtin_amdgcn_readfirstlane(a.stage_off[r]);
     const int32_t s1 = __builtin_amdgcn_readfirstlane(a.stage_off[r + 1]);
     uint4 v[kRegionStage];
@@ -83,7 +86,7 @@ __device__ __forceinline__ void stage_leaves(const FusedArgs& a, int32_t r, int 
         }
 }
 
-__device__ __forceinline__ void slot_load(const Lds& s, int sl, int lane, uint32_t* x) {
+__device__ __forceinline__ void slot_load(int sl, int lane, uint32_t* x) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint4 v = s.slot[(sl * 4 + q) * kWave + lane];
@@ -91,15 +94,14 @@ __device__ __forceinline__ void slot_load(const Lds& s, int sl, int lane, uint32
     }
 }
 
-__device__ __forceinline__ void slot_store(Lds& s, int sl, int lane, const uint32_t* x) {
+__device__ __forceinline__ void slot_store(int sl, int lane, const uint32_t* x) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.slot[(sl * 4 + q) * kWave + lane] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
 }
 
 // Post-order over the region (src/fitchSankoff.cpp:30-56); the region root's set goes to
 // HBM (up pass) or to its slot (down pass).
-__device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int tile, int lane, int64_t word,
-                                            Lds& s, bool root_to_hbm) {
+__device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int tile, int lane, int64_t word, bool root_to_hbm) {
     const int32_t n0 = __builtin_amdgcn_readfirstlane(a.node_off[r]);
     const int32_t n1 = __builtin_amdgcn_readfirstlane(a.node_off[r + 1]);
     for (int32_t e = n0; e < n1; ++e) {
@@ -117,7 +119,7 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             } else if (kind == 1) {
                 leaf_set16(a, val, word, x);
             } else if (kind == 2) {
-                slot_load(s, val, lane, x);
+                slot_load(val, lane, x);
             } else {
                 load_set16(a.sets, val, a.tiles, tile, lane, x);
             }
@@ -133,52 +135,96 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             onehot_from_code(F.x, F.y, F.z, F.w, ~0u, x);
         }
         if (e == n1 - 1 && root_to_hbm) store_set16(a.sets, dense, a.tiles, tile, lane, x);
-        else slot_store(s, e - n0, lane, x);
+        else slot_store(e - n0, lane, x);
     }
 }
 
 __global__ __launch_bounds__(kWave) void k_region_up(FusedArgs a) {
-    __shared__ Lds s;
     const int lane = threadIdx.x;
     const int32_t r = __builtin_amdgcn_readfirstlane(a.order[blockIdx.x]);
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
-    stage_leaves(a, r, lane, word, s);
-    region_sets(a, r, tile, lane, word, s, true);
+    stage_leaves(a, r, lane, word);
+    region_sets(a, r, tile, lane, word, true);
 }
 
-__device__ __forceinline__ uint32_t staged_diff(const Lds& s, int val, int lane, uint32_t valid, const uint32_t* F,
+__device__ __forceinline__ uint32_t staged_diff(int val, int lane, uint32_t valid, const uint32_t* F,
                                                 uint4& L) {
     L = s.stage[val * kWave + lane];
     return valid & s.mask[val * kWave + lane] & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
 }
 
+// Parent's final codes of region entry e: the region root reads HBM (or the consensus),
+// others the parent's slot (quad 0).
+__device__ __forceinline__ uint4 parent_codes(const FusedArgs& a, int32_t e, int32_t n1, int32_t dense,
+                                              bool is_root, int lane, int64_t word) {
+    // read both without selecting between an LDS and a global pointer (gfx950 codegen)
+    const int ps = max(__builtin_amdgcn_readfirstlane(a.node_pslot[e]), 0);
+    uint4 v = s.slot[(ps * 4) * kWave + lane];
+    // pin the LDS load so LLVM cannot merge it with the global one into a flat-pointer phi
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    if (e == n1 - 1) v = is_root ? a.cons[word] : a.finals[(size_t)a.parent_dense[dense] * a.wpad + word];
+    return v;
+}
+
+// Mutations of region entry e and of its leaf children: count only (EMIT = false) or
+// write them at out[pos...] (EMIT = true).  Returns the lane's record count.
+template <bool EMIT>
+__device__ __forceinline__ uint32_t node_mutations(const FusedArgs& a, int32_t r, int32_t e, int32_t n0,
+                                                   int32_t n1, int lane, int64_t word, uint32_t valid, pm_mut* out,
+                                                   int64_t pos) {
+    const int32_t dense = __builtin_amdgcn_readfirstlane(a.node_dense[e]);
+    const uint4 f4 = s.slot[((e - n0) * 4) * kWave + lane];
+    const uint32_t pres = s.slot[((e - n0) * 4 + 1) * kWave + lane].x;
+    const uint4 q = parent_codes(a, e, n1, dense, dense == a.root_dense, lane, word);
+    const uint32_t F[4] = {f4.x, f4.y, f4.z, f4.w};
+    const uint32_t pc[4] = {q.x, q.y, q.z, q.w};
+    const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+    uint32_t k = 0;
+    if (EMIT) k += emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[dense], self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    else k += __builtin_popcount(self_diff);
+    const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_off[e]);
+    const int32_t c1 = __builtin_amdgcn_readfirstlane(a.child_off[e + 1]);
+    for (int32_t j = c0; j < c1; ++j) {
+        const int32_t cc = __builtin_amdgcn_readfirstlane(a.child[j]);
+        const int kind = cc & 3;
+        if (kind > 1) continue;
+        if (kind == 0) {
+            const int sv = cc >> 2;
+            const uint4 L = s.stage[sv * kWave + lane];
+            const uint32_t d = valid & s.mask[sv * kWave + lane] & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
+            if (!EMIT) k += __builtin_popcount(d);
+            else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[a.stage[a.stage_off[r] + sv]], d, word, F,
+                                  L.x, L.y, L.z, L.w);
+        } else {
+            uint4 G;
+            const uint32_t d = leaf_diff(a, cc >> 2, word, valid, F, G);
+            if (!EMIT) k += __builtin_popcount(d);
+            else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[cc >> 2], d, word, F, G.x, G.y, G.z, G.w);
+        }
+    }
+    return k;
+}
+
 __global__ __launch_bounds__(kWave) void k_region_down(FusedArgs a) {
-    __shared__ Lds s;
     const int lane = threadIdx.x;
     const int32_t r = __builtin_amdgcn_readfirstlane(a.order[blockIdx.x]);
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
-    stage_leaves(a, r, lane, word, s);
-    region_sets(a, r, tile, lane, word, s, false);
+    stage_leaves(a, r, lane, word);
+    region_sets(a, r, tile, lane, word, false);
 
     const int32_t n0 = __builtin_amdgcn_readfirstlane(a.node_off[r]);
     const int32_t n1 = __builtin_amdgcn_readfirstlane(a.node_off[r + 1]);
-    const uint32_t shard = (uint32_t)(blockIdx.x + blockIdx.y * 7919u) % kShards;
-    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
-    for (int32_t e = n1 - 1; e >= n0; --e) {   // parents before children
+    // pass 1, parents first: final codes; a node's slot becomes {F, (pres, -, -, -), ...}
+    for (int32_t e = n1 - 1; e >= n0; --e) {
         const int32_t dense = __builtin_amdgcn_readfirstlane(a.node_dense[e]);
         const bool is_root = dense == a.root_dense;
-        uint32_t own[16], P[16], fin[16], pc[4];
-        slot_load(s, e - n0, lane, own);
-        {
-            uint4 q;
-            if (e == n1 - 1) q = is_root ? a.cons[word] : a.finals[(size_t)a.parent_dense[dense] * a.wpad + word];
-            else q = s.slot[(a.node_pslot[e] * 4) * kWave + lane];   // parent's final (quad 0)
-            pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
-        }
-        onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
+        uint32_t own[16], P[16], fin[16];
+        slot_load(e - n0, lane, own);
+        uint4 q = parent_codes(a, e, n1, dense, is_root, lane, word);
+        onehot_from_code(q.x, q.y, q.z, q.w, ~0u, P);
         const uint32_t pres = any_plane(own);
         lowest_code(own, fin);
         if (!is_root) {   // parent & own ? parent : lowest(own)  (src/fitchSankoff.cpp:115-123)
@@ -191,6 +237,7 @@ __global__ __launch_bounds__(kWave) void k_region_down(FusedArgs a) {
         uint32_t F[4];
         code_from_onehot(fin, F[0], F[1], F[2], F[3]);
         s.slot[((e - n0) * 4) * kWave + lane] = make_uint4(F[0], F[1], F[2], F[3]);
+        s.slot[((e - n0) * 4 + 1) * kWave + lane] = make_uint4(pres, 0, 0, 0);
         if (__builtin_amdgcn_readfirstlane(a.node_flags[e]) & 1)
             a.finals[(size_t)dense * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
         if (is_root) {
@@ -200,39 +247,21 @@ __global__ __launch_bounds__(kWave) void k_region_down(FusedArgs a) {
                     a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
             }
         }
-
-        // mutations of this node and of its leaf children (src/fitchSankoff.cpp:131-171)
-        const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-        uint32_t count = __builtin_popcount(self_diff);
-        const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_off[e]);
-        const int32_t c1 = __builtin_amdgcn_readfirstlane(a.child_off[e + 1]);
-        for (int32_t j = c0; j < c1; ++j) {
-            const int32_t cc = __builtin_amdgcn_readfirstlane(a.child[j]);
-            uint4 L;
-            if ((cc & 3) == 0) count += __builtin_popcount(staged_diff(s, cc >> 2, lane, valid, F, L));
-            else if ((cc & 3) == 1) count += __builtin_popcount(leaf_diff(a, cc >> 2, word, valid, F, L));
-        }
-        uint32_t total;
-        const uint32_t excl = wave_exclusive_scan(count, total);
-        if (total == 0) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
-        base = __shfl(base, 0, 64);
-        int64_t pos = (int64_t)base + excl;
-        pos += emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[dense], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-        for (int32_t j = c0; j < c1; ++j) {
-            const int32_t cc = __builtin_amdgcn_readfirstlane(a.child[j]);
-            uint4 L;
-            uint32_t d;
-            if ((cc & 3) == 0) d = staged_diff(s, cc >> 2, lane, valid, F, L);
-            else if ((cc & 3) == 1) d = leaf_diff(a, cc >> 2, word, valid, F, L);
-            else continue;
-            int32_t leaf;
-            if ((cc & 3) == 0) leaf = a.stage[a.stage_off[r] + (cc >> 2)];
-            else leaf = cc >> 2;
-            if (d) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
-        }
     }
+    // pass 2: count every mutation of the region (nodes + leaf children), one atomic per wave;
+    // pass 3: write them (src/fitchSankoff.cpp:131-171)
+    uint32_t count = 0;
+    for (int32_t e = n0; e < n1; ++e) count += node_mutations<false>(a, r, e, n0, n1, lane, word, valid, nullptr, 0);
+    uint32_t total;
+    const uint32_t excl = wave_exclusive_scan(count, total);
+    if (total == 0) return;
+    const uint32_t shard = (uint32_t)(blockIdx.x + blockIdx.y * 7919u) % kShards;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
+    base = __shfl(base, 0, 64);
+    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
+    int64_t pos = (int64_t)base + excl;
+    for (int32_t e = n0; e < n1; ++e) pos += node_mutations<true>(a, r, e, n0, n1, lane, word, valid, out, pos);
 }
 
 }  // namespace

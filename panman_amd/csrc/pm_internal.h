@@ -60,8 +60,8 @@ struct DevTree {
     int32_t* rg_down_order = nullptr;   // [R] regions by depth
 };
 
-constexpr int kRegionSlots = 6;   // internal nodes per region (LDS: 4 KiB each per wave)
-constexpr int kRegionStage = 8;   // staged leaves per region (LDS: 1 KiB + 256 B each)
+constexpr int kRegionSlots = 3;   // internal nodes per region (LDS: 4 KiB each per wave)
+constexpr int kRegionStage = 4;   // staged leaves per region (LDS: 1 KiB + 256 B each)
 
 struct HostTree {
     int32_t num_nodes = 0;
