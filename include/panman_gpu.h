@@ -82,9 +82,13 @@ void pm_destroy(pm_ctx* ctx);
 const char* pm_last_error(const pm_ctx* ctx);
 /* Queue all work on `hip_stream` (a hipStream_t; NULL = the ctx's own stream). */
 int pm_set_stream(pm_ctx* ctx, void* hip_stream);
-/* Options.  PM_OPT_FUSED (default 1): Fitch runs on subtree regions with intermediate
- * sets in LDS; 0 selects the one-launch-per-tree-level kernels (same results). */
+/* Options (results are identical either way):
+ *   PM_OPT_FUSED   (default 0): Fitch on subtree regions with intermediate sets in LDS
+ *                  (experimental; slower than the level kernels on MI355X so far).
+ *   PM_OPT_VIRTUAL (default 1): Fitch level kernels evaluate internal nodes whose children
+ *                  are all leaves inline in their parent instead of materialising them. */
 #define PM_OPT_FUSED 1
+#define PM_OPT_VIRTUAL 2
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

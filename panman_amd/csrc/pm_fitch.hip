@@ -32,7 +32,8 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0) load_set16(a.sets, c, a.tiles, tile, lane, s);
+        if (c >= 0 && (c & kVirtualBit)) virtual_set16(a, c & ~kVirtualBit, word, s);
+        else if (c >= 0) load_set16(a.sets, c, a.tiles, tile, lane, s);
         else leaf_set16(a, -c - 1, word, s);
 #pragma unroll
         for (int v = 0; v < 16; ++v) { both[v] &= s[v]; either[v] |= s[v]; }
@@ -87,9 +88,17 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const int32_t tiles = (c->words + kWave - 1) / kWave;
     const int64_t wpad = (int64_t)tiles * kWave;
 
+    // Fitch (not block Fitch) may skip materialising leaf-parents
+    const bool virt = !block && c->virtual_leaf_parents;
+    const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
+    const int32_t* up_order = virt ? dt.up_order_v : dt.up_order;
+    const int32_t* down_order = virt ? dt.down_order_v : dt.down_order;
+    const std::vector<int32_t>& up_off = virt ? ht.up_level_off_v : ht.up_level_off;
+    const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
+
     UpArgs up{};
     up.child_off = dt.child_off;
-    up.child_enc = dt.child_enc;
+    up.child_enc = child_enc;
     up.leaf_flag = c->leaf_flag;
     up.leaf_planes = c->leaf_planes;
     up.leaf_present = c->leaf_present;
@@ -99,10 +108,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
-    const int H = (int)ht.up_level_off.size() - 1;
+    const int H = (int)up_off.size() - 1;
     for (int h = 0; h < H; ++h) {
-        up.order = dt.up_order + ht.up_level_off[h];
-        up.count = ht.up_level_off[h + 1] - ht.up_level_off[h];
+        up.order = up_order + up_off[h];
+        up.count = up_off[h + 1] - up_off[h];
+        if (up.count == 0) continue;
         dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 0);
         hipLaunchKernelGGL(k_fitch_up, grid, dim3(kBlock), 0, c->stream, up);
@@ -113,7 +123,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     if (e != hipSuccess) return e;
     DownArgs dn{};
     dn.child_off = dt.child_off;
-    dn.child_enc = dt.child_enc;
+    dn.child_enc = child_enc;
     dn.parent_dense = dt.parent_dense;
     dn.internal_id = dt.internal_id;
     dn.leaf_id = dt.leaf_id;
@@ -134,10 +144,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.root_code = c->root_code;
     dn.forced = (c->has_forced && block) ? c->forced : nullptr;
     dn.absent_code0 = false;
-    const int D = (int)ht.down_level_off.size() - 1;
+    const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
-        dn.order = dt.down_order + ht.down_level_off[d];
-        dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
+        dn.order = down_order + down_off[d];
+        dn.count = down_off[d + 1] - down_off[d];
+        if (dn.count == 0) continue;
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
         if (block) hipLaunchKernelGGL(k_down<Mode::kBlockFitch>, grid, dim3(kBlock), 0, c->stream, dn);

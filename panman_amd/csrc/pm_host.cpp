@@ -57,6 +57,9 @@ void free_tree(DevTree& t) {
     dev_free(t.down_order);
     dev_free(t.leaf_parent);
     dev_free(t.leaf_down);
+    dev_free(t.child_enc_v);
+    dev_free(t.up_order_v);
+    dev_free(t.down_order_v);
     dev_free(t.rg_node_off);
     dev_free(t.rg_node_dense);
     dev_free(t.rg_node_pslot);
@@ -397,6 +400,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->fused = value != 0;
         return PM_OK;
     }
+    if (option == PM_OPT_VIRTUAL) {
+        c->virtual_leaf_parents = value != 0;
+        return PM_OK;
+    }
     return fail(c, PM_ERR_ARG, "unknown option");
 }
 
@@ -505,6 +512,39 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 
+    // virtual leaf-parents (Fitch level kernels)
+    std::vector<int32_t> child_enc_v(ht.child_enc), up_order_v, down_order_v;
+    {
+        std::vector<uint8_t> virt(I, 0);
+        for (int32_t d = 0; d < I; ++d) {
+            if (ht.internal_id[d] == t->root) continue;
+            const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
+            bool all_leaves = deg <= 4;
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1] && all_leaves; ++e) all_leaves = ht.child_enc[e] < 0;
+            virt[d] = all_leaves;
+            ht.num_virtual += all_leaves;
+        }
+        for (auto& x : child_enc_v)
+            if (x >= 0 && virt[x]) x |= kVirtualBit;
+        bucket(H, I, [&](int32_t d) { return virt[d] ? H - 1 : height[ht.internal_id[d]] - 1; }, ht.up_level_off_v,
+               up_order_v);
+        bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
+        // drop virtual nodes from the level lists (kept stable within levels)
+        auto strip = [&](std::vector<int32_t>& order, std::vector<int32_t>& offs, bool up) {
+            std::vector<int32_t> o2, f2{0};
+            for (size_t k = 0; k + 1 < offs.size(); ++k) {
+                for (int32_t i = offs[k]; i < offs[k + 1]; ++i)
+                    if (!virt[order[i]]) o2.push_back(order[i]);
+                if ((int32_t)o2.size() > f2.back()) f2.push_back((int32_t)o2.size());   // skip empty levels
+                (void)up;
+            }
+            order.swap(o2);
+            offs.swap(f2);
+        };
+        strip(up_order_v, ht.up_level_off_v, true);
+        strip(down_order_v, ht.down_level_off_v, false);
+    }
+
     Regions rg;
     build_regions(bfs, off, idx, t->root, ht, rg);
     ht.rg_up_level_off = rg.up_level_off;
@@ -527,6 +567,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.down_order, down_order, c->stream)) != hipSuccess ||
         (e = upload(&dt.leaf_parent, leaf_parent, c->stream)) != hipSuccess ||
         (e = upload(&dt.leaf_down, leaf_down, c->stream)) != hipSuccess ||
+        (e = upload(&dt.child_enc_v, child_enc_v, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_order_v, up_order_v, c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_order_v, down_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_dense, rg.node_dense, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_pslot, rg.node_pslot, c->stream)) != hipSuccess ||

@@ -46,6 +46,11 @@ struct DevTree {
     int32_t* down_order = nullptr;    // [I] dense indices grouped by depth (pre-order levels)
     int32_t* leaf_parent = nullptr;   // [L] parent dense index (synthetic generator)
     int32_t* leaf_down = nullptr;     // [L] leaf ranks grouped by depth (synthetic generator)
+    // Fitch with "virtual" leaf-parents: an internal node whose children are all leaves
+    // (<= 4) is never materialised; its parent evaluates it from the leaves in both passes
+    int32_t* child_enc_v = nullptr;   // [E] as child_enc, virtual children tagged kVirtualBit
+    int32_t* up_order_v = nullptr;    // [I'] materialised internal nodes by height
+    int32_t* down_order_v = nullptr;  // [I'] materialised internal nodes by depth
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
     int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
@@ -60,6 +65,7 @@ struct DevTree {
     int32_t* rg_down_order = nullptr;   // [R] regions by depth
 };
 
+constexpr int32_t kVirtualBit = 1 << 30;
 constexpr int kRegionSlots = 3;   // internal nodes per region (LDS: 4 KiB each per wave)
 constexpr int kRegionStage = 4;   // staged leaves per region (LDS: 1 KiB + 256 B each)
 
@@ -76,6 +82,9 @@ struct HostTree {
     std::vector<int32_t> leaf_level_off;  // [D+1] offsets into leaf_down by depth
     std::vector<int32_t> child_off;       // dense CSR (host copy)
     std::vector<int32_t> child_enc;
+    std::vector<int32_t> up_level_off_v;    // levels of up_order_v / down_order_v
+    std::vector<int32_t> down_level_off_v;
+    int64_t num_virtual = 0;
     std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
     std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
 };
@@ -98,7 +107,8 @@ struct pm_ctx {
     pm::DevTree dt;
     bool has_tree = false;
     int32_t max_degree = 0;
-    bool fused = true;                // Fitch: subtree-region kernels (PM_OPT_FUSED)
+    bool fused = false;               // Fitch: subtree-region kernels (PM_OPT_FUSED, experimental)
+    bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
 
     // column shard
     int64_t num_sites = 0;

@@ -67,6 +67,26 @@ __device__ __forceinline__ void leaf_set16(const Args& a, int32_t leaf, int64_t 
     if (a.absent_code0) s[0] |= ~m;
 }
 
+// Set of a "virtual" internal node whose children are all leaves (never materialised):
+// the Fitch AND-else-OR over its leaf children (src/fitchSankoff.cpp:39-55).
+template <class Args>
+__device__ __forceinline__ void virtual_set16(const Args& a, int32_t v, int64_t word, uint32_t* s) {
+    uint32_t both[16], either[16], x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { both[k] = ~0u; either[k] = 0u; }
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        leaf_set16(a, -c - 1, word, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { both[k] &= x[k]; either[k] |= x[k]; }
+    }
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s[k] = both[k] | (either[k] & ~nz);
+}
+
 struct DownArgs {
     const int32_t* order;
     int32_t count;
@@ -139,6 +159,38 @@ __device__ __forceinline__ uint32_t emit(pm_mut* out, int64_t pos, int64_t cap, 
         const uint32_t site = (uint32_t)(word * 32 + b);
         if (pos + k < cap) out[pos + k] = pm_mut{node, (site << 8) | (type << 4) | (type == PM_MUT_ND ? 0u : c)};
         ++k;
+    }
+    return k;
+}
+
+// A virtual child v of a node with final one-hot planes Pn (codes Fn): its final
+// (parent & own ? parent : lowest(own)), its mutation and its leaf children's mutations.
+// Count only (EMIT = false) or write at out[pos...].
+template <bool EMIT>
+__device__ __forceinline__ uint32_t virtual_child(const DownArgs& a, int32_t v, int64_t word, uint32_t valid,
+                                                  const uint32_t* Pn, const uint32_t* Fn, pm_mut* out, int64_t pos) {
+    uint32_t own[16], fin[16];
+    virtual_set16(a, v, word, own);
+    const uint32_t pres = any_plane(own);
+    lowest_code(own, fin);
+    uint32_t hit = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) hit |= Pn[k] & own[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) fin[k] = (Pn[k] & hit) | (fin[k] & ~hit);
+    uint32_t F[4];
+    code_from_onehot(fin, F[0], F[1], F[2], F[3]);
+    const uint32_t self = pres & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
+    uint32_t k = EMIT ? emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3])
+                      : (uint32_t)__builtin_popcount(self);
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        uint4 L;
+        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
+        if (!EMIT) k += __builtin_popcount(d);
+        else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
     }
     return k;
 }
@@ -229,7 +281,10 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     int ncached = 0;
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0) continue;
+        if (c >= 0) {
+            if (M == Mode::kFitch && (c & kVirtualBit)) count += virtual_child<false>(a, c & ~kVirtualBit, word, valid, fin, F, nullptr, 0);
+            continue;
+        }
         uint4 L;
         const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
         count += __builtin_popcount(d);
@@ -266,6 +321,12 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[cid[k]]);
         if (cd[k]) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], cd[k], word, F, cl[k].x, cl[k].y,
                                cl[k].z, cl[k].w);
+    }
+    if (M == Mode::kFitch) {
+        for (int32_t e = e0; e < e1; ++e) {
+            const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+            if (c >= 0 && (c & kVirtualBit)) pos += virtual_child<true>(a, c & ~kVirtualBit, word, valid, fin, F, out, pos);
+        }
     }
     if (ncached == kCached) {
         int seen = 0;

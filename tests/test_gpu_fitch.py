@@ -57,8 +57,16 @@ def _random_columns(rng, leaves, sites, absent_frac=0.1, gap=0.2):
     return codes, present
 
 
-def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, fused=True):
-    engine.set_fused(fused)
+VARIANTS = ["virtual", "plain", "regions"]
+
+
+def _variant(engine, variant):
+    engine.set_fused(variant == "regions")
+    engine.set_virtual(variant == "virtual")
+
+
+def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant="virtual"):
+    _variant(engine, variant)
     n = off.shape[0] - 1
     leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
     node_row = np.full(n, -1, np.int32)
@@ -81,26 +89,26 @@ def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, fused
     return got
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("sites", [1, 31, 32, 33, 700, 2049])
-def test_random_binary_vs_oracle(engine, oracle, sites, fused):
+def test_random_binary_vs_oracle(engine, oracle, sites, variant):
     rng = np.random.default_rng(sites)
     off, idx, root = panman_amd.random_join_tree(257, seed=sites)
     codes, present = _random_columns(rng, 257, sites)
     cons = rng.integers(0, 16, size=sites).astype(np.uint8)
-    _compare(engine, oracle, off, idx, root, codes, present, cons, None, fused)
+    _compare(engine, oracle, off, idx, root, codes, present, cons, None, variant)
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("seed", range(6))
-def test_random_polytomy_vs_oracle(engine, oracle, seed, fused):
+def test_random_polytomy_vs_oracle(engine, oracle, seed, variant):
     rng = np.random.default_rng(100 + seed)
     off, idx, root = random_tree(300, rng, max_children=[6, 3, 4, 26, 2, 12][seed], unary=[0.1, 0.3, 0, 0.1, 0.5, 0][seed])
     sites = 333
     codes, present = _random_columns(rng, 300, sites, absent_frac=0.2)
     cons = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=sites)
     forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
-    _compare(engine, oracle, off, idx, root, codes, present, cons, forced, fused)
+    _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant)
 
 
 def test_all_absent_subtree_and_tiny_tree(engine, oracle):
@@ -113,12 +121,12 @@ def test_all_absent_subtree_and_tiny_tree(engine, oracle):
     _compare(engine, oracle, off, idx, 0, np.vstack([codes, codes, codes]), present, cons, None)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_synthetic_columns_sample_vs_oracle(engine, oracle, fused):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_synthetic_columns_sample_vs_oracle(engine, oracle, variant):
     """Tree-evolved columns from the on-device generator (bench workload, reduced size)."""
     leaves, sites = 20000, 4096
     off, idx, root = panman_amd.random_join_tree(leaves, seed=1)
-    engine.set_fused(fused)
+    _variant(engine, variant)
     engine.tree_upload(off, idx, root)
     engine.synth_columns(0, sites, seed=2)
     engine.run(panman_amd.MODE_FITCH)
