@@ -67,24 +67,30 @@ __device__ __forceinline__ void leaf_set16(const Args& a, int32_t leaf, int64_t 
     if (a.absent_code0) s[0] |= ~m;
 }
 
-// Set of a "virtual" internal node whose children are all leaves (never materialised):
-// the Fitch AND-else-OR over its leaf children (src/fitchSankoff.cpp:39-55).
+// Set of a "virtual" internal node whose children are all leaves (never materialised).
+// Leaf sets are single codes or empty, so the Fitch AND is non-empty only when every leaf
+// is present with the same code -- and then equals the OR: the set is always the union of
+// the present leaves' codes (src/fitchSankoff.cpp:39-55).
 template <class Args>
 __device__ __forceinline__ void virtual_set16(const Args& a, int32_t v, int64_t word, uint32_t* s) {
-    uint32_t both[16], either[16], x[16];
+    uint32_t x[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { both[k] = ~0u; either[k] = 0u; }
+    for (int k = 0; k < 16; ++k) s[k] = 0u;
     const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
     for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        leaf_set16(a, -c - 1, word, x);
+        leaf_set16(a, -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1, word, x);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) { both[k] &= x[k]; either[k] |= x[k]; }
+        for (int k = 0; k < 16; ++k) s[k] |= x[k];
     }
-    const uint32_t nz = any_plane(both);
+}
+
+// bit-sliced a < b for 4-bit codes
+__device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t* B) {
+    uint32_t lt = ~A[0] & B[0];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s[k] = both[k] | (either[k] & ~nz);
+    for (int j = 1; j < 4; ++j) lt = (~A[j] & B[j]) | (~(A[j] ^ B[j]) & lt);
+    return lt;
 }
 
 struct DownArgs {
@@ -163,34 +169,41 @@ __device__ __forceinline__ uint32_t emit(pm_mut* out, int64_t pos, int64_t cap, 
     return k;
 }
 
-// A virtual child v of a node with final one-hot planes Pn (codes Fn): its final
-// (parent & own ? parent : lowest(own)), its mutation and its leaf children's mutations.
+// A virtual child v of a node with final codes Fn: its final (parent if the parent's code
+// is among its leaves', else the lowest of them -- src/fitchSankoff.cpp:115-123 on the
+// union set), its mutation and its leaf children's mutations, all in code-plane form.
 // Count only (EMIT = false) or write at out[pos...].
 template <bool EMIT>
 __device__ __forceinline__ uint32_t virtual_child(const DownArgs& a, int32_t v, int64_t word, uint32_t valid,
-                                                  const uint32_t* Pn, const uint32_t* Fn, pm_mut* out, int64_t pos) {
-    uint32_t own[16], fin[16];
-    virtual_set16(a, v, word, own);
-    const uint32_t pres = any_plane(own);
-    lowest_code(own, fin);
-    uint32_t hit = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) hit |= Pn[k] & own[k];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) fin[k] = (Pn[k] & hit) | (fin[k] & ~hit);
-    uint32_t F[4];
-    code_from_onehot(fin, F[0], F[1], F[2], F[3]);
-    const uint32_t self = pres & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
-    uint32_t k = EMIT ? emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3])
-                      : (uint32_t)__builtin_popcount(self);
+                                                  const uint32_t* Fn, pm_mut* out, int64_t pos) {
     const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
+    uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
     for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
+        const uint8_t flag = a.leaf_flag[leaf];
+        if (flag == kLeafAbsent) continue;
+        const uint4 L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+        const uint32_t m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
+        const uint32_t C[4] = {L.x, L.y, L.z, L.w};
+        hit |= m & ~((C[0] ^ Fn[0]) | (C[1] ^ Fn[1]) | (C[2] ^ Fn[2]) | (C[3] ^ Fn[3]));
+        const uint32_t take = m & (~have | code_less(C, low));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) low[j] = (C[j] & take) | (low[j] & ~take);
+        have |= m;
+    }
+    uint32_t F[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
+    const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
+    uint32_t k = EMIT ? emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3])
+                      : (uint32_t)__builtin_popcount(self);
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
         uint4 L;
-        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
+        const uint32_t d = leaf_diff(a, leaf, word, valid, F, L);
         if (!EMIT) k += __builtin_popcount(d);
-        else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
+        else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
     }
     return k;
 }
@@ -282,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         if (c >= 0) {
-            if (M == Mode::kFitch && (c & kVirtualBit)) count += virtual_child<false>(a, c & ~kVirtualBit, word, valid, fin, F, nullptr, 0);
+            if (M == Mode::kFitch && (c & kVirtualBit)) count += virtual_child<false>(a, c & ~kVirtualBit, word, valid, F, nullptr, 0);
             continue;
         }
         uint4 L;
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     if (M == Mode::kFitch) {
         for (int32_t e = e0; e < e1; ++e) {
             const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-            if (c >= 0 && (c & kVirtualBit)) pos += virtual_child<true>(a, c & ~kVirtualBit, word, valid, fin, F, out, pos);
+            if (c >= 0 && (c & kVirtualBit)) pos += virtual_child<true>(a, c & ~kVirtualBit, word, valid, F, out, pos);
         }
     }
     if (ncached == kCached) {
