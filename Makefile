@@ -14,7 +14,7 @@ build/%.o: panman_amd/csrc/% $(HDR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ) -l:liblzma.so.5
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -143,6 +143,10 @@ int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
  * or "#error\t<message>\n" where the reference would exit or has undefined behaviour. */
 char* pm_msa_build(const char* newick, const char* msa_text, const char* reference, int mode, int device);
 void pm_free(void* p);
+/* The same construction written as a PanMAN file (Tree(...) + writePanMAN,
+ * src/panmanUtils.cpp:1409-1465, :271-299): one tree, one block. */
+int pm_msa_to_panman(const char* newick, const char* msa_text, const char* reference, int mode, int device,
+                     const char* out_path, char* err, int64_t err_len);
 
 /* ---- root-to-leaf mutation replay (FASTA extraction) ---------------------------------- */
 /* PanMAT fields used by printFASTAUltraFast (src/panman.hpp:520-543 Block / GapList,
@@ -193,6 +197,23 @@ int pm_replay_format(pm_ctx* ctx, int aligned, char** text, int64_t* length);
 /* Canonical aligned columns per leaf of the prepared PanMAT (gap slots before each main
  * position, block sentinels included) and the number of leaves. */
 int pm_replay_shape(pm_ctx* ctx, int64_t* leaves, int64_t* columns, int64_t* edits);
+
+/* ---- PanMAN files (xz + Cap'n Proto, schema panman.capnp) ----------------------------- */
+typedef struct pm_panman pm_panman;
+/* Load a .panman: TreeGroup(istream) + Tree::protoMATToTree (src/panman.cpp:6847-6877,
+ * :1661-1751, mutations assigned in pre-order :576-618).  Host only, no device needed.
+ * On failure `err` (nullable, err_len bytes) receives the reason. */
+int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len);
+int pm_panman_tree_count(const pm_panman* file);
+/* View of tree `index` as a pm_panmat (pointers into `file`, valid until pm_panman_free);
+ * node ids are pre-order positions of the stored Newick, names follow the reference's
+ * Newick naming. */
+int pm_panman_tree(const pm_panman* file, int index, pm_panmat* view);
+const char* pm_panman_newick(const pm_panman* file, int index);
+void pm_panman_free(pm_panman* file);
+/* Write trees as TreeGroup::writeToFile + writePanMAN do (src/panman.cpp:6885-7015,
+ * src/panmanUtils.cpp:271-299): capnp message, xz level 9 when `compress`. */
+int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, int compress);
 
 /* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
 /* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes

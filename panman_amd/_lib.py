@@ -58,17 +58,25 @@ _SIGS = {
     "pm_consensus_fetch": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
     "pm_msa_build": (C.c_void_p, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
     "pm_free": (None, [C.c_void_p]),
+    "pm_msa_to_panman": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_char_p,
+                                   C.c_char_p, C.c_int64]),
     "pm_fasta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "pm_replay_prepare": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pm_replay_run": (C.c_int, [C.c_void_p]),
     "pm_replay_format": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pm_panman_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int64]),
+    "pm_panman_tree_count": (C.c_int, [C.c_void_p]),
+    "pm_panman_tree": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "pm_panman_newick": (C.c_char_p, [C.c_void_p, C.c_int]),
+    "pm_panman_free": (None, [C.c_void_p]),
+    "pm_panman_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 
 
 def header_symbols() -> list[str]:
     """Every function the public header declares."""
-    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", " ", open(HEADER).read(), flags=re.S)
     return sorted(set(re.findall(r"\b(pm_[a-z_0-9]+)\s*\(", text)))
 
 

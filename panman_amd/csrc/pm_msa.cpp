@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "pm_internal.h"
+#include "pm_newick.h"
 
 namespace pm {
 namespace {
@@ -29,77 +30,6 @@ int nuc_code(char c) {
         case 'H': return 11; case 'V': return 7;  case 'N': return 15;
         default: return 0;   // gap, lowercase, anything else (src/panman.cpp:78-113)
     }
-}
-
-// Split on `delim`, re-joining pieces while a single quote is open (src/panman.cpp:265-296).
-std::vector<std::string> split_quoted(const std::string& s, char delim) {
-    std::vector<std::string> out;
-    size_t start = 0, open_at = 0;
-    bool open = false;
-    for (size_t end; (end = s.find(delim, start)) != std::string::npos; start = end + 1) {
-        const size_t from = open ? open_at : start;
-        const std::string piece = s.substr(from, end - from);
-        const bool odd = std::count(piece.begin(), piece.end(), '\'') % 2 == 1;
-        if (!open && odd) { open = true; open_at = start; }
-        else if (!open) out.push_back(piece);
-        else if (!odd) { open = false; out.push_back(piece); }
-    }
-    if (start < s.size()) out.push_back(s.substr(start));
-    return out;
-}
-
-// Newick topology, nodes numbered in creation (pre-)order; internal nodes are named
-// node_<k> in order of '(' and internal labels are ignored (src/panman.cpp:310-450).
-struct Topology {
-    std::vector<std::string> name;
-    std::vector<std::vector<int32_t>> kids;
-    int32_t root = -1;
-};
-
-bool parse_topology(std::string text, Topology& t, std::string& err) {
-    while (!text.empty() && text.back() == ' ') text.pop_back();
-    const size_t first = text.find_first_not_of(' ');
-    text = first == std::string::npos ? std::string() : text.substr(first);
-    struct Tok { std::string leaf; size_t opens = 0, closes = 0; };
-    std::vector<Tok> toks;
-    long depth = 0;
-    for (const std::string& piece : split_quoted(text, ',')) {
-        Tok k;
-        bool stop = false, quote = false, quoted = false;
-        for (char ch : piece) {
-            if (quote) { k.leaf += ch; quote = ch != '\''; }
-            else if (ch == '\'') { quote = quoted = true; k.leaf += ch; }
-            else if (ch == ':') stop = true;
-            else if (ch == '(') { ++k.opens; ++depth; }
-            else if (ch == ')') { stop = true; ++k.closes; --depth; }
-            else if (!stop) k.leaf += ch;
-        }
-        if (quoted && k.leaf.size() >= 2 && k.leaf.front() == '\'' && k.leaf.back() == '\'')
-            k.leaf = k.leaf.substr(1, k.leaf.size() - 2);
-        toks.push_back(std::move(k));
-    }
-    if (depth != 0) { err = "incorrect Newick format"; return false; }
-    std::stack<int32_t> open;
-    int internal = 0;
-    auto add = [&](const std::string& nm) {
-        t.name.push_back(nm);
-        t.kids.emplace_back();
-        const int32_t id = (int32_t)t.name.size() - 1;
-        if (!open.empty()) t.kids[open.top()].push_back(id);
-        return id;
-    };
-    for (const Tok& k : toks) {
-        for (size_t j = 0; j < k.opens; ++j) {
-            const int32_t id = add("node_" + std::to_string(++internal));
-            if (t.root < 0) t.root = id;
-            open.push(id);
-        }
-        if (open.empty()) { err = "leaf outside any clade"; return false; }
-        add(k.leaf);
-        for (size_t j = 0; j < k.closes && !open.empty(); ++j) open.pop();
-    }
-    if (t.root < 0) { err = "empty tree"; return false; }
-    return true;
 }
 
 // M1 reader: rows keyed (and ordered) by name, '\r' stripped, equal lengths required
@@ -161,11 +91,24 @@ struct CtxGuard {
     ~CtxGuard() { pm_destroy(c); }
 };
 
-std::string build(const char* newick_c, const char* msa_c, const char* ref_c, int mode, int device) {
+struct MsaResult {
+    std::string err;
+    Topology t;
+    std::string consensus;
+    std::vector<std::vector<Grouped>> muts;   // per node id, NucMut runs in list order
+};
+
+// The constructor body: returns the tree, consensus block and per-node NucMut lists.
+MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_c, int mode, int device) {
+    MsaResult res;
     std::string newick(newick_c), err;
     const size_t nl = newick.find('\n');
     if (nl != std::string::npos) newick.resize(nl);
-    Topology t;
+    auto dump_error = [&](const std::string& e) {
+        res.err = e;
+        return res;
+    };
+    Topology& t = res.t;
     if (!parse_topology(newick, t, err)) return dump_error(err);
     const std::string reference = ref_c ? ref_c : "";
 
@@ -204,9 +147,9 @@ std::string build(const char* newick_c, const char* msa_c, const char* ref_c, in
         consensus[i] = pick;
     }
 
-    std::string dump = "#consensus\t" + consensus + "\n";
-    dump += "#blockmut\t" + t.name[t.root] + "\t0\t-1\t1\t0\n";
-    if (width == 0) return dump;
+    res.consensus = consensus;
+    res.muts.assign(t.name.size(), {});
+    if (width == 0) return res;
 
     // CSR + leaf rows (rows in name order; leaves missing from the alignment are absent)
     const int32_t N = (int32_t)t.name.size();
@@ -255,21 +198,42 @@ std::string build(const char* newick_c, const char* msa_c, const char* ref_c, in
     std::vector<pm_mut> recs((size_t)std::max<int64_t>(n, 1));
     if ((rc = pm_mutations_fetch(g.c, recs.data(), n, &n)) != PM_OK) return dump_error(pm_last_error(g.c));
 
-    std::map<std::string, std::vector<Grouped>> per_node;
     for (int64_t a = 0; a < n;) {
         int64_t b = a;
         while (b < n && recs[b].node == recs[a].node) ++b;
-        group_node(recs.data() + a, b - a, per_node[t.name[recs[a].node]]);
+        group_node(recs.data() + a, b - a, res.muts[recs[a].node]);
         a = b;
     }
+    return res;
+}
+
+std::string build(const char* newick_c, const char* msa_c, const char* ref_c, int mode, int device) {
+    MsaResult r = build_result(newick_c, msa_c, ref_c, mode, device);
+    if (!r.err.empty()) return dump_error(r.err);
+    std::string dump = "#consensus\t" + r.consensus + "\n";
+    dump += "#blockmut\t" + r.t.name[r.t.root] + "\t0\t-1\t1\t0\n";
+    std::map<std::string, const std::vector<Grouped>*> by_name;   // nodes in name order
+    for (size_t v = 0; v < r.muts.size(); ++v)
+        if (!r.muts[v].empty()) by_name[r.t.name[v]] = &r.muts[v];
     std::ostringstream os;
-    for (auto& kv : per_node)
-        for (auto& m : kv.second) {
+    for (auto& kv : by_name)
+        for (auto& m : *kv.second) {
             char buf[96];
             std::snprintf(buf, sizeof buf, "\t%d\t-1\t%u\t%06x\n", m.pos, m.info, m.nucs);
             os << kv.first << buf;
         }
     return dump + os.str();
+}
+
+// Block(0, consensus): 8 codes per word, MSB nibble first (src/panman.cpp:246-257).
+std::vector<uint32_t> encode_block(const std::string& seq) {
+    std::vector<uint32_t> w;
+    for (size_t i = 0; i < seq.size(); i += 8) {
+        uint32_t x = 0;
+        for (size_t j = i; j < std::min(i + 8, seq.size()); ++j) x ^= (uint32_t)nuc_code(seq[j]) << (4 * (7 - (j - i)));
+        w.push_back(x);
+    }
+    return w;
 }
 
 }  // namespace
@@ -288,5 +252,79 @@ char* pm_msa_build(const char* newick, const char* msa_text, const char* referen
 }
 
 void pm_free(void* p) { std::free(p); }
+
+int pm_msa_to_panman(const char* newick, const char* msa_text, const char* reference, int mode, int device,
+                     const char* out_path, char* err, int64_t err_len) {
+    auto set_err = [&](const std::string& e) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+    };
+    if (!newick || !msa_text || !out_path || (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF)) {
+        set_err("bad arguments");
+        return PM_ERR_ARG;
+    }
+    pm::MsaResult r = pm::build_result(newick, msa_text, reference, mode, device);
+    if (!r.err.empty()) {
+        set_err(r.err);
+        return PM_ERR_ARG;
+    }
+    const int32_t N = (int32_t)r.t.name.size();
+    std::vector<int32_t> off(N + 1, 0), idx;
+    std::string names;
+    for (int32_t i = 0; i < N; ++i) {
+        idx.insert(idx.end(), r.t.kids[i].begin(), r.t.kids[i].end());
+        off[i + 1] = (int32_t)idx.size();
+        names += r.t.name[i];
+        names.push_back('\0');
+    }
+    const std::vector<uint32_t> words = pm::encode_block(r.consensus);
+    const int32_t block_primary = 0;
+    const int64_t seq_off[2] = {0, (int64_t)words.size()};
+    const int64_t gap_off[1] = {0};
+    std::vector<int64_t> bm_off(N + 1, 0), nm_off(N + 1, 0);
+    for (int32_t v = 0; v < N; ++v) bm_off[v + 1] = bm_off[v] + (v == r.t.root ? 1 : 0);
+    const int32_t bm_primary = 0;
+    const uint8_t bm_info = 1, bm_inv = 0;   // root: BlockMut(0, BI, false)
+    std::vector<int32_t> np, ns, npos, ngap;
+    std::vector<uint8_t> ninfo;
+    std::vector<uint32_t> nnucs;
+    for (int32_t v = 0; v < N; ++v) {
+        for (auto& m : r.muts.empty() ? std::vector<pm::Grouped>() : r.muts[v]) {
+            np.push_back(0);
+            ns.push_back(-1);
+            npos.push_back(m.pos);
+            ngap.push_back(-1);
+            ninfo.push_back((uint8_t)m.info);
+            nnucs.push_back(m.nucs);
+        }
+        nm_off[v + 1] = (int64_t)np.size();
+    }
+    pm_panmat p{};
+    p.num_nodes = N;
+    p.root = r.t.root;
+    p.child_offsets = off.data();
+    p.child_index = idx.data();
+    p.names = names.data();
+    p.num_blocks = 1;
+    p.block_primary = &block_primary;
+    p.block_seq_offsets = seq_off;
+    p.block_seq = words.data();
+    p.num_gaps = 0;
+    p.gap_offsets = gap_off;
+    p.block_mut_offsets = bm_off.data();
+    p.block_mut_primary = &bm_primary;
+    p.block_mut_info = &bm_info;
+    p.block_mut_inversion = &bm_inv;
+    p.nuc_mut_offsets = nm_off.data();
+    p.nuc_mut_primary = np.data();
+    p.nuc_mut_secondary = ns.data();
+    p.nuc_mut_position = npos.data();
+    p.nuc_mut_gap_position = ngap.data();
+    p.nuc_mut_info = ninfo.data();
+    p.nuc_mut_nucs = nnucs.data();
+    const pm_panmat* list[1] = {&p};
+    const int rc = pm_panman_write(out_path, list, 1, 1);
+    if (rc != PM_OK) set_err(std::string("cannot write ") + out_path);
+    return rc;
+}
 
 }  // extern "C"

@@ -1,0 +1,717 @@
+// pm_panman.cpp -- PanMAN file IO without the capnp library: xz (liblzma) + the standard
+// (unpacked) Cap'n Proto wire format, for the schema in panman.capnp.
+//
+// Reader: TreeGroup(istream) + Tree::protoMATToTree + assignMutationsToNodes
+//   (src/panman.cpp:6847-6877, :1661-1751, :576-618; NucMut / BlockMut from a reader:
+//   src/panman.hpp:192-210, :441-452).  Multi-segment messages, far and double-far
+//   pointers are followed; every offset is bounds-checked.
+// Writer: TreeGroup::writeToFile + Tree::getNodesPreorder (src/panman.cpp:6885-7015,
+//   :2854-2932), xz-compressed as writePanMAN does (src/panmanUtils.cpp:271-299).
+//
+// Struct layouts (data words, pointers) follow capnp's field allocation for panman.capnp:
+//   NucMut(2,0): nucPosition i32@0 nucGapPosition i32@32 nucGapExist bit64 mutInfo u32@96
+//   Mutation(2,1): blockId i64@0 blockGapExist bit64 blockMutExist bit65 blockMutInfo
+//     bit66 blockInversion bit67; ptr0 nucMutation
+//   Node(0,2) ConsensusSeqToBlockIds(0,4) GapList(2,2: blockId i64@0, blockGapExist bit64)
+//   BlockGapList(0,2) CircularOffset / RotationIndex(1,1: i32@0) SequenceInverted(1,1: bit0)
+//   Tree(0,8) TreeGroup(0,2) ComplexMutation(10,3)
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pm_internal.h"
+#include "pm_newick.h"
+
+// ---- liblzma (linked as liblzma.so.5; prototypes of its stable C ABI) ----------------
+extern "C" {
+struct pm_lzma_stream {
+    const uint8_t* next_in;
+    size_t avail_in;
+    uint64_t total_in;
+    uint8_t* next_out;
+    size_t avail_out;
+    uint64_t total_out;
+    const void* allocator;
+    void* internal;
+    void* reserved_ptr1;
+    void* reserved_ptr2;
+    void* reserved_ptr3;
+    void* reserved_ptr4;
+    uint64_t reserved_int1;
+    uint64_t reserved_int2;
+    size_t reserved_int3;
+    size_t reserved_int4;
+    int reserved_enum1;
+    int reserved_enum2;
+};
+int lzma_stream_decoder(pm_lzma_stream* strm, uint64_t memlimit, uint32_t flags);
+int lzma_easy_encoder(pm_lzma_stream* strm, uint32_t preset, int check);
+int lzma_code(pm_lzma_stream* strm, int action);
+void lzma_end(pm_lzma_stream* strm);
+}
+
+namespace pm {
+namespace {
+
+constexpr int kLzmaOk = 0, kLzmaStreamEnd = 1, kLzmaFinish = 3, kLzmaCheckCrc64 = 4;
+constexpr uint32_t kLzmaConcatenated = 0x08;
+
+bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
+    pm_lzma_stream s{};
+    if (lzma_stream_decoder(&s, UINT64_MAX, kLzmaConcatenated) != kLzmaOk) { err = "xz decoder init"; return false; }
+    out.resize(std::max<size_t>(in.size() * 4, 1 << 20));
+    s.next_in = in.data();
+    s.avail_in = in.size();
+    size_t done = 0;
+    for (;;) {
+        s.next_out = out.data() + done;
+        s.avail_out = out.size() - done;
+        const int rc = lzma_code(&s, kLzmaFinish);
+        done = out.size() - s.avail_out;
+        if (rc == kLzmaStreamEnd) break;
+        if (rc != kLzmaOk) { lzma_end(&s); err = "xz data error " + std::to_string(rc); return false; }
+        if (s.avail_out == 0) out.resize(out.size() * 2);
+        else if (s.avail_in == 0) { lzma_end(&s); err = "truncated xz stream"; return false; }
+    }
+    lzma_end(&s);
+    out.resize(done);
+    return true;
+}
+
+bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string& err) {
+    pm_lzma_stream s{};
+    if (lzma_easy_encoder(&s, 9, kLzmaCheckCrc64) != kLzmaOk) { err = "xz encoder init"; return false; }
+    out.resize(n / 2 + (1 << 16));
+    s.next_in = in;
+    s.avail_in = n;
+    size_t done = 0;
+    for (;;) {
+        s.next_out = out.data() + done;
+        s.avail_out = out.size() - done;
+        const int rc = lzma_code(&s, kLzmaFinish);
+        done = out.size() - s.avail_out;
+        if (rc == kLzmaStreamEnd) break;
+        if (rc != kLzmaOk) { lzma_end(&s); err = "xz encode error"; return false; }
+        if (s.avail_out == 0) out.resize(out.size() * 2);
+    }
+    lzma_end(&s);
+    out.resize(done);
+    return true;
+}
+
+// ---- Cap'n Proto reader ---------------------------------------------------------------
+struct Msg {
+    std::vector<uint8_t> bytes;
+    std::vector<const uint64_t*> seg;
+    std::vector<size_t> len;
+    std::string err;
+
+    bool init() {
+        if (bytes.size() < 8) return fail("message too short");
+        const uint32_t* h = reinterpret_cast<const uint32_t*>(bytes.data());
+        const size_t count = (size_t)h[0] + 1;
+        const size_t header = ((count + 1) * 4 + 7) / 8 * 8;
+        if (count > (1u << 20) || header > bytes.size()) return fail("bad segment table");
+        size_t at = header;
+        for (size_t i = 0; i < count; ++i) {
+            const size_t w = h[1 + i];
+            if (at + w * 8 > bytes.size()) return fail("segment beyond the message");
+            seg.push_back(reinterpret_cast<const uint64_t*>(bytes.data() + at));
+            len.push_back(w);
+            at += w * 8;
+        }
+        return true;
+    }
+    bool fail(const std::string& m) {
+        if (err.empty()) err = m;
+        return false;
+    }
+};
+
+struct Ref {   // where an object's content starts, after resolving far pointers
+    int32_t seg = -1;
+    size_t pos = 0;
+    uint64_t tag = 0;   // the pointer word describing the layout (offset field ignored)
+};
+
+struct Struct {
+    const Msg* m = nullptr;
+    int32_t seg = -1;
+    size_t data = 0;
+    uint16_t dwords = 0, ptrs = 0;
+
+    uint64_t word(int i) const { return i < dwords ? m->seg[seg][data + i] : 0; }
+    uint32_t u32(int bit) const { return (uint32_t)(word(bit / 64) >> (bit % 64)); }
+    int32_t i32(int bit) const { return (int32_t)u32(bit); }
+    int64_t i64(int bit) const { return (int64_t)word(bit / 64); }
+    bool flag(int bit) const { return (word(bit / 64) >> (bit % 64)) & 1u; }
+    bool has_ptr(int i) const { return i < ptrs; }
+    size_t ptr_pos(int i) const { return data + dwords + i; }
+};
+
+struct List {
+    const Msg* m = nullptr;
+    int32_t seg = -1;
+    size_t pos = 0;
+    int esize = 0;
+    uint32_t count = 0;
+    uint16_t dwords = 0, ptrs = 0;   // composite element layout
+
+    Struct at(uint32_t i) const {
+        Struct s;
+        s.m = m;
+        s.seg = seg;
+        s.data = pos + (size_t)i * (dwords + ptrs);
+        s.dwords = dwords;
+        s.ptrs = ptrs;
+        return s;
+    }
+    uint64_t raw(uint32_t i) const {   // primitive element i (bits / bytes / words)
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(m->seg[seg] + pos);
+        switch (esize) {
+            case 1: return (base[i / 8] >> (i % 8)) & 1u;
+            case 2: return base[i];
+            case 3: return reinterpret_cast<const uint16_t*>(base)[i];
+            case 4: return reinterpret_cast<const uint32_t*>(base)[i];
+            case 5: return reinterpret_cast<const uint64_t*>(base)[i];
+            default: return 0;
+        }
+    }
+};
+
+bool resolve(Msg& m, int32_t seg, size_t pos, Ref& out, bool& null) {
+    if (seg < 0 || (size_t)seg >= m.seg.size() || pos >= m.len[seg]) return m.fail("pointer outside its segment");
+    uint64_t w = m.seg[seg][pos];
+    null = w == 0;
+    if (null) return true;
+    const int kind = (int)(w & 3);
+    if (kind == 2) {   // far pointer
+        const bool dbl = (w >> 2) & 1;
+        const size_t pad = (size_t)((w >> 3) & 0x1FFFFFFF);
+        const uint32_t ps = (uint32_t)(w >> 32);
+        if (ps >= m.seg.size() || pad + (dbl ? 2 : 1) > m.len[ps]) return m.fail("bad far pointer");
+        if (!dbl) return resolve(m, (int32_t)ps, pad, out, null);
+        const uint64_t land = m.seg[ps][pad];
+        const uint64_t tag = m.seg[ps][pad + 1];
+        if ((land & 7) != 2) return m.fail("bad double-far landing pad");
+        const uint32_t ts = (uint32_t)(land >> 32);
+        const size_t tpos = (size_t)((land >> 3) & 0x1FFFFFFF);
+        if (ts >= m.seg.size() || tpos > m.len[ts]) return m.fail("bad double-far target");
+        out = Ref{(int32_t)ts, tpos, tag};
+        return true;
+    }
+    if (kind == 3) return m.fail("capability pointer in a PanMAN");
+    const int32_t off = (int32_t)(uint32_t)w >> 2;   // signed 30-bit word offset
+    const int64_t target = (int64_t)pos + 1 + off;
+    if (target < 0 || (size_t)target > m.len[seg]) return m.fail("pointer offset out of range");
+    out = Ref{seg, (size_t)target, w};
+    return true;
+}
+
+bool read_struct(Msg& m, int32_t seg, size_t pos, Struct& s) {
+    Ref r;
+    bool null = false;
+    if (!resolve(m, seg, pos, r, null)) return false;
+    s = Struct{};
+    s.m = &m;
+    if (null) return true;
+    if ((r.tag & 3) != 0) return m.fail("expected a struct pointer");
+    s.seg = r.seg;
+    s.data = r.pos;
+    s.dwords = (uint16_t)(r.tag >> 32);
+    s.ptrs = (uint16_t)(r.tag >> 48);
+    if (s.data + s.dwords + s.ptrs > m.len[s.seg]) return m.fail("struct beyond its segment");
+    return true;
+}
+
+bool read_list(Msg& m, int32_t seg, size_t pos, List& l) {
+    Ref r;
+    bool null = false;
+    if (!resolve(m, seg, pos, r, null)) return false;
+    l = List{};
+    l.m = &m;
+    if (null) return true;
+    if ((r.tag & 3) != 1) return m.fail("expected a list pointer");
+    l.seg = r.seg;
+    l.esize = (int)((r.tag >> 32) & 7);
+    const uint32_t n = (uint32_t)(r.tag >> 35);
+    if (l.esize == 7) {
+        if (r.pos >= m.len[r.seg]) return m.fail("composite tag outside the segment");
+        const uint64_t tag = m.seg[r.seg][r.pos];
+        l.count = (uint32_t)((uint32_t)tag >> 2);
+        l.dwords = (uint16_t)(tag >> 32);
+        l.ptrs = (uint16_t)(tag >> 48);
+        l.pos = r.pos + 1;
+        if ((uint64_t)l.count * (l.dwords + l.ptrs) > n || l.pos + n > m.len[r.seg]) return m.fail("bad composite list");
+    } else {
+        l.count = n;
+        l.pos = r.pos;
+        static const int bits[7] = {0, 1, 8, 16, 32, 64, 64};
+        const uint64_t words = ((uint64_t)n * bits[l.esize] + 63) / 64;
+        if (l.pos + words > m.len[r.seg]) return m.fail("list beyond its segment");
+        if (l.esize == 6) { l.dwords = 0; l.ptrs = 1; }
+    }
+    return true;
+}
+
+bool read_text(Msg& m, const Struct& s, int ptr, std::string& out) {
+    out.clear();
+    if (!s.has_ptr(ptr)) return true;
+    List l;
+    if (!read_list(m, s.seg, s.ptr_pos(ptr), l)) return false;
+    if (l.seg < 0) return true;
+    if (l.esize != 2) return m.fail("text is not a byte list");
+    const char* p = reinterpret_cast<const char*>(m.seg[l.seg] + l.pos);
+    out.assign(p, l.count > 0 ? l.count - 1 : 0);   // drop the NUL terminator
+    return true;
+}
+
+bool child_list(Msg& m, const Struct& s, int ptr, List& l) {
+    l = List{};
+    l.m = &m;
+    if (!s.has_ptr(ptr) || s.seg < 0) return true;
+    return read_list(m, s.seg, s.ptr_pos(ptr), l);
+}
+
+}  // namespace
+
+// One loaded tree, owning the arrays a pm_panmat view points into.
+struct PanmanTree {
+    std::string names_blob;
+    std::vector<int32_t> child_off, child_idx;
+    int32_t root = 0;
+    std::vector<int32_t> block_primary;
+    std::vector<int64_t> block_seq_off;
+    std::vector<uint32_t> block_seq;
+    std::vector<int32_t> gap_primary;
+    std::vector<int64_t> gap_off;
+    std::vector<uint32_t> gap_pos, gap_len;
+    std::vector<int64_t> bm_off;
+    std::vector<int32_t> bm_primary;
+    std::vector<uint8_t> bm_info, bm_inv;
+    std::vector<int64_t> nm_off;
+    std::vector<int32_t> nm_primary, nm_secondary, nm_pos, nm_gap;
+    std::vector<uint8_t> nm_info;
+    std::vector<uint32_t> nm_nucs;
+    std::vector<int32_t> circular, rotation;
+    std::vector<uint8_t> inverted;
+    std::string newick;
+    int32_t num_nodes = 0;
+
+    void view(pm_panmat& v) const {
+        v.num_nodes = num_nodes;
+        v.root = root;
+        v.child_offsets = child_off.data();
+        v.child_index = child_idx.data();
+        v.names = names_blob.data();
+        v.num_blocks = (int32_t)block_primary.size();
+        v.block_primary = block_primary.data();
+        v.block_seq_offsets = block_seq_off.data();
+        v.block_seq = block_seq.data();
+        v.num_gaps = (int32_t)gap_primary.size();
+        v.gap_primary = gap_primary.data();
+        v.gap_offsets = gap_off.data();
+        v.gap_position = gap_pos.data();
+        v.gap_length = gap_len.data();
+        v.block_mut_offsets = bm_off.data();
+        v.block_mut_primary = bm_primary.data();
+        v.block_mut_info = bm_info.data();
+        v.block_mut_inversion = bm_inv.data();
+        v.nuc_mut_offsets = nm_off.data();
+        v.nuc_mut_primary = nm_primary.data();
+        v.nuc_mut_secondary = nm_secondary.data();
+        v.nuc_mut_position = nm_pos.data();
+        v.nuc_mut_gap_position = nm_gap.data();
+        v.nuc_mut_info = nm_info.data();
+        v.nuc_mut_nucs = nm_nucs.data();
+        v.circular_offset = circular.data();
+        v.rotation_index = rotation.data();
+        v.sequence_inverted = inverted.data();
+    }
+};
+
+namespace {
+
+bool load_tree(Msg& m, const Struct& t, PanmanTree& out) {
+    // Newick -> nodes in pre-order (== the order of the stored node list)
+    if (!read_text(m, t, 0, out.newick)) return false;
+    Topology topo;
+    std::string err;
+    if (!parse_topology(out.newick, topo, err)) return m.fail("newick: " + err);
+    const int32_t N = (int32_t)topo.name.size();
+    out.num_nodes = N;
+    out.root = topo.root;
+    out.child_off.assign(N + 1, 0);
+    for (int32_t i = 0; i < N; ++i) {
+        out.child_idx.insert(out.child_idx.end(), topo.kids[i].begin(), topo.kids[i].end());
+        out.child_off[i + 1] = (int32_t)out.child_idx.size();
+    }
+    std::unordered_map<std::string, int32_t> index;
+    for (int32_t i = 0; i < N; ++i) {
+        out.names_blob += topo.name[i];
+        out.names_blob.push_back('\0');
+        index[topo.name[i]] = i;
+    }
+    // nodes: assignMutationsToNodes walks the tree in pre-order (src/panman.cpp:576-618)
+    List nodes;
+    if (!child_list(m, t, 1, nodes)) return false;
+    out.bm_off.assign(N + 1, 0);
+    out.nm_off.assign(N + 1, 0);
+    for (int32_t v = 0; v < N; ++v) {
+        if ((uint32_t)v < nodes.count) {
+            const Struct node = nodes.at((uint32_t)v);
+            List muts;
+            if (!child_list(m, node, 0, muts)) return false;
+            for (uint32_t k = 0; k < muts.count; ++k) {
+                const Struct mu = muts.at(k);
+                const int64_t block_id = mu.i64(0);
+                const bool gap_exist = mu.flag(64);
+                const int32_t primary = (int32_t)(block_id >> 32);
+                const int32_t secondary = gap_exist ? (int32_t)(block_id & 0xFFFFFFFF) : -1;
+                List nucs;
+                if (!child_list(m, mu, 0, nucs)) return false;
+                for (uint32_t j = 0; j < nucs.count; ++j) {
+                    const Struct nm = nucs.at(j);
+                    const uint32_t info = nm.u32(96);
+                    const uint32_t len = (info & 0xFF) >> 4;
+                    out.nm_primary.push_back(primary);
+                    out.nm_secondary.push_back(secondary);
+                    out.nm_pos.push_back(nm.i32(0));
+                    out.nm_gap.push_back(nm.flag(64) ? nm.i32(32) : -1);
+                    out.nm_info.push_back((uint8_t)(info & 0xFF));
+                    out.nm_nucs.push_back(len <= 6 ? (info >> 8) << (24 - 4 * len) : 0);
+                }
+                if (mu.flag(65)) {   // blockMutExist
+                    out.bm_primary.push_back(primary);
+                    out.bm_info.push_back(mu.flag(66));
+                    out.bm_inv.push_back(mu.flag(67));
+                }
+            }
+        }
+        out.bm_off[v + 1] = (int64_t)out.bm_primary.size();
+        out.nm_off[v + 1] = (int64_t)out.nm_primary.size();
+    }
+    // blocks in (primary, secondary) order (std::map, src/panman.cpp:1668-1724)
+    std::map<std::pair<int32_t, int32_t>, std::vector<uint32_t>> blocks;
+    List cmap;
+    if (!child_list(m, t, 2, cmap)) return false;
+    for (uint32_t k = 0; k < cmap.count; ++k) {
+        const Struct c = cmap.at(k);
+        List ids, seq, gapx;
+        if (!child_list(m, c, 0, ids) || !child_list(m, c, 1, seq) || !child_list(m, c, 2, gapx)) return false;
+        std::vector<uint32_t> words(seq.count);
+        for (uint32_t j = 0; j < seq.count; ++j) words[j] = (uint32_t)seq.raw(j);
+        for (uint32_t j = 0; j < ids.count; ++j) {
+            const int64_t id = (int64_t)ids.raw(j);
+            const bool gx = j < gapx.count && gapx.raw(j);
+            blocks[{(int32_t)(id >> 32), gx ? (int32_t)(id & 0xFFFFFFFF) : -1}] = words;
+        }
+    }
+    out.block_seq_off.push_back(0);
+    for (auto& b : blocks) {
+        out.block_primary.push_back(b.first.first);
+        out.block_seq.insert(out.block_seq.end(), b.second.begin(), b.second.end());
+        out.block_seq_off.push_back((int64_t)out.block_seq.size());
+    }
+    // gaps
+    List gaps;
+    if (!child_list(m, t, 3, gaps)) return false;
+    out.gap_off.push_back(0);
+    for (uint32_t k = 0; k < gaps.count; ++k) {
+        const Struct g = gaps.at(k);
+        List len, pos;
+        if (!child_list(m, g, 0, len) || !child_list(m, g, 1, pos)) return false;
+        out.gap_primary.push_back((int32_t)(g.i64(0) >> 32));
+        for (uint32_t j = 0; j < pos.count; ++j) {
+            out.gap_pos.push_back((uint32_t)pos.raw(j));
+            out.gap_len.push_back(j < len.count ? (uint32_t)len.raw(j) : 0);
+        }
+        out.gap_off.push_back((int64_t)out.gap_pos.size());
+    }
+    // circular offsets, rotation indexes, inversions (by sequence id)
+    out.circular.assign(N, -1);
+    out.rotation.assign(N, 0);
+    out.inverted.assign(N, 0);
+    for (int ptr = 5; ptr <= 7; ++ptr) {
+        List l;
+        if (!child_list(m, t, ptr, l)) return false;
+        for (uint32_t k = 0; k < l.count; ++k) {
+            const Struct e = l.at(k);
+            std::string id;
+            if (!read_text(m, e, 0, id)) return false;
+            auto it = index.find(id);
+            if (it == index.end()) continue;
+            if (ptr == 5) out.circular[it->second] = e.i32(0);
+            else if (ptr == 6) out.rotation[it->second] = e.i32(0);
+            else out.inverted[it->second] = e.flag(0);
+        }
+    }
+    return true;
+}
+
+// ---- Cap'n Proto writer (one segment) ---------------------------------------------------
+struct Writer {
+    std::vector<uint64_t> w{0};   // word 0: root pointer
+
+    size_t alloc(size_t words) {
+        const size_t at = w.size();
+        w.resize(at + words, 0);
+        return at;
+    }
+    void struct_ptr(size_t ptr, size_t target, uint16_t dwords, uint16_t ptrs) {
+        const int64_t off = (int64_t)target - (int64_t)(ptr + 1);
+        w[ptr] = ((uint64_t)(uint32_t)(off << 2)) | ((uint64_t)dwords << 32) | ((uint64_t)ptrs << 48);
+    }
+    void list_ptr(size_t ptr, size_t target, int esize, uint64_t count) {
+        const int64_t off = (int64_t)target - (int64_t)(ptr + 1);
+        w[ptr] = ((uint64_t)(uint32_t)(off << 2)) | 1u | ((uint64_t)esize << 32) | (count << 35);
+    }
+    // composite list of n structs; returns the position of element 0
+    size_t composite(size_t ptr, uint32_t n, uint16_t dwords, uint16_t ptrs) {
+        const size_t per = (size_t)dwords + ptrs;
+        const size_t tag = alloc(1 + per * n);
+        list_ptr(ptr, tag, 7, per * n);
+        w[tag] = ((uint64_t)n << 2) | ((uint64_t)dwords << 32) | ((uint64_t)ptrs << 48);
+        return tag + 1;
+    }
+    template <class T>
+    void prim_list(size_t ptr, const std::vector<T>& v, int esize) {
+        static const int bits[7] = {0, 1, 8, 16, 32, 64, 64};
+        const size_t words = (v.size() * bits[esize] + 63) / 64;
+        const size_t at = alloc(words);
+        uint8_t* base = reinterpret_cast<uint8_t*>(w.data() + at);
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (esize == 1) base[i / 8] |= (uint8_t)((v[i] ? 1 : 0) << (i % 8));
+            else std::memcpy(base + i * (bits[esize] / 8), &v[i], bits[esize] / 8);
+        }
+        list_ptr(ptr, at, esize, v.size());
+    }
+    void text(size_t ptr, const std::string& s) {
+        const size_t at = alloc((s.size() + 1 + 7) / 8);
+        std::memcpy(w.data() + at, s.data(), s.size());
+        list_ptr(ptr, at, 2, s.size() + 1);
+    }
+    void set_u32(size_t word, int bit, uint32_t v) { w[word + bit / 64] |= (uint64_t)v << (bit % 64); }
+    void set_i64(size_t word, int64_t v) { w[word] = (uint64_t)v; }
+    void set_bit(size_t word, int bit, bool v) {
+        if (v) w[word + bit / 64] |= 1ull << (bit % 64);
+    }
+};
+
+void write_tree(Writer& wr, size_t tree_pos, const pm_panmat& p) {
+    const int32_t N = p.num_nodes;
+    std::vector<std::string> names(N);
+    const char* nm = p.names;
+    for (int32_t i = 0; i < N; ++i) {
+        names[i] = nm;
+        nm += names[i].size() + 1;
+    }
+    Topology topo;
+    topo.name = names;
+    topo.kids.assign(N, {});
+    topo.root = p.root;
+    for (int32_t i = 0; i < N; ++i)
+        for (int32_t e = p.child_offsets[i]; e < p.child_offsets[i + 1]; ++e) topo.kids[i].push_back(p.child_index[e]);
+    // ptr slots of the Tree struct are at tree_pos + k (0 data words)
+    wr.text(tree_pos + 0, newick_of(topo));
+    // nodes in pre-order, plus the trailing empty node the reference writes (:6898)
+    std::vector<int32_t> pre;
+    std::vector<int32_t> st{p.root};
+    while (!st.empty()) {
+        const int32_t v = st.back();
+        st.pop_back();
+        pre.push_back(v);
+        for (int32_t e = p.child_offsets[v + 1] - 1; e >= p.child_offsets[v]; --e) st.push_back(p.child_index[e]);
+    }
+    const size_t nodes = wr.composite(tree_pos + 1, (uint32_t)N + 1, 0, 2);
+    for (int32_t k = 0; k < N; ++k) {
+        const int32_t v = pre[k];
+        const size_t node = nodes + (size_t)k * 2;
+        // group by (primary, secondary) in std::map order (:2857-2887)
+        struct Group { std::vector<int64_t> nucs; int block = 2; bool inv = false; };
+        std::map<std::pair<int32_t, int32_t>, Group> groups;
+        for (int64_t i = p.nuc_mut_offsets[v]; i < p.nuc_mut_offsets[v + 1]; ++i)
+            groups[{p.nuc_mut_primary[i], p.nuc_mut_secondary ? p.nuc_mut_secondary[i] : -1}].nucs.push_back(i);
+        for (int64_t i = p.block_mut_offsets[v]; i < p.block_mut_offsets[v + 1]; ++i) {
+            Group& g = groups[{p.block_mut_primary[i], -1}];
+            g.block = p.block_mut_info[i] ? 1 : 0;
+            g.inv = p.block_mut_inversion[i] != 0;
+        }
+        const size_t muts = wr.composite(node + 0, (uint32_t)groups.size(), 2, 1);
+        size_t gi = 0;
+        for (auto& kv : groups) {
+            const size_t mu = muts + gi++ * 3;
+            const int32_t prim = kv.first.first, sec = kv.first.second;
+            wr.set_i64(mu, sec != -1 ? ((int64_t)prim << 32) + sec : ((int64_t)prim << 32));
+            wr.set_bit(mu, 64, sec != -1);
+            wr.set_bit(mu, 65, kv.second.block != 2);
+            wr.set_bit(mu, 66, kv.second.block != 0);   // setBlockMutInfo(2) stores true (:2889)
+            wr.set_bit(mu, 67, kv.second.block != 2 ? kv.second.inv : true);
+            const size_t nl = wr.composite(mu + 2, (uint32_t)kv.second.nucs.size(), 2, 0);
+            for (size_t j = 0; j < kv.second.nucs.size(); ++j) {
+                const int64_t i = kv.second.nucs[j];
+                const size_t rec = nl + j * 2;
+                const uint32_t info = p.nuc_mut_info[i];
+                const uint32_t len = info >> 4;
+                const uint32_t disk = len <= 6 ? (((p.nuc_mut_nucs[i] >> (24 - 4 * len)) << 8) + info) : info;
+                wr.set_u32(rec, 0, (uint32_t)p.nuc_mut_position[i]);
+                if (p.nuc_mut_gap_position[i] != -1) {
+                    wr.set_u32(rec, 32, (uint32_t)p.nuc_mut_gap_position[i]);
+                    wr.set_bit(rec, 64, true);
+                }
+                wr.set_u32(rec, 96, disk);
+            }
+        }
+        wr.composite(node + 1, 0, 0, 1);   // annotations: empty list of text
+    }
+    // consensusSeqMap: blocks grouped by identical consensus words, in map order
+    std::map<std::vector<uint32_t>, std::vector<int64_t>> by_seq;
+    for (int32_t b = 0; b < p.num_blocks; ++b) {
+        std::vector<uint32_t> words(p.block_seq + p.block_seq_offsets[b], p.block_seq + p.block_seq_offsets[b + 1]);
+        by_seq[words].push_back((int64_t)p.block_primary[b] << 32);
+    }
+    const size_t cm = wr.composite(tree_pos + 2, (uint32_t)by_seq.size(), 0, 4);
+    size_t ci = 0;
+    for (auto& kv : by_seq) {
+        const size_t c = cm + ci++ * 4;
+        wr.prim_list(c + 0, kv.second, 5);
+        wr.prim_list(c + 1, kv.first, 4);
+        wr.prim_list(c + 2, std::vector<uint8_t>(kv.second.size(), 0), 1);
+        wr.composite(c + 3, 0, 0, 1);   // chromosomeName: empty
+    }
+    // gaps
+    const size_t gl = wr.composite(tree_pos + 3, (uint32_t)p.num_gaps, 2, 2);
+    for (int32_t g = 0; g < p.num_gaps; ++g) {
+        const size_t e = gl + (size_t)g * 4;
+        wr.set_i64(e, (int64_t)p.gap_primary[g] << 32);
+        std::vector<int32_t> len, pos;
+        for (int64_t k = p.gap_offsets[g]; k < p.gap_offsets[g + 1]; ++k) {
+            len.push_back((int32_t)p.gap_length[k]);
+            pos.push_back((int32_t)p.gap_position[k]);
+        }
+        wr.prim_list(e + 2, len, 4);
+        wr.prim_list(e + 3, pos, 4);
+    }
+    // blockGaps (ptr 4) is not written by TreeGroup::writeToFile: left null
+    // circular / rotation / inverted
+    std::vector<int32_t> circ, rot, inv;
+    for (int32_t i = 0; i < N; ++i) {
+        if (p.circular_offset && p.circular_offset[i] >= 0) circ.push_back(i);
+        if (p.rotation_index && p.rotation_index[i] != 0) rot.push_back(i);
+        if (p.sequence_inverted && p.sequence_inverted[i]) inv.push_back(i);
+    }
+    const size_t co = wr.composite(tree_pos + 5, (uint32_t)circ.size(), 1, 1);
+    for (size_t k = 0; k < circ.size(); ++k) {
+        wr.set_u32(co + k * 2, 0, (uint32_t)p.circular_offset[circ[k]]);
+        wr.text(co + k * 2 + 1, names[circ[k]]);
+    }
+    const size_t ro = wr.composite(tree_pos + 6, (uint32_t)rot.size(), 1, 1);
+    for (size_t k = 0; k < rot.size(); ++k) {
+        wr.set_u32(ro + k * 2, 0, (uint32_t)p.rotation_index[rot[k]]);
+        wr.text(ro + k * 2 + 1, names[rot[k]]);
+    }
+    const size_t io = wr.composite(tree_pos + 7, (uint32_t)inv.size(), 1, 1);
+    for (size_t k = 0; k < inv.size(); ++k) {
+        wr.set_bit(io + k * 2, 0, true);
+        wr.text(io + k * 2 + 1, names[inv[k]]);
+    }
+}
+
+}  // namespace
+}  // namespace pm
+
+struct pm_panman {
+    std::vector<pm::PanmanTree> trees;
+    std::string err;
+};
+
+using namespace pm;
+
+extern "C" {
+
+int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len) {
+    auto set_err = [&](const std::string& e) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+    };
+    if (!path || !out) return PM_ERR_ARG;
+    *out = nullptr;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return PM_ERR_ARG; }
+    std::vector<uint8_t> raw;
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
+    std::fclose(f);
+    Msg m;
+    std::string e;
+    const bool is_xz = raw.size() >= 6 && raw[0] == 0xFD && raw[1] == '7' && raw[2] == 'z' && raw[3] == 'X';
+    if (is_xz) {
+        if (!xz_decode(raw, m.bytes, e)) { set_err(e); return PM_ERR_ARG; }
+    } else {
+        m.bytes.swap(raw);   // an uncompressed capnp message is accepted too
+    }
+    if (!m.init()) { set_err(m.err); return PM_ERR_ARG; }
+    Struct tg;
+    if (!read_struct(m, 0, 0, tg)) { set_err(m.err); return PM_ERR_ARG; }
+    List trees;
+    if (!child_list(m, tg, 0, trees)) { set_err(m.err); return PM_ERR_ARG; }
+    auto* pm_ = new pm_panman();
+    pm_->trees.resize(trees.count);
+    for (uint32_t t = 0; t < trees.count; ++t)
+        if (!load_tree(m, trees.at(t), pm_->trees[t])) {
+            set_err(m.err);
+            delete pm_;
+            return PM_ERR_ARG;
+        }
+    *out = pm_;
+    return PM_OK;
+}
+
+int pm_panman_tree_count(const pm_panman* p) { return p ? (int)p->trees.size() : 0; }
+
+int pm_panman_tree(const pm_panman* p, int index, pm_panmat* view) {
+    if (!p || !view || index < 0 || index >= (int)p->trees.size()) return PM_ERR_ARG;
+    p->trees[index].view(*view);
+    return PM_OK;
+}
+
+const char* pm_panman_newick(const pm_panman* p, int index) {
+    if (!p || index < 0 || index >= (int)p->trees.size()) return nullptr;
+    return p->trees[index].newick.c_str();
+}
+
+void pm_panman_free(pm_panman* p) { delete p; }
+
+int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, int compress) {
+    if (!path || (!trees && count > 0) || count < 0) return PM_ERR_ARG;
+    Writer wr;
+    const size_t tg = wr.alloc(2);
+    wr.struct_ptr(0, tg, 0, 2);
+    const size_t tl = wr.composite(tg + 0, (uint32_t)count, 0, 8);
+    for (int t = 0; t < count; ++t) write_tree(wr, tl + (size_t)t * 8, *trees[t]);
+    wr.composite(tg + 1, 0, 10, 3);   // complexMutations: none
+    std::vector<uint8_t> msg(8 + wr.w.size() * 8);
+    const uint32_t hdr[2] = {0, (uint32_t)wr.w.size()};
+    std::memcpy(msg.data(), hdr, 8);
+    std::memcpy(msg.data() + 8, wr.w.data(), wr.w.size() * 8);
+    std::vector<uint8_t> outb;
+    std::string e;
+    if (compress) {
+        if (!xz_encode(msg.data(), msg.size(), outb, e)) return PM_ERR_HIP;
+    } else {
+        outb.swap(msg);
+    }
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return PM_ERR_ARG;
+    const bool ok = std::fwrite(outb.data(), 1, outb.size(), f) == outb.size();
+    std::fclose(f);
+    return ok ? PM_OK : PM_ERR_ARG;
+}
+
+}  // extern "C"

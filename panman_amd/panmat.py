@@ -25,7 +25,7 @@ def encode_block(seq: str) -> list[int]:
 class PanmatStruct(C.Structure):
     _fields_ = [
         ("num_nodes", C.c_int32), ("root", C.c_int32),
-        ("child_offsets", C.c_void_p), ("child_index", C.c_void_p), ("names", C.c_char_p),
+        ("child_offsets", C.c_void_p), ("child_index", C.c_void_p), ("names", C.c_void_p),
         ("num_blocks", C.c_int32), ("block_primary", C.c_void_p), ("block_seq_offsets", C.c_void_p),
         ("block_seq", C.c_void_p),
         ("num_gaps", C.c_int32), ("gap_primary", C.c_void_p), ("gap_offsets", C.c_void_p),
@@ -104,8 +104,9 @@ class PanMAT:
             keep.append(a)
             return a.ctypes.data
 
-        blob = b"".join(n.encode() + b"\0" for n in self.names)
+        blob = C.create_string_buffer(b"".join(n.encode() + b"\0" for n in self.names) or b"\0")
         keep.append(blob)
+        blob = C.addressof(blob)
         a = getattr(self, "_arrays", None)
         if a is not None:
             return PanmatStruct(
@@ -173,3 +174,98 @@ def from_msa_dump(dump: str, names, child_offsets, child_index, root) -> PanMAT:
         else:
             pm.add_nuc_mut_raw(index[f[0]], 0, int(f[1]), int(f[2]), int(f[3]), int(f[4], 16))
     return pm
+
+
+class PanmanFile:
+    """A loaded .panman (libpanman_amd: xz + Cap'n Proto reader, host only)."""
+
+    def __init__(self, path: str):
+        from ._lib import PanmanError, load
+        self.lib = load()
+        self.h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = self.lib.pm_panman_load(path.encode(), C.byref(self.h), err, 512)
+        if rc != 0:
+            raise PanmanError(f"pm_panman_load({path}): {err.value.decode()}")
+
+    def __len__(self):
+        return self.lib.pm_panman_tree_count(self.h)
+
+    def view(self, i: int = 0) -> PanmatStruct:
+        v = PanmatStruct()
+        if self.lib.pm_panman_tree(self.h, i, C.byref(v)) != 0:
+            raise IndexError(i)
+        return v
+
+    def newick(self, i: int = 0) -> str:
+        return self.lib.pm_panman_newick(self.h, i).decode()
+
+    def to_panmat(self, i: int = 0) -> PanMAT:
+        """Copy tree i into a PanMAT (numpy arrays)."""
+        v = self.view(i)
+        n = v.num_nodes
+
+        def a(ptr, dt, count):
+            if count == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(count,)).copy()
+        off = a(v.child_offsets, np.int32, n + 1)
+        idx = a(v.child_index, np.int32, n - 1)
+        blob = b""
+        p = v.names
+        for _ in range(n):
+            s = C.string_at(p)
+            blob += s + b"\0"
+            p += len(s) + 1
+        names = [x.decode() for x in blob.split(b"\0")[:n]]
+        pm = PanMAT(names, off, idx, v.root)
+        bo = a(v.block_seq_offsets, np.int64, v.num_blocks + 1)
+        go = a(v.gap_offsets, np.int64, v.num_gaps + 1)
+        bmo = a(v.block_mut_offsets, np.int64, n + 1)
+        nmo = a(v.nuc_mut_offsets, np.int64, n + 1)
+        pm.set_arrays(
+            block_primary=a(v.block_primary, np.int32, v.num_blocks), block_seq_offsets=bo,
+            block_seq=a(v.block_seq, np.uint32, int(bo[-1])), gap_primary=a(v.gap_primary, np.int32, v.num_gaps),
+            gap_offsets=go, gap_position=a(v.gap_position, np.uint32, int(go[-1])),
+            gap_length=a(v.gap_length, np.uint32, int(go[-1])), block_mut_offsets=bmo,
+            block_mut_primary=a(v.block_mut_primary, np.int32, int(bmo[-1])),
+            block_mut_info=a(v.block_mut_info, np.uint8, int(bmo[-1])),
+            block_mut_inversion=a(v.block_mut_inversion, np.uint8, int(bmo[-1])), nuc_mut_offsets=nmo,
+            nuc_mut_primary=a(v.nuc_mut_primary, np.int32, int(nmo[-1])),
+            nuc_mut_secondary=a(v.nuc_mut_secondary, np.int32, int(nmo[-1])),
+            nuc_mut_position=a(v.nuc_mut_position, np.int32, int(nmo[-1])),
+            nuc_mut_gap_position=a(v.nuc_mut_gap_position, np.int32, int(nmo[-1])),
+            nuc_mut_info=a(v.nuc_mut_info, np.uint8, int(nmo[-1])),
+            nuc_mut_nucs=a(v.nuc_mut_nucs, np.uint32, int(nmo[-1])))
+        pm.circular = a(v.circular_offset, np.int32, n)
+        pm.rotation = a(v.rotation_index, np.int32, n)
+        pm.inverted = a(v.sequence_inverted, np.uint8, n)
+        return pm
+
+    def close(self):
+        if self.h:
+            self.lib.pm_panman_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def write_panman(path: str, panmats: list, compress: bool = True):
+    """TreeGroup::writeToFile + writePanMAN (xz level 9) for PanMATs."""
+    from ._lib import PanmanError, load
+    lib = load()
+    structs, keep = [], []
+    for pm in panmats:
+        st, k = pm.as_struct()
+        structs.append(st)
+        keep.append(k)
+    arr = (C.c_void_p * max(1, len(structs)))(*[C.cast(C.pointer(s), C.c_void_p) for s in structs])
+    rc = lib.pm_panman_write(path.encode(), arr, len(structs), int(compress))
+    del keep
+    if rc != 0:
+        raise PanmanError(f"pm_panman_write({path}) failed ({rc})")

@@ -79,6 +79,40 @@ def test_msa_to_fasta_round_trip_on_gpu(engine, oracle):
     assert parse_records(engine.fasta(pm, True)) == rows
 
 
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_msa_to_panman_file_round_trip(engine, oracle, tmp_path, mode):
+    """MSA -> pm_msa_to_panman (GPU build + writer) -> .panman -> loader -> pm_fasta
+    reproduces the alignment rows; the file's tree equals the in-memory dump's."""
+    rng = np.random.default_rng(78 + mode)
+    off, idx, root = random_tree(60, rng, max_children=4)
+    names = names_for(off)
+    nwk = to_newick(off, idx, root, names)
+    base = rng.choice(list("ACGT"), size=517)
+    rows = {}
+    for i in range(len(names)):
+        if off[i] == off[i + 1]:
+            s = base.copy()
+            f = rng.random(517) < 0.1
+            s[f] = rng.choice(list("ACGTRN-"), size=f.sum())
+            rows[names[i]] = "".join(s)
+    msa = "".join(f">{k}\n{v}\n" for k, v in rows.items())
+    ref = next(iter(rows)) if mode == panman_amd.MODE_SANKOFF else ""
+    path = str(tmp_path / "t.panman")
+    panman_amd.msa_to_panman(nwk, msa, path, ref, mode)
+    f = panman_amd.PanmanFile(path)
+    try:
+        assert len(f) == 1
+        got = parse_records(engine.fasta(f.view(0), True))
+        assert got == rows
+        unal = parse_records(engine.fasta(f.view(0), False))
+        assert unal == {k: v.replace("-", "") for k, v in rows.items()}
+        pnames, poff, pidx, proot = parse_newick(nwk)
+        pm = from_msa_dump(panman_amd.msa_build(nwk, msa, ref, mode), pnames, poff, pidx, proot)
+        assert _records(engine.fasta(pm, True)) == _records(engine.fasta(f.view(0), True))
+    finally:
+        f.close()
+
+
 @pytest.mark.parametrize("aligned", [True, False])
 def test_c5_like_panmat_vs_oracle(engine, oracle, aligned):
     """Bulk generator (bench workload family C5) at reduced size, every leaf compared."""
