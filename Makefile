@@ -6,8 +6,9 @@ SRC := $(wildcard panman_amd/csrc/*.cpp) $(wildcard panman_amd/csrc/*.hip)
 HDR := $(wildcard panman_amd/csrc/*.h) include/panman_gpu.h
 OBJ := $(patsubst panman_amd/csrc/%,build/%.o,$(SRC))
 LIB := panman_amd/libpanman_amd.so
+CLI := bin/panmanUtils
 
-all: $(LIB) oracle
+all: $(LIB) $(CLI) oracle
 
 build/%.o: panman_amd/csrc/% $(HDR)
 	@mkdir -p build
@@ -16,11 +17,17 @@ build/%.o: panman_amd/csrc/% $(HDR)
 $(LIB): $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ) -l:liblzma.so.5
 
+# panmanUtils-compatible CLI (host C++ over the C-ABI; finds the library next to the package)
+$(CLI): panman_amd/csrc/cli/panmanUtils.cpp include/panman_gpu.h $(LIB)
+	@mkdir -p bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lpanman_amd -l:libpanman_amd.so \
+	    -Wl,-rpath,'$$ORIGIN/../panman_amd'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build bin $(LIB)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,0 +1,268 @@
+// panmanUtils-compatible command line for the GPU path (src/panmanUtils.cpp:128-182 option
+// table, :1302-1325 PanMAN load, :1409-1465 MSA build, :271-299 writePanMAN, :385-415 and
+// :458-490 FASTA / aligned FASTA, :766-786 Newick).  Only the commands on the accelerated
+// path are implemented; any other reference command is rejected with a message.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "panman_gpu.h"
+
+namespace {
+
+using Clock = std::chrono::high_resolution_clock;
+
+long long ns_since(Clock::time_point t0) {
+    return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+}
+
+struct Options {
+    std::map<std::string, std::string> values;   // long name -> value ("" for flags)
+    bool has(const char* k) const { return values.count(k) != 0; }
+    const std::string& get(const char* k) const { return values.at(k); }
+};
+
+struct Spec {
+    const char* name;
+    char shortc;
+    bool takes_value;
+    const char* help;
+};
+
+const Spec kSpecs[] = {
+    {"help", 'h', false, "Print help messages"},
+    {"input-panman", 'I', true, "Input PanMAN file path"},
+    {"input-msa", 'M', true, "Input MSA file (FASTA format) to build a PanMAN"},
+    {"input-newick", 'N', true, "Input tree topology as Newick string"},
+    {"newick", 't', false, "Print newick string of all trees in a PanMAN"},
+    {"fasta", 'f', false, "Print tip sequences (FASTA format)"},
+    {"fasta-aligned", 'm', false, "Print MSA of sequences for each PanMAT in a PanMAN (FASTA format)"},
+    {"low-mem-mode", 0, false, "Build with the Sankoff driver (the reference's batched low-memory mode)"},
+    {"reference", 'n', true, "Identifier of reference sequence for PanMAN construction (optional)"},
+    {"output-file", 'o', true, "Prefix of the output file name"},
+    {"threads", 0, true, "Accepted for compatibility (the build runs on the GPU)"},
+    {"device", 0, true, "HIP device ordinal (default 0)"},
+};
+
+// Reference commands outside the accelerated path: recognised so the error is explicit.
+const char* const kOther[] = {"input-pangraph", "input-gfa", "impute", "create-network", "printTips",
+                              "summary", "subnet", "vcf", "gfa", "maf", "annotate", "reroot",
+                              "aa-translation", "extended-newick", "printMutations", "acr", "index",
+                              "toUsher"};
+
+void usage(std::ostream& os) {
+    os << "Allowed options:\n";
+    for (const Spec& s : kSpecs) {
+        std::string flag = "  --" + std::string(s.name);
+        if (s.shortc) flag += std::string(" [ -") + s.shortc + " ]";
+        if (s.takes_value) flag += " arg";
+        os << flag << std::string(flag.size() < 36 ? 36 - flag.size() : 1, ' ') << s.help << "\n";
+    }
+}
+
+const Spec* find_long(const std::string& n) {
+    for (const Spec& s : kSpecs)
+        if (n == s.name) return &s;
+    return nullptr;
+}
+
+const Spec* find_short(char c) {
+    for (const Spec& s : kSpecs)
+        if (s.shortc == c) return &s;
+    return nullptr;
+}
+
+bool parse(int argc, char** argv, Options& o, std::string& err) {
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        const Spec* s = nullptr;
+        std::string inline_value;
+        bool has_inline = false;
+        if (a.rfind("--", 0) == 0) {
+            std::string n = a.substr(2);
+            const size_t eq = n.find('=');
+            if (eq != std::string::npos) {
+                inline_value = n.substr(eq + 1);
+                n.resize(eq);
+                has_inline = true;
+            }
+            s = find_long(n);
+            if (!s) {
+                for (const char* other : kOther)
+                    if (n == other) {
+                        err = "--" + n + " is not part of the GPU path of this build";
+                        return false;
+                    }
+                err = "unrecognised option '" + a + "'";
+                return false;
+            }
+        } else if (a.size() >= 2 && a[0] == '-') {
+            s = find_short(a[1]);
+            if (!s) {
+                err = "unrecognised option '" + a + "'";
+                return false;
+            }
+            if (a.size() > 2) {
+                inline_value = a.substr(2);
+                has_inline = true;
+            }
+        } else {
+            o.values["input-panman"] = a;   // positional argument (src/panmanUtils.cpp:183)
+            continue;
+        }
+        if (s->takes_value) {
+            if (has_inline) {
+                o.values[s->name] = inline_value;
+            } else if (i + 1 < argc) {
+                o.values[s->name] = argv[++i];
+            } else {
+                err = std::string("the required argument for option '--") + s->name + "' is missing";
+                return false;
+            }
+        } else {
+            o.values[s->name] = "";
+        }
+    }
+    return true;
+}
+
+bool read_file(const std::string& path, std::string& out) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return false;
+    std::ostringstream ss;
+    ss << in.rdbuf();
+    out = ss.str();
+    return true;
+}
+
+void print_error(const std::string& e) { std::cerr << "\033[1;31mError: " << e << "\033[0m\n"; }
+
+int build_from_msa(const Options& o, int device) {
+    if (!o.has("input-newick")) {
+        print_error("File containing newick string not provided!");
+        return 1;
+    }
+    if (!o.has("output-file")) {
+        print_error("Output file not provided!");
+        usage(std::cout);
+        return 1;
+    }
+    std::string msa, newick;
+    if (!read_file(o.get("input-msa"), msa)) {
+        print_error("cannot read " + o.get("input-msa"));
+        return 1;
+    }
+    if (!read_file(o.get("input-newick"), newick)) {
+        print_error("cannot read " + o.get("input-newick"));
+        return 1;
+    }
+    const std::string ref = o.has("reference") ? o.get("reference") : "";
+    const int mode = o.has("low-mem-mode") ? PM_MODE_SANKOFF : PM_MODE_FITCH;
+    std::cout << "Creating PanMAN from MSA and Newick" << std::endl;
+    ::mkdir("./panman", 0777);
+    const std::string out = "./panman/" + o.get("output-file") + ".panman";
+    const auto t0 = Clock::now();
+    char err[512] = {0};
+    const int rc = pm_msa_to_panman(newick.c_str(), msa.c_str(), ref.c_str(), mode, device, out.c_str(), err,
+                                    sizeof err);
+    if (rc != PM_OK) {
+        print_error(err[0] ? err : "PanMAN construction failed");
+        return 1;
+    }
+    // Construction and the xz write are one call here; both lines report its time.
+    const long long t = ns_since(t0);
+    std::cout << "Data load time: " << t << " nanoseconds \n";
+    std::cout << "Writing PanMAN" << std::endl;
+    std::cout << "\nNetwork Write execution time: " << t << " nanoseconds\n";
+    return 0;
+}
+
+int from_panman(const Options& o, int device) {
+    const std::string path = o.get("input-panman");
+    std::cout << "starting reading panman" << std::endl;
+    const auto t0 = Clock::now();
+    pm_panman* file = nullptr;
+    char err[512] = {0};
+    if (pm_panman_load(path.c_str(), &file, err, sizeof err) != PM_OK) {
+        print_error(err[0] ? err : ("cannot load " + path));
+        return 1;
+    }
+    std::cout << "Data load time: " << ns_since(t0) << " nanoseconds \n";
+    ::mkdir("./info", 0777);
+    const int trees = pm_panman_tree_count(file);
+    const bool to_file = o.has("output-file");
+    auto sink = [&](const char* ext, int i, const char* data, size_t n) -> bool {
+        if (!to_file) {
+            std::cout.write(data, (std::streamsize)n);
+            return true;
+        }
+        const std::string p = "./info/" + o.get("output-file") + "_" + std::to_string(i) + ext;
+        std::ofstream f(p, std::ios::binary);
+        f.write(data, (std::streamsize)n);
+        return (bool)f;
+    };
+    int status = 0;
+    if (o.has("newick")) {
+        for (int i = 0; i < trees; ++i) {
+            std::string s = pm_panman_newick(file, i);
+            s += "\n";
+            if (!sink(".newick", i, s.data(), s.size())) status = 1;
+        }
+    }
+    for (int aligned = 0; aligned < 2 && status == 0; ++aligned) {
+        if (!o.has(aligned ? "fasta-aligned" : "fasta")) continue;
+        pm_ctx* ctx = nullptr;
+        if (pm_create(device, &ctx) != PM_OK) {
+            print_error("no HIP device");
+            status = 1;
+            break;
+        }
+        const auto f0 = Clock::now();
+        for (int i = 0; i < trees && status == 0; ++i) {
+            pm_panmat view;
+            char* text = nullptr;
+            int64_t len = 0;
+            if (pm_panman_tree(file, i, &view) != PM_OK || pm_fasta(ctx, &view, aligned, &text, &len) != PM_OK) {
+                print_error(pm_last_error(ctx));
+                status = 1;
+                break;
+            }
+            if (!sink(aligned ? ".msa" : ".fasta", i, text, (size_t)len)) status = 1;
+            pm_free(text);
+        }
+        std::cout << "\nFASTA execution time: " << ns_since(f0) << " nanoseconds\n";
+        pm_destroy(ctx);
+    }
+    pm_panman_free(file);
+    return status;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options o;
+    std::string err;
+    if (!parse(argc, argv, o, err)) {
+        print_error(err);
+        usage(std::cerr);
+        return 1;
+    }
+    if (o.has("help") || argc == 1) {
+        usage(std::cout);
+        return 0;
+    }
+    const int device = o.has("device") ? std::atoi(o.get("device").c_str()) : 0;
+    if (o.has("input-msa")) return build_from_msa(o, device);
+    if (o.has("input-panman")) return from_panman(o, device);
+    print_error("no input: give -I <file.panman> or -M <msa> -N <newick>");
+    usage(std::cerr);
+    return 1;
+}

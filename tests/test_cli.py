@@ -1,0 +1,92 @@
+"""panmanUtils-compatible CLI (bin/panmanUtils, src/panmanUtils.cpp:128-182, :271-299,
+:385-490, :766-786).  Host commands run here; -M builds and -f/-m replays need the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from _panmat import parse_records, random_panmat
+from _trees import names_for, random_tree, to_newick
+from panman_amd.panmat import PanmanFile, write_panman
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "bin", "panmanUtils")
+
+
+def _run(args, cwd):
+    if not os.path.exists(CLI):
+        pytest.fail(f"{CLI} missing: run `make`")
+    return subprocess.run([CLI] + args, cwd=cwd, capture_output=True, text=True, timeout=300)
+
+
+def test_help_and_unknown_commands(tmp_path):
+    r = _run(["-h"], tmp_path)
+    assert r.returncode == 0 and "--input-panman" in r.stdout and "--fasta-aligned" in r.stdout
+    r = _run(["x.panman", "--vcf"], tmp_path)
+    assert r.returncode != 0 and "not part of the GPU path" in r.stderr
+    r = _run(["--bogus"], tmp_path)
+    assert r.returncode != 0 and "unrecognised option" in r.stderr
+    r = _run(["-M", "a.fa", "-o", "x"], tmp_path)
+    assert r.returncode != 0 and "newick string not provided" in r.stderr
+
+
+def test_newick_to_info_file_and_stdout(tmp_path):
+    rng = np.random.default_rng(3)
+    off, idx, root = random_tree(25, rng, max_children=3)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2)
+    path = str(tmp_path / "in.panman")
+    write_panman(path, [pm, pm])
+    f = PanmanFile(path)
+    want = [f.newick(0), f.newick(1)]
+    f.close()
+    r = _run(["-I", path, "-t", "-o", "out"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Data load time:" in r.stdout
+    for i in range(2):
+        assert open(tmp_path / "info" / f"out_{i}.newick").read() == want[i] + "\n"
+    r = _run([path, "--newick"], tmp_path)   # positional input file, output to stdout
+    assert r.returncode == 0 and r.stdout.count(want[0] + "\n") == 2
+
+
+def test_corrupt_input_is_an_error(tmp_path):
+    p = tmp_path / "bad.panman"
+    p.write_bytes(b"\xfd7zXZ\x00garbage")
+    r = _run(["-I", str(p), "-t"], tmp_path)
+    assert r.returncode != 0 and "Error" in r.stderr
+
+
+def _msa_case(rng, n, width):
+    off, idx, root = random_tree(n, rng, max_children=3)
+    names = names_for(off)
+    base = rng.choice(list("ACGT"), size=width)
+    rows = {}
+    for i in range(len(names)):
+        if off[i] == off[i + 1]:
+            s = base.copy()
+            f = rng.random(width) < 0.12
+            s[f] = rng.choice(list("ACGTN-"), size=f.sum())
+            rows[names[i]] = "".join(s)
+    return to_newick(off, idx, root, names), rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("low_mem", [False, True])
+def test_msa_build_then_fasta(tmp_path, low_mem):
+    rng = np.random.default_rng(12 + low_mem)
+    nwk, rows = _msa_case(rng, 45, 401)
+    (tmp_path / "t.nwk").write_text(nwk + "\n")
+    (tmp_path / "a.fa").write_text("".join(f">{k}\n{v}\n" for k, v in rows.items()))
+    args = ["-M", "a.fa", "-N", "t.nwk", "-o", "demo"]
+    if low_mem:
+        args += ["--low-mem-mode", "-n", next(iter(rows))]
+    r = _run(args, tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(tmp_path / "panman" / "demo.panman")
+    r = _run(["-I", "panman/demo.panman", "-m", "-o", "demo"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert parse_records(open(tmp_path / "info" / "demo_0.msa").read()) == rows
+    r = _run(["-I", "panman/demo.panman", "-f"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    text = r.stdout[r.stdout.index(">"):r.stdout.index("\nFASTA execution time")]
+    assert parse_records(text) == {k: v.replace("-", "") for k, v in rows.items()}
