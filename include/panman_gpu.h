@@ -181,6 +181,7 @@ typedef struct pm_panmat {
     const int32_t* circular_offset;  /* nullable [num_nodes]; < 0 = not circular */
     const int32_t* rotation_index;   /* nullable [num_nodes] */
     const uint8_t* sequence_inverted;/* nullable [num_nodes] */
+    const float* branch_length;      /* nullable [num_nodes]; Newick branch lengths (root 0) */
 } pm_panmat;
 
 /* Drop-in for Tree::printFASTAUltraFast(fout, aligned) (src/fasta.cpp:1981-2099): one

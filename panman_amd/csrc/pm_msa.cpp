@@ -321,6 +321,7 @@ int pm_msa_to_panman(const char* newick, const char* msa_text, const char* refer
     p.nuc_mut_gap_position = ngap.data();
     p.nuc_mut_info = ninfo.data();
     p.nuc_mut_nucs = nnucs.data();
+    p.branch_length = r.t.length.data();
     const pm_panmat* list[1] = {&p};
     const int rc = pm_panman_write(out_path, list, 1, 1);
     if (rc != PM_OK) set_err(std::string("cannot write ") + out_path);

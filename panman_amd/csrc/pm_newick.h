@@ -13,12 +13,15 @@ namespace pm {
 struct Topology {
     std::vector<std::string> name;
     std::vector<std::vector<int32_t>> kids;
+    std::vector<float> length;   // branch length per node (root 0)
     int32_t root = -1;
 };
 
 std::vector<std::string> split_quoted(const std::string& s, char delim);
 bool parse_topology(std::string text, Topology& t, std::string& err);
-// Newick text that parse_topology maps back to the same topology and leaf names.
+// Tree::getNewickString (src/panman.cpp:1921-2029): leaves "name:len", clades
+// "(...)name:len", lengths printed with "%f", terminated by ';'.  Empty `length` prints
+// the parser's defaults (1 for every node, 0 for the root).
 std::string newick_of(const Topology& t);
 
 }  // namespace pm

@@ -301,6 +301,7 @@ struct PanmanTree {
     std::vector<uint32_t> nm_nucs;
     std::vector<int32_t> circular, rotation;
     std::vector<uint8_t> inverted;
+    std::vector<float> length;
     std::string newick;
     int32_t num_nodes = 0;
 
@@ -333,6 +334,7 @@ struct PanmanTree {
         v.circular_offset = circular.data();
         v.rotation_index = rotation.data();
         v.sequence_inverted = inverted.data();
+        v.branch_length = length.data();
     }
 };
 
@@ -347,6 +349,7 @@ bool load_tree(Msg& m, const Struct& t, PanmanTree& out) {
     const int32_t N = (int32_t)topo.name.size();
     out.num_nodes = N;
     out.root = topo.root;
+    out.length = topo.length;
     out.child_off.assign(N + 1, 0);
     for (int32_t i = 0; i < N; ++i) {
         out.child_idx.insert(out.child_idx.end(), topo.kids[i].begin(), topo.kids[i].end());
@@ -516,6 +519,7 @@ void write_tree(Writer& wr, size_t tree_pos, const pm_panmat& p) {
     topo.name = names;
     topo.kids.assign(N, {});
     topo.root = p.root;
+    if (p.branch_length) topo.length.assign(p.branch_length, p.branch_length + N);
     for (int32_t i = 0; i < N; ++i)
         for (int32_t e = p.child_offsets[i]; e < p.child_offsets[i + 1]; ++e) topo.kids[i].push_back(p.child_index[e]);
     // ptr slots of the Tree struct are at tree_pos + k (0 data words)

@@ -36,6 +36,7 @@ class PanmatStruct(C.Structure):
         ("nuc_mut_position", C.c_void_p), ("nuc_mut_gap_position", C.c_void_p), ("nuc_mut_info", C.c_void_p),
         ("nuc_mut_nucs", C.c_void_p),
         ("circular_offset", C.c_void_p), ("rotation_index", C.c_void_p), ("sequence_inverted", C.c_void_p),
+        ("branch_length", C.c_void_p),
     ]
 
 
@@ -55,6 +56,7 @@ class PanMAT:
         self.circular = np.full(n, -1, np.int32)
         self.rotation = np.zeros(n, np.int32)
         self.inverted = np.zeros(n, np.uint8)
+        self.branch_length = None   # optional float32 [n]; None = Newick defaults
 
     def set_arrays(self, **arrays):
         """Bulk form: block_primary, block_seq_offsets, block_seq, gap_primary, gap_offsets,
@@ -121,7 +123,8 @@ class PanMAT:
                 arr(a["nuc_mut_secondary"], np.int32), arr(a["nuc_mut_position"], np.int32),
                 arr(a["nuc_mut_gap_position"], np.int32), arr(a["nuc_mut_info"], np.uint8),
                 arr(a["nuc_mut_nucs"], np.uint32),
-                arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8)), keep
+                arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8),
+                self._lengths(arr)), keep
         seq_off = np.zeros(len(self.blocks) + 1, np.int64)
         seq = []
         for i, (_, w) in enumerate(self.blocks):
@@ -155,8 +158,12 @@ class PanMAT:
             arr(b_off, np.int64), arr(bm[:, 0], np.int32), arr(bm[:, 1], np.uint8), arr(bm[:, 2], np.uint8),
             arr(n_off, np.int64), arr(nm[:, 0], np.int32), arr(nm[:, 1], np.int32), arr(nm[:, 2], np.int32),
             arr(nm[:, 3], np.int32), arr(nm[:, 4], np.uint8), arr(nm[:, 5] & 0xFFFFFFFF, np.uint32),
-            arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8))
+            arr(self.circular, np.int32), arr(self.rotation, np.int32), arr(self.inverted, np.uint8),
+            self._lengths(arr))
         return s, keep
+
+    def _lengths(self, arr):
+        return None if self.branch_length is None else arr(self.branch_length, np.float32)
 
 
 def from_msa_dump(dump: str, names, child_offsets, child_index, root) -> PanMAT:
@@ -241,6 +248,8 @@ class PanmanFile:
         pm.circular = a(v.circular_offset, np.int32, n)
         pm.rotation = a(v.rotation_index, np.int32, n)
         pm.inverted = a(v.sequence_inverted, np.uint8, n)
+        if v.branch_length:
+            pm.branch_length = a(v.branch_length, np.float32, n)
         return pm
 
     def close(self):

@@ -79,3 +79,52 @@ def test_corrupt_files_are_errors(tmp_path):
     trunc.write_bytes(b"\x00\x00\x00\x00\xff\x00\x00\x00" + b"\x00" * 16)
     with pytest.raises(panman_amd.PanmanError):
         PanmanFile(str(trunc))
+
+
+def _newick_only_message(newick: str) -> bytes:
+    """Uncompressed capnp message: TreeGroup{trees=[Tree{newick}]} (other fields null)."""
+    import struct
+    text = newick.encode() + b"\0"
+    tw = (len(text) + 7) // 8
+    # words: 0 root ptr | 1-2 TreeGroup ptrs | 3 list tag | 4-11 Tree ptrs | 12.. text
+    words = [0] * (12 + tw)
+
+    def sptr(at, target, dw, pc):
+        return ((target - at - 1) << 2) | (dw << 32) | (pc << 48)
+
+    def lptr(at, target, size, n):
+        return ((target - at - 1) << 2) | 1 | (size << 32) | (n << 35)
+
+    words[0] = sptr(0, 1, 0, 2)
+    words[1] = lptr(1, 3, 7, 8)                  # composite, 8 words of elements
+    words[3] = (1 << 2) | (0 << 32) | (8 << 48)  # tag: 1 element, 0 data words, 8 ptrs
+    words[4] = lptr(4, 12, 2, len(text))         # newick: List(UInt8) with NUL
+    body = b"".join(struct.pack("<Q", w & (2**64 - 1)) for w in words[:12]) + text.ljust(tw * 8, b"\0")
+    return struct.pack("<II", 0, len(body) // 8) + body
+
+
+@pytest.mark.parametrize("newick,want", [
+    # lengths kept, internal labels ignored and renamed, root printed with 0
+    ("((a:1,b:2)X:0.5,c:3);", "((a:1.000000,b:2.000000)node_2:0.500000,c:3.000000)node_1:0.000000;"),
+    # a clade without ':len' takes the last length of its piece; 0 and missing become 1
+    ("(((a:0.5,b:0.7)),c:2);",
+     "(((a:0.500000,b:0.700000)node_3:0.700000)node_2:0.700000,c:2.000000)node_1:0.000000;"),
+    ("(a,b:0,(c:1e-05,d));", "(a:1.000000,b:1.000000,(c:105.000000,d:1.000000)node_2:1.000000)node_1:0.000000;"),
+])
+def test_newick_lengths_follow_reference_rules(tmp_path, newick, want):
+    """createTreeFromNewickString length queues (src/panman.cpp:339-435) and
+    getNewickString (:1921-2029), through load -> write -> load."""
+    src = tmp_path / "n.capnp"
+    src.write_bytes(_newick_only_message(newick))
+    f = PanmanFile(str(src))
+    assert f.newick(0) == newick
+    pm = f.to_panmat(0)
+    f.close()
+    pm.add_block(0, "ACGT")
+    out = str(tmp_path / "o.panman")
+    write_panman(out, [pm])
+    g = PanmanFile(out)
+    assert g.newick(0) == want
+    again = g.to_panmat(0)
+    g.close()
+    assert np.array_equal(again.branch_length, pm.branch_length)
