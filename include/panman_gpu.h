@@ -216,6 +216,16 @@ void pm_panman_free(pm_panman* file);
  * src/panmanUtils.cpp:271-299): capnp message, xz level 9 when `compress`. */
 int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, int compress);
 
+/* Drop-in for Tree::reroot(leaf) (src/reroot.cpp:4-262; CLI --reroot,
+ * src/panmanUtils.cpp:855-892): every leaf's sequence is replayed on the GPU
+ * (getSequenceFromReference, src/panman.cpp:4676-5000), the root moves next to `leaf`
+ * (transform, :5831-5906) and every block and nucleotide mutation is re-derived by Fitch
+ * with the root forced to the leaf's states.  The result is a new one-tree pm_panman (in
+ * the pre-order of the new topology; release with pm_panman_free).  Replaces the ctx's
+ * tree, columns and replay state.  Within a node, block mutations are ordered by block
+ * id (the reference's order is TBB-scheduled). */
+int pm_reroot(pm_ctx* ctx, const pm_panmat* tree, const char* leaf, pm_panman** out);
+
 /* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
 /* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes
  * 2*leaves-1 nodes as CSR; leaves are ids [0, leaves), internal nodes follow. */

@@ -36,6 +36,8 @@ def load() -> "Oracle":
             C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
         lib.oracle_fasta.restype = C.c_void_p
         lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
+        lib.oracle_reroot.restype = C.c_void_p
+        lib.oracle_reroot.argtypes = [C.c_void_p, C.c_char_p]
         _lib = lib
     return Oracle(_lib)
 
@@ -69,6 +71,14 @@ class Oracle:
         del keep
         text = _take_string(self.lib, p)
         return (text, secs.value) if timed else text
+
+    def reroot(self, panmat, leaf: str) -> str:
+        """Tree::reroot(leaf) dump: the new Newick, then per node (name order) its block
+        mutations sorted by block and its NucMut records in list order."""
+        st, keep = panmat.as_struct()
+        p = self.lib.oracle_reroot(C.byref(st), leaf.encode())
+        del keep
+        return _take_string(self.lib, p)
 
     def column(self, newick: str, leaves: str, algo: str, forced: int, parent: int) -> dict:
         p = self.lib.oracle_column(newick.encode(), leaves.encode(), self.ALGO[algo], forced, parent)

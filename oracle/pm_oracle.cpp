@@ -735,13 +735,15 @@ struct RNucMut { int32_t pos; int32_t gap; int32_t primary; int32_t secondary; u
                  uint32_t type() const { return info & 0x7; }
                  int code(int i) const { return (nucs >> (4 * (5 - i))) & 0xF; } };
 struct RNode { std::string id; RNode* parent = nullptr; std::vector<RNode*> children;
-               std::vector<RBlockMut> bmuts; std::vector<RNucMut> nmuts; };
+               std::vector<RBlockMut> bmuts; std::vector<RNucMut> nmuts; float len = 1.0f; };
 struct RBlock { int32_t primary; std::vector<uint32_t> seq; };
 struct RGap { int32_t primary; std::vector<uint32_t> pos, len; };
 using Seq = std::vector<std::vector<std::pair<char, std::vector<char>>>>;
 
 struct RTree {
     std::vector<std::unique_ptr<RNode>> nodes;
+    RNode* root = nullptr;
+    size_t internal_counter = 0;          // m_currInternalNode after the Newick parse
     std::map<std::string, RNode*> all;
     std::vector<RBlock> blocks;
     std::vector<RGap> gaps;
@@ -1152,17 +1154,16 @@ struct OraclePanmat {
     const int32_t* circular_offset;    // nullable, [num_nodes]; < 0 = none
     const int32_t* rotation_index;     // nullable
     const uint8_t* sequence_inverted;  // nullable
+    const float* branch_length;        // nullable
 };
 
-// FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name; at most
-// `leaf_limit` leaves (<= 0: all) and, when `seconds` is set, the replay wall time.
-char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* seconds) {
-    RTree t;
+void build_rtree(const OraclePanmat* p, RTree& t) {
     const char* nm = p->names;
     for (int32_t i = 0; i < p->num_nodes; ++i) {
         auto n = std::make_unique<RNode>();
         n->id = nm;
         nm += n->id.size() + 1;
+        if (p->branch_length) n->len = p->branch_length[i];
         t.nodes.push_back(std::move(n));
     }
     for (int32_t i = 0; i < p->num_nodes; ++i) {
@@ -1173,6 +1174,7 @@ char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* s
             c->parent = n;
             n->children.push_back(c);
         }
+        if (p->child_offsets[i + 1] > p->child_offsets[i]) ++t.internal_counter;
         for (int64_t k = p->block_mut_offsets[i]; k < p->block_mut_offsets[i + 1]; ++k)
             n->bmuts.push_back({p->block_mut_primary[k], -1, p->block_mut_info[k] != 0, p->block_mut_inversion[k] != 0});
         for (int64_t k = p->nuc_mut_offsets[i]; k < p->nuc_mut_offsets[i + 1]; ++k)
@@ -1182,6 +1184,7 @@ char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* s
         if (p->rotation_index && p->rotation_index[i] != 0) t.rotation[n->id] = p->rotation_index[i];
         if (p->sequence_inverted && p->sequence_inverted[i]) t.inverted[n->id] = true;
     }
+    t.root = t.nodes[p->root].get();
     for (int32_t b = 0; b < p->num_blocks; ++b)
         t.blocks.push_back({p->block_primary[b], std::vector<uint32_t>(p->block_seq + p->block_seq_offsets[b],
                                                                       p->block_seq + p->block_seq_offsets[b + 1])});
@@ -1193,6 +1196,278 @@ char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* s
         }
         t.gaps.push_back(gl);
     }
+}
+
+// ---------------------------------------------------------------- M4 reroot ----
+// R4 getSequenceFromReference (src/panman.cpp:4676-5000) with rotateSequence = false:
+// every block expanded (absent ones keep the consensus), gap slots resized, block
+// mutations over the whole path, then nucleotide mutations of blocks that exist.
+bool sequence_from_reference(RTree& t, RNode* ref, Seq& seq, std::vector<bool>& exists, std::vector<bool>& strand,
+                             std::string& err) {
+    std::vector<RNode*> path;
+    for (RNode* it = ref; it != t.root; it = it->parent) path.push_back(it);
+    path.push_back(t.root);
+    seq.assign(t.blocks.size() + 1, {});
+    exists.assign(t.blocks.size() + 1, false);
+    strand.assign(t.blocks.size() + 1, true);
+    int32_t max_id = 0;
+    for (auto& b : t.blocks) {
+        max_id = std::max(max_id, b.primary);
+        if ((size_t)b.primary >= seq.size()) { err = "block id beyond the block count"; return false; }
+        bool end = false;
+        for (size_t j = 0; j < b.seq.size() && !end; ++j)
+            for (int k = 0; k < 8; ++k) {
+                const int code = (b.seq[j] >> (4 * (7 - k))) & 15;
+                if (code == 0) { end = true; break; }
+                seq[b.primary].push_back({char_of(code), {}});
+            }
+        seq[b.primary].push_back({'x', {}});
+    }
+    seq.resize(max_id + 1);
+    exists.resize(max_id + 1);
+    strand.resize(max_id + 1);
+    for (auto& g : t.gaps)
+        for (size_t j = 0; j < g.pos.size(); ++j) {
+            if (g.pos[j] >= seq[g.primary].size()) { err = "gap position beyond the block"; return false; }
+            seq[g.primary][g.pos[j]].second.resize(g.len[j], '-');
+        }
+    for (auto it = path.rbegin(); it != path.rend(); ++it)
+        for (auto& m : (*it)->bmuts) {
+            if (m.info) { exists[m.primary] = true; strand[m.primary] = !m.inversion; }
+            else if (m.inversion) strand[m.primary] = !strand[m.primary];
+            else { exists[m.primary] = false; strand[m.primary] = true; }
+        }
+    for (auto it = path.rbegin(); it != path.rend(); ++it)
+        for (auto& m : (*it)->nmuts) {
+            if (!exists[m.primary]) continue;
+            auto& blk = seq[m.primary];
+            const uint32_t type = m.type();
+            auto put = [&](int32_t pos, int32_t gap, char v) {
+                if (pos < 0 || (size_t)pos >= blk.size()) return false;
+                if (gap != -1) {
+                    if (gap < 0 || (size_t)gap >= blk[pos].second.size()) return false;
+                    blk[pos].second[gap] = v;
+                } else {
+                    blk[pos].first = v;
+                }
+                return true;
+            };
+            bool ok = true;
+            if (type < 3) {
+                for (int j = 0; j < m.length() && ok; ++j) {
+                    const char v = type == ND ? '-' : char_of(m.code(j));
+                    ok = m.gap != -1 ? put(m.pos, m.gap + j, v) : put(m.pos + j, -1, v);
+                }
+            } else if (type <= 5) {
+                ok = put(m.pos, m.gap, type == 5 ? '-' : char_of(m.code(0)));
+            }
+            if (!ok) { err = "mutation outside its block"; return false; }
+        }
+    return true;
+}
+
+// transformHelper (src/panman.cpp:5831-5865)
+RNode* transform_helper(RTree& t, RNode* node, bool& ok) {
+    if (node == t.root) {
+        if (node->children.size() > 1) {
+            node->len = 0;
+            return node;
+        }
+        if (node->children.empty()) { ok = false; return node; }   // reference: children[0] of an empty list
+        RNode* c = node->children[0];
+        c->len = 0;
+        t.all.erase(node->id);
+        node->children.clear();
+        return c;
+    }
+    RNode* par = node->parent;
+    par->children.erase(std::find(par->children.begin(), par->children.end(), node));
+    node->parent = nullptr;
+    const float old = node->len;
+    node->len = 0;
+    RNode* c = transform_helper(t, par, ok);
+    node->children.push_back(c);
+    c->parent = node;
+    c->len = old;
+    return node;
+}
+
+// transform (src/panman.cpp:5867-5906)
+bool transform(RTree& t, RNode* node) {
+    RNode* par = node->parent;
+    if (!par) return true;
+    if (par == t.root) { node->len = 0; return true; }
+    par->children.erase(std::find(par->children.begin(), par->children.end(), node));
+    node->parent = nullptr;
+    const float old = node->len;
+    auto nr = std::make_unique<RNode>();
+    nr->id = "node_" + std::to_string(++t.internal_counter);
+    nr->len = 0;
+    nr->children.push_back(node);
+    node->parent = nr.get();
+    node->len = 0;
+    bool ok = true;
+    RNode* sib = transform_helper(t, par, ok);
+    nr->children.push_back(sib);
+    sib->parent = nr.get();
+    sib->len = old;
+    t.root = nr.get();
+    t.all[nr->id] = nr.get();
+    t.nodes.push_back(std::move(nr));
+    return ok;
+}
+
+// getNewickString (src/panman.cpp:1921-2029) -- the level walk there prints exactly this
+// recursive form: "(children)name:len", leaves "name:len", lengths with "%f".
+void newick_rec(RNode* n, std::string& out) {
+    char buf[64];
+    std::snprintf(buf, sizeof buf, ":%f", (double)n->len);
+    if (!n->children.empty()) {
+        out += '(';
+        for (size_t i = 0; i < n->children.size(); ++i) {
+            if (i) out += ',';
+            newick_rec(n->children[i], out);
+        }
+        out += ')';
+    }
+    out += n->id;
+    if (n->len >= 0) out += buf;
+}
+
+ONode* mirror(OTree& o, RNode* n, ONode* par) {
+    ONode* x = o.make(n->id, par);
+    o.all[x->id] = x;
+    for (RNode* c : n->children) mirror(o, c, x);
+    return x;
+}
+
+using Tup6 = std::tuple<int, int, int, int, int, int>;   // block, secondary, pos, gap, type, code
+
+// NucMut runs (src/reroot.cpp:228-262, NucMut(vector<tuple6>, start, end) src/panman.hpp:150-180)
+void group6(std::vector<Tup6>& v, bool gap, std::vector<RNucMut>& out) {
+    std::sort(v.begin(), v.end());
+    auto emit = [&](size_t a, size_t b) {
+        RNucMut m{std::get<2>(v[a]), std::get<3>(v[a]), std::get<0>(v[a]), std::get<1>(v[a]),
+                  (uint8_t)(((b - a) << 4) + std::get<4>(v[a])), 0};
+        for (size_t i = a; i < b; ++i) m.nucs += (uint32_t)std::get<5>(v[i]) << (4 * (5 - (i - a)));
+        out.push_back(m);
+    };
+    size_t start = 0;
+    for (size_t i = 1; i < v.size(); ++i) {
+        const bool brk = i - start == 6 || std::get<0>(v[i]) != std::get<0>(v[i - 1]) ||
+                         std::get<1>(v[i]) != std::get<1>(v[i - 1]) ||
+                         (gap ? (std::get<2>(v[i]) != std::get<2>(v[i - 1]) || std::get<3>(v[i]) != std::get<3>(v[i - 1]) + 1)
+                              : std::get<2>(v[i]) != std::get<2>(v[i - 1]) + 1) ||
+                         std::get<4>(v[i]) != std::get<4>(v[i - 1]);
+        if (brk) { emit(start, i); start = i; }
+    }
+    if (!v.empty()) emit(start, v.size());
+}
+
+// Tree::reroot (src/reroot.cpp:4-262), columns in sequence; returns the dump (or "#error").
+std::string reroot_dump(RTree& t, const std::string& name) {
+    auto it = t.all.find(name);
+    if (it == t.all.end()) return "#error\tSequence with name " + name + " not found!\n";
+    RNode* new_root = it->second;
+    if (!new_root->children.empty()) return "#error\tNode with id " + name + " is not a tip!\n";
+    std::string err;
+    Seq seq;
+    std::vector<bool> bex, bst;
+    if (!sequence_from_reference(t, new_root, seq, bex, bst, err)) return "#error\t" + err + "\n";
+    std::map<std::string, Seq> leaf_seq;
+    std::map<std::string, std::vector<bool>> leaf_ex, leaf_st;
+    for (auto& kv : t.all)
+        if (kv.second->children.empty()) {
+            Seq s2;
+            std::vector<bool> e2, st2;
+            if (!sequence_from_reference(t, kv.second, s2, e2, st2, err)) return "#error\t" + err + "\n";
+            leaf_seq[kv.first] = std::move(s2);
+            leaf_ex[kv.first] = std::move(e2);
+            leaf_st[kv.first] = std::move(st2);
+        }
+    if (!transform(t, new_root)) return "#error\tunary root\n";
+    for (auto& kv : t.all) { kv.second->bmuts.clear(); kv.second->nmuts.clear(); }
+    OTree o;
+    o.root = mirror(o, t.root, nullptr);
+    // block mutations (src/reroot.cpp:53-125)
+    for (size_t i = 0; i < bex.size(); ++i) {
+        StateMap st;
+        BlockMutMap muts;
+        for (auto& kv : leaf_ex) st[kv.first] = !kv.second[i] ? 1 : (leaf_st[kv.first][i] ? 2 : 4);
+        const int def = !bex[i] ? 1 : (bst[i] ? 2 : 4);
+        block_fitch_up(o.root, st);
+        block_fitch_down(o.root, o.root, st, 1, def);
+        block_fitch_assign(o.root, st, muts, 1);
+        for (auto& m : muts) t.all[m.first]->bmuts.push_back({(int32_t)i, -1, m.second.first == BI, m.second.second});
+    }
+    // nucleotide mutations (src/reroot.cpp:130-226)
+    std::map<std::string, std::vector<Tup6>> non_gap, gap;
+    for (size_t i = 0; i < seq.size(); ++i) {
+        const RBlock* blk = nullptr;
+        for (auto& b : t.blocks)
+            if (b.primary == (int32_t)i) { blk = &b; break; }
+        if (!blk) return "#error\tBlock with id " + std::to_string(i) + " -1 not found!\n";
+        std::string cons;
+        bool end = false;
+        for (size_t j = 0; j < blk->seq.size() && !end; ++j)
+            for (int k = 0; k < 8; ++k) {
+                const int code = (blk->seq[j] >> (4 * (7 - k))) & 15;
+                if (code == 0) { end = true; break; }
+                cons += char_of(code);
+            }
+        cons += '-';
+        if (cons.size() != seq[i].size()) return "#error\tconsensus length mismatch\n";
+        auto state_of = [](char ch) { return ch != '-' && ch != 'x' ? 1 << code_of(ch) : 1; };
+        for (size_t k = 0; k < seq[i].size(); ++k) {
+            for (size_t w = 0; w < seq[i][k].second.size(); ++w) {
+                StateMap st;
+                NucMutMap muts;
+                for (auto& kv : leaf_seq) st[kv.first] = state_of(kv.second[i][k].second[w]);
+                const int code = state_of(seq[i][k].second[w]);
+                fitch_up(o.root, st, code);
+                fitch_down(o.root, o.root, st, code, code);
+                fitch_assign(o.root, st, muts, 1);
+                for (auto& m : muts)
+                    gap[m.first].emplace_back((int)i, -1, (int)k, (int)w, m.second.first, code_of(m.second.second));
+            }
+            StateMap st;
+            NucMutMap muts;
+            for (auto& kv : leaf_seq) st[kv.first] = state_of(kv.second[i][k].first);
+            const int code = state_of(seq[i][k].first);
+            fitch_up(o.root, st, code);
+            fitch_down(o.root, o.root, st, code, code);
+            fitch_assign(o.root, st, muts, 1 << code_of(cons[k]));
+            for (auto& m : muts)
+                non_gap[m.first].emplace_back((int)i, -1, (int)k, -1, m.second.first, code_of(m.second.second));
+        }
+    }
+    for (auto& kv : non_gap) group6(kv.second, false, t.all[kv.first]->nmuts);
+    for (auto& kv : gap) group6(kv.second, true, t.all[kv.first]->nmuts);
+    std::string out = "newick\t";
+    newick_rec(t.root, out);
+    out += ";\n";
+    char buf[160];
+    for (auto& kv : t.all) {
+        auto bm = kv.second->bmuts;
+        std::sort(bm.begin(), bm.end(), [](const RBlockMut& a, const RBlockMut& b) { return a.primary < b.primary; });
+        for (auto& m : bm) {
+            std::snprintf(buf, sizeof buf, "\tB\t%d\t%d\t%d\n", m.primary, (int)m.info, (int)m.inversion);
+            out += kv.first + buf;
+        }
+        for (auto& m : kv.second->nmuts) {
+            std::snprintf(buf, sizeof buf, "\tN\t%d\t%d\t%d\t%u\t%06x\n", m.primary, m.pos, m.gap, (unsigned)m.info,
+                          m.nucs);
+            out += kv.first + buf;
+        }
+    }
+    return out;
+}
+
+// FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name; at most
+// `leaf_limit` leaves (<= 0: all) and, when `seconds` is set, the replay wall time.
+char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* seconds) {
+    RTree t;
+    build_rtree(p, t);
     std::string out;
     int done = 0;
     auto t0 = std::chrono::steady_clock::now();
@@ -1204,6 +1479,15 @@ char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* s
     }
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return dup_string(out);
+}
+
+// Reroot at `leaf` (Tree::reroot) and dump the new tree: "newick\t<text>" then per node
+// in name order its block mutations (sorted by block) and nucleotide mutations (list
+// order) -- see reroot_dump.
+char* oracle_reroot(const OraclePanmat* p, const char* leaf) {
+    RTree t;
+    build_rtree(p, t);
+    return dup_string(reroot_dump(t, leaf));
 }
 
 }  // extern "C"

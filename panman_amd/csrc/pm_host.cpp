@@ -348,6 +348,35 @@ void timer_end(pm_ctx* c, int cls) {
 
 using namespace pm;
 
+namespace pm {
+
+// Leaf columns already on the device (packed codes, [row][row_stride]); every leaf with a
+// row is fully present.  Used by drivers that produce the columns on the GPU (reroot).
+int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_stride, const int32_t* node_row) {
+    if (!c->has_tree) return fail(c, PM_ERR_STATE, "upload the tree first");
+    if (S <= 0 || S >= (int64_t)1 << 24 || row_stride < (S + 1) / 2) return fail(c, PM_ERR_ARG, "bad leaf columns");
+    const int32_t L = c->dt.num_leaves;
+    std::vector<int32_t> row_of_leaf(L);
+    std::vector<uint8_t> flag(L);
+    for (int32_t l = 0; l < L; ++l) {
+        row_of_leaf[l] = node_row[c->ht.leaf_id[l]];
+        flag[l] = row_of_leaf[l] < 0 ? kLeafAbsent : kLeafPresent;
+    }
+    int rc = alloc_columns(c, S);
+    if (rc != PM_OK) return rc;
+    int32_t* d_rows = nullptr;
+    hipError_t e = upload(&d_rows, row_of_leaf, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->leaf_flag, flag.data(), L, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_pack_codes(c, d_codes4, row_stride, d_rows, nullptr, 0);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d_rows);
+    if (e != hipSuccess) return hip_fail(c, e, "leaf install");
+    c->has_leaves = true;
+    return PM_OK;
+}
+
+}  // namespace pm
+
 extern "C" {
 
 int pm_create(int device, pm_ctx** out) {

@@ -164,6 +164,7 @@ hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
 void free_replay(pm_ctx* c);
+int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_stride, const int32_t* node_row);
 
 // replay kernels (pm_replay.hip)
 struct ReplayDev {
@@ -183,5 +184,8 @@ struct ReplayDev {
     const int32_t* edit_blk = nullptr;
 };
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d);
+// rows[leaf][c0 .. c0+n) chars -> packed codes out[leaf][(n+1)/2] ('-', 'x' -> 0)
+hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride, int32_t leaves, int64_t c0,
+                                int64_t n, uint8_t* out, int64_t out_stride);
 
 }  // namespace pm

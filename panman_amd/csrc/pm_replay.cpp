@@ -19,41 +19,9 @@
 #include <thread>
 #include <vector>
 
-#include "pm_internal.h"
+#include "pm_replay.h"
 
 namespace pm {
-
-struct ReplayState {
-    // topology
-    int32_t num_nodes = 0;
-    std::vector<std::string> names;
-    std::vector<int32_t> parent;
-    std::vector<int32_t> leaves;                 // leaf node ids, increasing
-    // blocks, indexed by primary id (0..max_id)
-    int32_t max_id = -1;
-    std::vector<uint8_t> is_block;               // [max_id+1]
-    std::vector<int64_t> col_start, width;       // canonical columns per block
-    std::vector<int64_t> absent_len;             // blockLengths when absent (len + sum of gap lengths)
-    int64_t columns = 0;
-    // per leaf (host, for the formatter)
-    std::vector<std::vector<uint8_t>> present;   // [leaf][max_id+1]
-    std::vector<std::vector<uint8_t>> exists, strand;
-    std::vector<int32_t> circular, rotation;
-    std::vector<uint8_t> inverted;
-    int64_t edits = 0;
-    // device
-    ReplayDev dev{};
-    char* d_rows = nullptr;
-    char* d_cons = nullptr;
-    int32_t* d_parent = nullptr;
-    int32_t* d_leaf = nullptr;
-    uint32_t* d_presence = nullptr;
-    int64_t* d_eoff = nullptr;
-    uint32_t* d_ecol = nullptr;
-    uint8_t* d_echr = nullptr;
-    int32_t* d_eblk = nullptr;
-    bool ran = false;
-};
 
 namespace {
 
@@ -85,7 +53,9 @@ hipError_t dput(T** dst, const std::vector<T>& v, hipStream_t s) {
     return hipMemcpyAsync(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
 }
 
-int prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
+}  // namespace
+
+int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
     const int32_t N = p->num_nodes;
     if (N < 1 || p->root < 0 || p->root >= N || !p->child_offsets || !p->names)
         return fail(c, PM_ERR_ARG, "bad PanMAT topology");
@@ -166,6 +136,10 @@ int prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
         r.absent_len[id] = len[id] + gap_sum[id];
     }
     r.columns = (int64_t)cons.size();
+    r.cons = cons;
+    r.main_col = main_col;
+    r.gap_col = gap_col;
+    r.slots = slots;
     if (r.columns >= ((int64_t)1 << 32)) return fail(c, PM_ERR_UNSUPPORTED, "more than 2^32 aligned columns");
 
     // ---- per-node edits (column, char, block), last write per column within a node wins
@@ -303,6 +277,8 @@ int prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
     return PM_OK;
 }
 
+namespace {
+
 // printSequenceLinesNew for one leaf, from its replayed canonical row.
 void format_leaf(const ReplayState& r, int32_t li, const char* row, bool aligned, std::string& out) {
     const int32_t M = r.max_id + 1;
@@ -396,7 +372,7 @@ int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) {
     (void)hipSetDevice(c->device);
     free_replay(c);
     c->replay = new ReplayState();
-    int rc = prepare(c, p, *c->replay);
+    int rc = replay_prepare(c, p, *c->replay);
     if (rc != PM_OK) free_replay(c);
     return rc;
 }

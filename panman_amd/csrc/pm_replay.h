@@ -1,0 +1,53 @@
+// pm_replay.h -- replay state shared by the FASTA path (pm_replay.cpp) and the reroot
+// driver (pm_reroot.cpp).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "pm_internal.h"
+
+namespace pm {
+
+struct ReplayState {
+    // topology
+    int32_t num_nodes = 0;
+    std::vector<std::string> names;
+    std::vector<int32_t> parent;
+    std::vector<int32_t> leaves;                 // leaf node ids, increasing
+    // blocks, indexed by primary id (0..max_id)
+    int32_t max_id = -1;
+    std::vector<uint8_t> is_block;               // [max_id+1]
+    std::vector<int64_t> col_start, width;       // canonical columns per block
+    std::vector<int64_t> absent_len;             // blockLengths when absent (len + sum of gap lengths)
+    int64_t columns = 0;
+    // per leaf (host, for the formatter)
+    std::vector<std::vector<uint8_t>> present;   // [leaf][max_id+1]
+    std::vector<std::vector<uint8_t>> exists, strand;
+    std::vector<int32_t> circular, rotation;
+    std::vector<uint8_t> inverted;
+    int64_t edits = 0;
+    // canonical layout (host): consensus row, and per block the column of main position j
+    // and of the first gap slot before j, plus the slot counts
+    std::string cons;
+    std::vector<std::vector<int64_t>> main_col, gap_col;
+    std::vector<std::vector<int32_t>> slots;
+    // device
+    ReplayDev dev{};
+    char* d_rows = nullptr;
+    char* d_cons = nullptr;
+    int32_t* d_parent = nullptr;
+    int32_t* d_leaf = nullptr;
+    uint32_t* d_presence = nullptr;
+    int64_t* d_eoff = nullptr;
+    uint32_t* d_ecol = nullptr;
+    uint8_t* d_echr = nullptr;
+    int32_t* d_eblk = nullptr;
+    bool ran = false;
+};
+
+// Flatten a PanMAT for the GPU (canonical columns, per-node edits, per-leaf block state)
+// and upload it; the rows are produced by launch_replay(c, r.dev).
+int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r);
+
+}  // namespace pm

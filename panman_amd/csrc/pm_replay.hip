@@ -54,7 +54,41 @@ __global__ __launch_bounds__(256) void k_replay_apply(ReplayDev d) {
     }
 }
 
+// getCodeFromNucleotide (src/panman.cpp:78-113) for the replayed characters; the reroot
+// driver turns '-' and the 'x' sentinel into state 1 = code 0 (src/reroot.cpp:176-181).
+__device__ __forceinline__ uint32_t code_of_char(char ch) {
+    switch (ch) {
+        case 'A': return 1;  case 'C': return 2;  case 'G': return 4;  case 'T': return 8;
+        case 'R': return 5;  case 'Y': return 10; case 'S': return 6;  case 'W': return 9;
+        case 'K': return 12; case 'M': return 3;  case 'B': return 14; case 'D': return 13;
+        case 'H': return 11; case 'V': return 7;  case 'N': return 15;
+        default: return 0;
+    }
+}
+
+// One thread per output byte (two columns); row reads and code writes are coalesced.
+__global__ __launch_bounds__(256) void k_rows_to_codes(const char* rows, int64_t row_stride, int32_t leaves, int64_t c0,
+                                                       int64_t n, uint8_t* out, int64_t out_stride) {
+    const int64_t per_row = (n + 1) / 2;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= per_row * leaves) return;
+    const int64_t leaf = t / per_row, b = t % per_row;
+    const char* r = rows + leaf * row_stride + c0 + 2 * b;
+    uint32_t v = code_of_char(r[0]);
+    if (2 * b + 1 < n) v |= code_of_char(r[1]) << 4;
+    out[leaf * out_stride + b] = (uint8_t)v;
+}
+
 }  // namespace
+
+hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride, int32_t leaves, int64_t c0, int64_t n,
+                                uint8_t* out, int64_t out_stride) {
+    const int64_t total = (n + 1) / 2 * leaves;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rows_to_codes, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, rows, row_stride,
+                       leaves, c0, n, out, out_stride);
+    return hipGetLastError();
+}
 
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;

@@ -186,10 +186,13 @@ def from_msa_dump(dump: str, names, child_offsets, child_index, root) -> PanMAT:
 class PanmanFile:
     """A loaded .panman (libpanman_amd: xz + Cap'n Proto reader, host only)."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str = None, handle: C.c_void_p = None):
         from ._lib import PanmanError, load
         self.lib = load()
         self.h = C.c_void_p()
+        if handle is not None:   # an owned pm_panman produced by the engine (e.g. pm_reroot)
+            self.h = handle
+            return
         err = C.create_string_buffer(512)
         rc = self.lib.pm_panman_load(path.encode(), C.byref(self.h), err, 512)
         if rc != 0:
@@ -251,6 +254,15 @@ class PanmanFile:
         if v.branch_length:
             pm.branch_length = a(v.branch_length, np.float32, n)
         return pm
+
+    def write(self, path: str, compress: bool = True):
+        """Write every tree of this file (pm_panman_write)."""
+        from ._lib import PanmanError
+        views = [self.view(i) for i in range(len(self))]
+        arr = (C.c_void_p * max(1, len(views)))(*[C.addressof(v) for v in views])
+        rc = self.lib.pm_panman_write(path.encode(), arr, len(views), int(compress))
+        if rc != 0:
+            raise PanmanError(f"pm_panman_write({path}) failed ({rc})")
 
     def close(self):
         if self.h:

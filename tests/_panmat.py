@@ -101,3 +101,87 @@ def random_panmat(rng, off, idx, root, names, blocks=6, block_len=(5, 40), gap_r
             elif r < 0.45:
                 pm.circular[v] = int(rng.integers(0, 30))
     return pm
+
+
+def tree_dump(f, i: int = 0) -> str:
+    """The oracle's reroot dump format for tree i of a PanmanFile: Newick, then per node in
+    name order its block mutations (stored order) and NucMut records (list order)."""
+    pm = f.to_panmat(i)
+    a = pm._arrays
+    out = ["newick\t" + f.newick(i)]
+    for name in sorted(pm.names):
+        v = pm.index(name)
+        for k in range(a["block_mut_offsets"][v], a["block_mut_offsets"][v + 1]):
+            out.append(f"{name}\tB\t{a['block_mut_primary'][k]}\t{a['block_mut_info'][k]}\t{a['block_mut_inversion'][k]}")
+        for k in range(a["nuc_mut_offsets"][v], a["nuc_mut_offsets"][v + 1]):
+            out.append(f"{name}\tN\t{a['nuc_mut_primary'][k]}\t{a['nuc_mut_position'][k]}\t"
+                       f"{a['nuc_mut_gap_position'][k]}\t{a['nuc_mut_info'][k]}\t{int(a['nuc_mut_nucs'][k]):06x}")
+    return "\n".join(out) + "\n"
+
+
+def _parse_labelled(newick: str):
+    """'(a:1,b:1)x:0;' with every node labelled -> (names, child lists, root) in pre-order."""
+    s = newick.strip().rstrip(";")
+    names, kids = [], []
+    pos = 0
+
+    def node():
+        nonlocal pos
+        me = len(names)
+        names.append(None)
+        kids.append([])
+        if s[pos] == "(":
+            pos += 1
+            while True:
+                kids[me].append(node())
+                if s[pos] == ",":
+                    pos += 1
+                    continue
+                assert s[pos] == ")"
+                pos += 1
+                break
+        start = pos
+        while pos < len(s) and s[pos] not in ",():":
+            pos += 1
+        names[me] = s[start:pos]
+        if pos < len(s) and s[pos] == ":":
+            pos += 1
+            while pos < len(s) and s[pos] not in ",()":
+                pos += 1
+        return me
+
+    root = node()
+    return names, kids, root
+
+
+def panmat_from_dump(dump: str, original: PanMAT) -> PanMAT:
+    """Rebuild a PanMAT from a reroot dump plus the original's blocks, gaps and per-name
+    rotation / inversion / circular offsets."""
+    lines = dump.splitlines()
+    assert lines[0].startswith("newick\t"), lines[0]
+    names, kids, root = _parse_labelled(lines[0][7:])
+    off = np.zeros(len(names) + 1, np.int32)
+    idx = []
+    for v in range(len(names)):
+        idx += kids[v]
+        off[v + 1] = len(idx)
+    pm = PanMAT(names, off, np.array(idx, np.int32), root)
+    a = getattr(original, "_arrays", None)
+    assert a is None, "use a list-built PanMAT"
+    pm.blocks = list(original.blocks)
+    pm.gaps = list(original.gaps)
+    by_name = {n: i for i, n in enumerate(original.names)}
+    for v, n in enumerate(names):
+        o = by_name.get(n)
+        if o is not None and off[v] == off[v + 1]:
+            pm.rotation[v] = original.rotation[o]
+            pm.inverted[v] = original.inverted[o]
+            pm.circular[v] = original.circular[o]
+    for line in lines[1:]:
+        f = line.split("\t")
+        v = pm.index(f[0])
+        if f[1] == "B":
+            pm.add_block_mut(v, int(f[2]), f[3] == "1", f[4] == "1")
+        else:
+            pm.add_nuc_mut_raw(v, int(f[2]), int(f[3]), int(f[4]), int(f[5]), int(f[6], 16))
+    return pm
