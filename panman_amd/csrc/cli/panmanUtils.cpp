@@ -45,8 +45,10 @@ const Spec kSpecs[] = {
     {"newick", 't', false, "Print newick string of all trees in a PanMAN"},
     {"fasta", 'f', false, "Print tip sequences (FASTA format)"},
     {"fasta-aligned", 'm', false, "Print MSA of sequences for each PanMAT in a PanMAN (FASTA format)"},
+    {"reroot", 'r', false, "Reroot a PanMAT in a PanMAN based on the input sequence id (--reference)"},
+    {"treeID", 'd', true, "Tree ID, required for --reroot"},
     {"low-mem-mode", 0, false, "Build with the Sankoff driver (the reference's batched low-memory mode)"},
-    {"reference", 'n', true, "Identifier of reference sequence for PanMAN construction (optional)"},
+    {"reference", 'n', true, "Identifier of reference sequence for PanMAN construction (optional) or reroot (required)"},
     {"output-file", 'o', true, "Prefix of the output file name"},
     {"threads", 0, true, "Accepted for compatibility (the build runs on the GPU)"},
     {"device", 0, true, "HIP device ordinal (default 0)"},
@@ -54,7 +56,7 @@ const Spec kSpecs[] = {
 
 // Reference commands outside the accelerated path: recognised so the error is explicit.
 const char* const kOther[] = {"input-pangraph", "input-gfa", "impute", "create-network", "printTips",
-                              "summary", "subnet", "vcf", "gfa", "maf", "annotate", "reroot",
+                              "summary", "subnet", "vcf", "gfa", "maf", "annotate",
                               "aa-translation", "extended-newick", "printMutations", "acr", "index",
                               "toUsher"};
 
@@ -185,6 +187,64 @@ int build_from_msa(const Options& o, int device) {
     return 0;
 }
 
+int reroot(const Options& o, const pm_panman* file, int device) {
+    if (!o.has("treeID")) {
+        print_error("TreeID not provided!");
+        usage(std::cout);
+        return 1;
+    }
+    const int tree_id = std::atoi(o.get("treeID").c_str());
+    if (tree_id < 0 || tree_id >= pm_panman_tree_count(file)) {
+        print_error("TreeID out of range");
+        return 1;
+    }
+    if (!o.has("reference")) {
+        print_error("Refence ID not provided!");
+        usage(std::cout);
+        return 1;
+    }
+    if (!o.has("output-file")) {
+        print_error("Output file not provided!");
+        return 1;
+    }
+    pm_ctx* ctx = nullptr;
+    if (pm_create(device, &ctx) != PM_OK) {
+        print_error("no HIP device");
+        return 1;
+    }
+    pm_panmat view;
+    pm_panman* res = nullptr;
+    const auto t0 = Clock::now();
+    int rc = pm_panman_tree(file, tree_id, &view);
+    if (rc == PM_OK) rc = pm_reroot(ctx, &view, o.get("reference").c_str(), &res);
+    if (rc != PM_OK) {
+        print_error(pm_last_error(ctx));
+        pm_destroy(ctx);
+        return 1;
+    }
+    std::cout << "\nReroot execution time: " << ns_since(t0) << " nanoseconds\n";
+    std::vector<pm_panmat> views(pm_panman_tree_count(file));
+    std::vector<const pm_panmat*> list;
+    for (int i = 0; i < (int)views.size(); ++i) {
+        if (i == tree_id) pm_panman_tree(res, 0, &views[i]);
+        else pm_panman_tree(file, i, &views[i]);
+        list.push_back(&views[i]);
+    }
+    std::cout << "Writing PanMAN" << std::endl;
+    ::mkdir("./panman", 0777);
+    const std::string out = "./panman/" + o.get("output-file") + ".panman";
+    const auto w0 = Clock::now();
+    rc = pm_panman_write(out.c_str(), list.data(), (int)list.size(), 1);
+    std::cout << "\nNetwork Write execution time: " << ns_since(w0) << " nanoseconds\n";
+    pm_panman_free(res);
+    pm_destroy(ctx);
+    if (rc != PM_OK) {
+        print_error("cannot write " + out);
+        return 1;
+    }
+    return 0;
+}
+
 int from_panman(const Options& o, int device) {
     const std::string path = o.get("input-panman");
     std::cout << "starting reading panman" << std::endl;
@@ -210,6 +270,11 @@ int from_panman(const Options& o, int device) {
         return (bool)f;
     };
     int status = 0;
+    if (o.has("reroot")) {   // src/panmanUtils.cpp:855-892, then writePanMAN
+        status = reroot(o, file, device);
+        pm_panman_free(file);
+        return status;
+    }
     if (o.has("newick")) {
         for (int i = 0; i < trees; ++i) {
             std::string s = pm_panman_newick(file, i);

@@ -90,3 +90,43 @@ def test_msa_build_then_fasta(tmp_path, low_mem):
     assert r.returncode == 0, r.stderr
     text = r.stdout[r.stdout.index(">"):r.stdout.index("\nFASTA execution time")]
     assert parse_records(text) == {k: v.replace("-", "") for k, v in rows.items()}
+
+
+@pytest.mark.gpu
+def test_reroot_command(tmp_path):
+    """--reroot -n <leaf> -d 0 -o out writes ./panman/out.panman whose FASTA equals the
+    input's (rerooting re-derives mutations, sequences are unchanged)."""
+    from _panmat import random_panmat
+    from _trees import parse_newick
+    rng = np.random.default_rng(21)
+    off, idx, root = random_tree(30, rng, max_children=3, unary=0.0)
+    names, off, idx, root = parse_newick(to_newick(off, idx, root, names_for(off)))
+    pm = random_panmat(rng, off, idx, root, names, blocks=4)
+    write_panman(str(tmp_path / "in.panman"), [pm, pm])
+    leaf = names[pm.leaves()[5]]
+    r = _run(["-I", "in.panman", "--reroot", "-n", leaf, "-d", "1", "-o", "rr"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Reroot execution time" in r.stdout
+    f = PanmanFile(str(tmp_path / "panman" / "rr.panman"))
+    assert len(f) == 2
+    nw0, nw1 = f.newick(0), f.newick(1)
+    f.close()
+    assert f"{leaf}:0.000000" in nw1 and f"{leaf}:0.000000" not in nw0
+    a = _run(["-I", "in.panman", "-m", "-o", "a"], tmp_path)
+    b = _run(["-I", "panman/rr.panman", "-m", "-o", "b"], tmp_path)
+    assert a.returncode == 0 and b.returncode == 0
+    for i in range(2):
+        ra = parse_records(open(tmp_path / "info" / f"a_{i}.msa").read())
+        rb = parse_records(open(tmp_path / "info" / f"b_{i}.msa").read())
+        assert ra == rb
+
+
+def test_reroot_command_arguments(tmp_path):
+    rng = np.random.default_rng(2)
+    off, idx, root = random_tree(8, rng, max_children=3)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2)
+    write_panman(str(tmp_path / "in.panman"), [pm])
+    r = _run(["-I", "in.panman", "--reroot", "-n", "s1", "-o", "x"], tmp_path)
+    assert r.returncode != 0 and "TreeID not provided" in r.stderr
+    r = _run(["-I", "in.panman", "--reroot", "-d", "0", "-o", "x"], tmp_path)
+    assert r.returncode != 0 and "Refence ID not provided" in r.stderr
