@@ -9,7 +9,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpanman_amd.so")
+LIB_PATH = os.environ.get("PANMAN_AMD_LIB") or os.path.join(_HERE, "libpanman_amd.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "panman_gpu.h")
 
 PM_OK = 0

@@ -181,7 +181,7 @@ __device__ __forceinline__ uint32_t node_mutations(const FusedArgs& a, int32_t r
     const uint32_t pc[4] = {q.x, q.y, q.z, q.w};
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
     uint32_t k = 0;
-    if (EMIT) k += emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[dense], self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    if (EMIT) k += emit_at(out, pos, a.shard_cap, (uint32_t)a.internal_id[dense], self_diff, word, pc, F[0], F[1], F[2], F[3]);
     else k += __builtin_popcount(self_diff);
     const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_off[e]);
     const int32_t c1 = __builtin_amdgcn_readfirstlane(a.child_off[e + 1]);
@@ -194,13 +194,13 @@ __device__ __forceinline__ uint32_t node_mutations(const FusedArgs& a, int32_t r
             const uint4 L = s.stage[sv * kWave + lane];
             const uint32_t d = valid & s.mask[sv * kWave + lane] & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
             if (!EMIT) k += __builtin_popcount(d);
-            else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[a.stage[a.stage_off[r] + sv]], d, word, F,
+            else if (d) k += emit_at(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[a.stage[a.stage_off[r] + sv]], d, word, F,
                                   L.x, L.y, L.z, L.w);
         } else {
             uint4 G;
             const uint32_t d = leaf_diff(a, cc >> 2, word, valid, F, G);
             if (!EMIT) k += __builtin_popcount(d);
-            else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[cc >> 2], d, word, F, G.x, G.y, G.z, G.w);
+            else if (d) k += emit_at(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[cc >> 2], d, word, F, G.x, G.y, G.z, G.w);
         }
     }
     return k;

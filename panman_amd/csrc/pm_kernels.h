@@ -150,18 +150,60 @@ __device__ __forceinline__ uint32_t leaf_diff(const Args& a, int32_t leaf, int64
     return m & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
 }
 
+// Record sinks.  A wave's records are first staged in LDS (positions from an LDS counter,
+// so children are processed in one pass with no re-reads); the wave then reserves global
+// space with one atomic and copies them out.  If a wave has more than kStage records the
+// pass is redone writing straight to the reserved global range (rare).
+constexpr uint32_t kStage = 512;   // records per wave (4 KiB of LDS)
+
+struct LdsSink {
+    pm_mut* buf;
+    uint32_t* cnt;
+    __device__ __forceinline__ uint32_t reserve(uint32_t k) const { return atomicAdd(cnt, k); }
+    __device__ __forceinline__ void put(uint32_t p, pm_mut m) const {
+        if (p < kStage) buf[p] = m;
+    }
+};
+
+struct GlobalSink {
+    pm_mut* out;
+    int64_t base, cap;
+    uint32_t* cnt;   // the wave's LDS counter, reset to 0
+    __device__ __forceinline__ uint32_t reserve(uint32_t k) const { return atomicAdd(cnt, k); }
+    __device__ __forceinline__ void put(uint32_t p, pm_mut m) const {
+        if (base + p < cap) out[base + p] = m;
+    }
+};
+
 // One record per changed site (src/fitchSankoff.cpp:140-166): parent gap -> NI,
 // child gap -> ND (char '-', code 0), else NS; NI/NS carry the child's code.
-__device__ __forceinline__ uint32_t emit(pm_mut* out, int64_t pos, int64_t cap, uint32_t node, uint32_t diff,
-                                         int64_t word, const uint32_t* pc, uint32_t c0, uint32_t c1,
-                                         uint32_t c2, uint32_t c3) {
+template <class Sink>
+__device__ __forceinline__ void emit(const Sink& sink, uint32_t node, uint32_t diff, int64_t word, const uint32_t* pc,
+                                     uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    if (!diff) return;
+    uint32_t p = sink.reserve((uint32_t)__builtin_popcount(diff));
+    while (diff) {
+        const int b = __builtin_ctz(diff);
+        diff &= diff - 1;
+        const uint32_t pcode = code_at(pc[0], pc[1], pc[2], pc[3], b);
+        const uint32_t c = code_at(c0, c1, c2, c3, b);
+        const uint32_t type = pcode == 0 ? PM_MUT_NI : (c == 0 ? PM_MUT_ND : PM_MUT_NS);
+        const uint32_t site = (uint32_t)(word * 32 + b);
+        sink.put(p++, pm_mut{node, (site << 8) | (type << 4) | (type == PM_MUT_ND ? 0u : c)});
+    }
+}
+
+// Same records written at out[pos...] (count returned): the region kernels' two-pass form.
+__device__ __forceinline__ uint32_t emit_at(pm_mut* out, int64_t pos, int64_t cap, uint32_t node, uint32_t diff,
+                                            int64_t word, const uint32_t* pc, uint32_t c0, uint32_t c1,
+                                            uint32_t c2, uint32_t c3) {
     uint32_t k = 0;
     while (diff) {
         const int b = __builtin_ctz(diff);
         diff &= diff - 1;
-        const uint32_t p = code_at(pc[0], pc[1], pc[2], pc[3], b);
+        const uint32_t pcode = code_at(pc[0], pc[1], pc[2], pc[3], b);
         const uint32_t c = code_at(c0, c1, c2, c3, b);
-        const uint32_t type = p == 0 ? PM_MUT_NI : (c == 0 ? PM_MUT_ND : PM_MUT_NS);
+        const uint32_t type = pcode == 0 ? PM_MUT_NI : (c == 0 ? PM_MUT_ND : PM_MUT_NS);
         const uint32_t site = (uint32_t)(word * 32 + b);
         if (pos + k < cap) out[pos + k] = pm_mut{node, (site << 8) | (type << 4) | (type == PM_MUT_ND ? 0u : c)};
         ++k;
@@ -172,10 +214,9 @@ __device__ __forceinline__ uint32_t emit(pm_mut* out, int64_t pos, int64_t cap, 
 // A virtual child v of a node with final codes Fn: its final (parent if the parent's code
 // is among its leaves', else the lowest of them -- src/fitchSankoff.cpp:115-123 on the
 // union set), its mutation and its leaf children's mutations, all in code-plane form.
-// Count only (EMIT = false) or write at out[pos...].
-template <bool EMIT>
-__device__ __forceinline__ uint32_t virtual_child(const DownArgs& a, int32_t v, int64_t word, uint32_t valid,
-                                                  const uint32_t* Fn, pm_mut* out, int64_t pos) {
+template <class Sink>
+__device__ __forceinline__ void virtual_child(const DownArgs& a, const Sink& sink, int32_t v, int64_t word,
+                                              uint32_t valid, const uint32_t* Fn) {
     const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
@@ -196,16 +237,33 @@ __device__ __forceinline__ uint32_t virtual_child(const DownArgs& a, int32_t v, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
     const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
-    uint32_t k = EMIT ? emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3])
-                      : (uint32_t)__builtin_popcount(self);
-    for (int32_t e = e0; e < e1; ++e) {
+    emit(sink, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3]);
+    for (int32_t e = e0; e < e1; ++e) {   // second touch of the same leaf words: cache hits
         const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
         uint4 L;
         const uint32_t d = leaf_diff(a, leaf, word, valid, F, L);
-        if (!EMIT) k += __builtin_popcount(d);
-        else if (d) k += emit(out, pos + k, a.shard_cap, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
+        emit(sink, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
     }
-    return k;
+}
+
+// Every record of node n's wave: the node itself, its leaf children, its virtual children.
+template <Mode M, class Sink>
+__device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int64_t word,
+                                             uint32_t valid, const uint32_t* pc, const uint32_t* F,
+                                             uint32_t self_diff) {
+    emit(sink, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        if (c >= 0) {
+            if (M == Mode::kFitch && (c & kVirtualBit)) virtual_child(a, sink, c & ~kVirtualBit, word, valid, F);
+            continue;
+        }
+        uint4 L;
+        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
+        emit(sink, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
+    }
 }
 
 // Pre-order + assignment for one node and its leaf children.  Final state:
@@ -219,9 +277,12 @@ __device__ __forceinline__ uint32_t virtual_child(const DownArgs& a, int32_t v, 
 template <Mode M>
 __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
+    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;   // whole wave leaves together
+    if (lane == 0) stage_cnt[wave] = 0;
     const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
@@ -281,34 +342,6 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     code_from_onehot(fin, F[0], F[1], F[2], F[3]);
     a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
 
-    const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-    uint32_t count = __builtin_popcount(self_diff);
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
-    // The first kCached leaf children keep their planes and masks in registers for the
-    // emission pass (binary trees: every leaf child); further ones are reloaded.
-    constexpr int kCached = 2;
-    uint4 cl[kCached];
-    uint32_t cd[kCached];
-    int32_t cid[kCached];
-    int ncached = 0;
-    for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0) {
-            if (M == Mode::kFitch && (c & kVirtualBit)) count += virtual_child<false>(a, c & ~kVirtualBit, word, valid, F, nullptr, 0);
-            continue;
-        }
-        uint4 L;
-        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
-        count += __builtin_popcount(d);
-        if (ncached < kCached) {
-#pragma unroll
-            for (int k = 0; k < kCached; ++k)
-                if (k == ncached) { cl[k] = L; cd[k] = d; cid[k] = e; }
-            ++ncached;
-        }
-    }
-
     if (is_root) {
         for (int b = 0; b < 32; ++b) {
             const int64_t site = word * 32 + b;
@@ -317,40 +350,26 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
         }
     }
 
-    uint32_t total;
-    const uint32_t excl = wave_exclusive_scan(count, total);
+    const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+    node_records<M>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, word, valid, pc, F, self_diff);
+    const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+#ifdef PM_EXP_NOEMIT
+    if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
+    return;
+#endif
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
     base = __shfl(base, 0, 64);
     pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
-    int64_t pos = (int64_t)base + excl;
-
-    pos += emit(out, pos, a.shard_cap, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-#pragma unroll
-    for (int k = 0; k < kCached; ++k) {
-        if (k >= ncached) break;
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[cid[k]]);
-        if (cd[k]) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], cd[k], word, F, cl[k].x, cl[k].y,
-                               cl[k].z, cl[k].w);
+    if (total <= kStage) {
+        for (uint32_t i = lane; i < total; i += kWave)
+            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
+        return;
     }
-    if (M == Mode::kFitch) {
-        for (int32_t e = e0; e < e1; ++e) {
-            const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-            if (c >= 0 && (c & kVirtualBit)) pos += virtual_child<true>(a, c & ~kVirtualBit, word, valid, F, out, pos);
-        }
-    }
-    if (ncached == kCached) {
-        int seen = 0;
-        for (int32_t e = e0; e < e1; ++e) {
-            const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-            if (c >= 0 || seen++ < kCached) continue;
-            uint4 L;
-            const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
-            if (d) pos += emit(out, pos, a.shard_cap, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
-        }
-    }
+    if (lane == 0) stage_cnt[wave] = 0;   // overflowed the stage: redo straight into global
+    node_records<M>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, word, valid, pc, F, self_diff);
 }
 
 }  // namespace pm
