@@ -15,6 +15,9 @@
 #include "pm_kernels.h"
 
 namespace pm {
+#ifdef PM_EXP_COUNT_COMPLEX
+__device__ unsigned long long g_exp_words[2];
+#endif
 namespace {
 
 __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
@@ -33,7 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         if (c >= 0 && (c & kVirtualBit)) virtual_set16(a, c & ~kVirtualBit, word, s);
-        else if (c >= 0) load_set16(a.sets, c, a.tiles, tile, lane, s);
+        else if (c >= 0) load_fitch_set(a.sets, a.cmask, c, a.tiles, tile, lane, s);
         else leaf_set16(a, -c - 1, word, s);
 #pragma unroll
         for (int v = 0; v < 16; ++v) { both[v] &= s[v]; either[v] |= s[v]; }
@@ -47,7 +50,22 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, s);
     }
-    store_set16(a.sets, n, a.tiles, tile, lane, s);
+    store_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, s);
+#ifdef PM_EXP_COUNT_COMPLEX
+    {
+        uint32_t one = 0, two = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) { two |= one & s[v]; one |= s[v]; }
+        const int64_t left = a.wpad * 32;   // all lanes in range count
+        (void)left;
+        const bool complex_word = (one != ~0u) || two;
+        const unsigned long long m = __ballot(complex_word);
+        if (lane == 0) {
+            atomicAdd(&g_exp_words[0], (unsigned long long)__popcll(m));
+            atomicAdd(&g_exp_words[1], 64ull);
+        }
+    }
+#endif
 }
 
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
@@ -103,6 +121,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.leaf_planes = c->leaf_planes;
     up.leaf_present = c->leaf_present;
     up.sets = reinterpret_cast<uint4*>(c->sets);
+    up.cmask = c->cmask;
     up.forced = (c->has_forced && !block) ? c->forced : nullptr;   // refState (M1); blocks force in backward
     up.absent_code0 = false;
     up.root_dense = dt.root_dense;
@@ -131,6 +150,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.leaf_planes = c->leaf_planes;
     dn.leaf_present = c->leaf_present;
     dn.sets = reinterpret_cast<const uint4*>(c->sets);
+    dn.cmask = c->cmask;
     dn.finals = c->finals;
     dn.cons = c->cons;
     dn.root_dense = dt.root_dense;
@@ -173,3 +193,9 @@ hipError_t launch_score(pm_ctx* c) {
 }
 
 }  // namespace pm
+
+#ifdef PM_EXP_COUNT_COMPLEX
+extern "C" int pm_exp_counters(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_words), 16) == hipSuccess ? 0 : -1;
+}
+#endif

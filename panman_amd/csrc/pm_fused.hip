@@ -33,6 +33,7 @@ struct FusedArgs {
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
     uint4* sets;
+    uint64_t* cmask;
     uint4* finals;
     const uint4* cons;
     const uint4* forced;
@@ -121,7 +122,7 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             } else if (kind == 2) {
                 slot_load(val, lane, x);
             } else {
-                load_set16(a.sets, val, a.tiles, tile, lane, x);
+                load_fitch_set(a.sets, a.cmask, val, a.tiles, tile, lane, x);
             }
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] &= x[v]; either[v] |= x[v]; }
@@ -134,7 +135,7 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             const uint4 F = a.forced[word];
             onehot_from_code(F.x, F.y, F.z, F.w, ~0u, x);
         }
-        if (e == n1 - 1 && root_to_hbm) store_set16(a.sets, dense, a.tiles, tile, lane, x);
+        if (e == n1 - 1 && root_to_hbm) store_fitch_set(a.sets, a.cmask, dense, a.tiles, tile, lane, x);
         else slot_store(e - n0, lane, x);
     }
 }
@@ -283,6 +284,7 @@ hipError_t launch_fitch_fused(pm_ctx* c) {
     a.leaf_planes = c->leaf_planes;
     a.leaf_present = c->leaf_present;
     a.sets = reinterpret_cast<uint4*>(c->sets);
+    a.cmask = c->cmask;
     a.finals = c->finals;
     a.cons = c->cons;
     a.forced = c->has_forced ? c->forced : nullptr;

@@ -87,10 +87,11 @@ void free_columns(pm_ctx* c) {
 
 void free_work(pm_ctx* c) {
     dev_free(c->sets);
+    dev_free(c->cmask);
     dev_free(c->finals);
     dev_free(c->recs);
     dev_free(c->shard_cnt);
-    c->sets_bytes = c->finals_bytes = 0;
+    c->sets_bytes = c->finals_bytes = c->cmask_bytes = 0;
     c->shard_cap = 0;
 }
 
@@ -120,8 +121,10 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
 // that pm_mutation_count grows on overflow.
 int alloc_work(pm_ctx* c, int mode) {
     const int64_t wpad = wpad_of(c);
-    const size_t planes = (mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH) ? 16 : 32;
+    const bool fitch = mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH;
+    const size_t planes = fitch ? 20 : 32;   // Fitch record: 5 uint4 per word slot (kFitchRec)
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
+    const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * sizeof(uint64_t);
     const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
     hipError_t e;
     if (need_sets > c->sets_bytes) {
@@ -129,6 +132,12 @@ int alloc_work(pm_ctx* c, int mode) {
         if ((e = hipMalloc(reinterpret_cast<void**>(&c->sets), need_sets)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("state sets: ") + hipGetErrorString(e));
         c->sets_bytes = need_sets;
+    }
+    if (fitch && need_mask > c->cmask_bytes) {
+        dev_free(c->cmask);
+        if ((e = hipMalloc(reinterpret_cast<void**>(&c->cmask), need_mask)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));
+        c->cmask_bytes = need_mask;
     }
     if (need_fin > c->finals_bytes) {
         dev_free(c->finals);

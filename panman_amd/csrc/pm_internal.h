@@ -3,7 +3,8 @@
 // HBM layout (one pm_ctx = one GPU = one shard of S sites, W = ceil(S/32) words):
 //   leaf planes   [L][W] uint4     4 code bit-planes of 32 sites (16 B / 32 sites)
 //   leaf present  [L][W] uint32    only for leaves with partially present columns
-//   Fitch sets    [I][W][16] u32   16 one-hot bit-planes of 32 sites (64 B / 32 sites)
+//   Fitch sets    [I][tile] records: 4 code planes per word + dense 16-plane sets for the
+//                 words holding a multi-code or empty set (pm_kernels.h store_fitch_set)
 //   Sankoff sets  [I][W][32] u32   Z0 (optimal codes) + Z1 (one above optimal) planes
 //   finals        [I][W] uint4     4 code bit-planes of the internal node's final state
 //   consensus     [W] uint4        root's parent state; forced [W] uint4 (optional)
@@ -123,8 +124,10 @@ struct pm_ctx {
     bool has_sites = false;
 
     // work buffers
-    uint32_t* sets = nullptr;         // [I][W][16 or 32]
+    uint32_t* sets = nullptr;         // Fitch: [I][tile] 320 uint4 records; Sankoff: [I][W][32]
     size_t sets_bytes = 0;
+    uint64_t* cmask = nullptr;        // Fitch: [I][tile] complex-lane masks
+    size_t cmask_bytes = 0;
     uint4* finals = nullptr;          // [I][W]
     size_t finals_bytes = 0;
     pm_mut* recs = nullptr;           // [kShards][shard_cap]

@@ -21,6 +21,7 @@ struct UpArgs {
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
     uint4* sets;
+    uint64_t* cmask;       // Fitch record masks (see store_fitch_set)
     const uint4* forced;   // nullable
     int32_t root_dense;
     int32_t tiles;
@@ -49,6 +50,62 @@ __device__ __forceinline__ void store_set16(uint4* sets, int64_t node, int32_t t
     uint4* p = sets + ((size_t)node * tiles + tile) * (Q * 64) + q0 * 64 + lane;
 #pragma unroll
     for (int q = 0; q < 4; ++q) p[q * 64] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+}
+
+// Fitch set records, compressed.  Per (node, 64-word tile): 64 entries of 4 code planes
+// (uint4 per lane, 1 KiB) for words whose 32 sets are all single codes -- the common case
+// -- and, for the other ("complex") words only, the 16 one-hot planes packed densely by
+// rank among the complex lanes (4 x 64 uint4 reserved, quad-major so each quad of the
+// complex lanes is one contiguous run).  A 64-bit mask per (node, tile) marks the complex
+// lanes.  Traffic per record: 1 KiB + 64 B per complex word instead of 4 KiB.
+constexpr int kFitchRec = 5 * kWave;   // uint4 per (node, tile)
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t* cmask, int64_t node, int32_t tiles,
+                                               int tile, int lane, uint32_t* s) {
+    const size_t rec = (size_t)node * tiles + tile;
+    const uint64_t m = cmask[rec];
+    const uint4* p = sets + rec * kFitchRec;
+    if ((m >> lane) & 1ull) {
+        const uint32_t k = lanes_below(m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[kWave + q * kWave + k];
+            s[4 * q + 0] = v.x;
+            s[4 * q + 1] = v.y;
+            s[4 * q + 2] = v.z;
+            s[4 * q + 3] = v.w;
+        }
+    } else {
+        const uint4 c = p[lane];
+        onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
+    }
+}
+
+__device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, int64_t node, int32_t tiles, int tile,
+                                                int lane, const uint32_t* s) {
+    uint32_t one = 0, two = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        two |= one & s[v];
+        one |= s[v];
+    }
+    const bool complex_word = (one != ~0u) || two != 0u;   // an empty or multi-code set
+    const uint64_t m = __ballot(complex_word);
+    const size_t rec = (size_t)node * tiles + tile;
+    uint4* p = sets + rec * kFitchRec;
+    uint32_t c0, c1, c2, c3;
+    code_from_onehot(s, c0, c1, c2, c3);
+    p[lane] = make_uint4(c0, c1, c2, c3);   // every lane: whole lines written
+    if (complex_word) {
+        const uint32_t k = lanes_below(m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+    }
+    if (lane == 0) cmask[rec] = m;
 }
 
 // Leaf child as a one-hot set: src/fitchSankoff.cpp:32-38 (absent leaf -> 0).
@@ -105,6 +162,7 @@ struct DownArgs {
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
     const uint4* sets;
+    const uint64_t* cmask;
     uint4* finals;
     const uint4* cons;
     int32_t root_dense;
@@ -217,15 +275,24 @@ __device__ __forceinline__ uint32_t emit_at(pm_mut* out, int64_t pos, int64_t ca
 template <class Sink>
 __device__ __forceinline__ void virtual_child(const DownArgs& a, const Sink& sink, int32_t v, int64_t word,
                                               uint32_t valid, const uint32_t* Fn) {
+    constexpr int kKeep = 2;   // leaves whose planes stay in registers for the emission loop
     const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
     const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
+    uint4 keep[kKeep];
+    uint32_t keep_m[kKeep];
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
         const uint8_t flag = a.leaf_flag[leaf];
-        if (flag == kLeafAbsent) continue;
-        const uint4 L = a.leaf_planes[(size_t)leaf * a.wpad + word];
-        const uint32_t m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
+        uint4 L = make_uint4(0, 0, 0, 0);
+        uint32_t m = 0;
+        if (flag != kLeafAbsent) {
+            L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+            m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kKeep; ++k)
+            if (e - e0 == k) { keep[k] = L; keep_m[k] = m; }
         const uint32_t C[4] = {L.x, L.y, L.z, L.w};
         hit |= m & ~((C[0] ^ Fn[0]) | (C[1] ^ Fn[1]) | (C[2] ^ Fn[2]) | (C[3] ^ Fn[3]));
         const uint32_t take = m & (~have | code_less(C, low));
@@ -238,7 +305,15 @@ __device__ __forceinline__ void virtual_child(const DownArgs& a, const Sink& sin
     for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
     const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
     emit(sink, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3]);
-    for (int32_t e = e0; e < e1; ++e) {   // second touch of the same leaf words: cache hits
+#pragma unroll
+    for (int k = 0; k < kKeep; ++k) {
+        if (e0 + k >= e1) break;
+        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e0 + k]) - 1;
+        const uint4 L = keep[k];
+        const uint32_t d = keep_m[k] & valid & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
+        emit(sink, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
+    }
+    for (int32_t e = e0 + kKeep; e < e1; ++e) {   // further leaves: second touch, cache hits
         const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
         uint4 L;
         const uint32_t d = leaf_diff(a, leaf, word, valid, F, L);
@@ -289,7 +364,8 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     const uint32_t valid = valid_mask(a, word);
 
     uint32_t own[16], P[16], fin[16], pc[4];
-    load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
+    if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
+    else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
     const bool is_root = n == a.root_dense;
     {
         uint4 q = is_root ? a.cons[word] : a.finals[(size_t)a.parent_dense[n] * a.wpad + word];
