@@ -110,7 +110,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const bool virt = !block && c->virtual_leaf_parents;
     const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
     const int32_t* up_order = virt ? dt.up_order_v : dt.up_order;
-    const int32_t* down_order = virt ? dt.down_order_v : dt.down_order;
+    const int4* down_desc = reinterpret_cast<const int4*>(virt ? dt.down_desc_v : dt.down_desc);
     const std::vector<int32_t>& up_off = virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
 
@@ -164,9 +164,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.root_code = c->root_code;
     dn.forced = (c->has_forced && block) ? c->forced : nullptr;
     dn.absent_code0 = false;
+    dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
+    dn.all_present = c->leaves_all_present;
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
-        dn.order = down_order + down_off[d];
+        dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);

@@ -60,6 +60,9 @@ void free_tree(DevTree& t) {
     dev_free(t.child_enc_v);
     dev_free(t.up_order_v);
     dev_free(t.down_order_v);
+    dev_free(t.down_desc);
+    dev_free(t.down_desc_v);
+    dev_free(t.vleaf);
     dev_free(t.rg_node_off);
     dev_free(t.rg_node_dense);
     dev_free(t.rg_node_pslot);
@@ -377,6 +380,7 @@ int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_st
     hipError_t e = upload(&d_rows, row_of_leaf, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(c->leaf_flag, flag.data(), L, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_pack_codes(c, d_codes4, row_stride, d_rows, nullptr, 0);
+    c->leaves_all_present = std::all_of(flag.begin(), flag.end(), [](uint8_t f) { return f == kLeafPresent; });
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(d_rows);
     if (e != hipSuccess) return hip_fail(c, e, "leaf install");
@@ -551,7 +555,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 
     // virtual leaf-parents (Fitch level kernels)
-    std::vector<int32_t> child_enc_v(ht.child_enc), up_order_v, down_order_v;
+    std::vector<int32_t> child_enc_v(ht.child_enc), up_order_v, down_order_v, vleaf((size_t)I * 4, -1);
     {
         std::vector<uint8_t> virt(I, 0);
         for (int32_t d = 0; d < I; ++d) {
@@ -564,6 +568,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
         for (auto& x : child_enc_v)
             if (x >= 0 && virt[x]) x |= kVirtualBit;
+        for (int32_t d = 0; d < I; ++d)
+            if (virt[d])
+                for (int32_t e = ht.child_off[d], k = 0; e < ht.child_off[d + 1]; ++e, ++k)
+                    vleaf[(size_t)d * 4 + k] = -ht.child_enc[e] - 1;
         bucket(H, I, [&](int32_t d) { return virt[d] ? H - 1 : height[ht.internal_id[d]] - 1; }, ht.up_level_off_v,
                up_order_v);
         bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
@@ -582,6 +590,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         strip(up_order_v, ht.up_level_off_v, true);
         strip(down_order_v, ht.down_level_off_v, false);
     }
+
+    auto make_desc = [&](const std::vector<int32_t>& order) {
+        std::vector<int32_t> desc(order.size() * 4);
+        for (size_t k = 0; k < order.size(); ++k) {
+            const int32_t d = order[k];
+            desc[4 * k + 0] = d;
+            desc[4 * k + 1] = parent_dense[d];
+            desc[4 * k + 2] = ht.child_off[d];
+            desc[4 * k + 3] = ht.child_off[d + 1];
+        }
+        return desc;
+    };
+    const std::vector<int32_t> down_desc = make_desc(down_order), down_desc_v = make_desc(down_order_v);
 
     Regions rg;
     build_regions(bfs, off, idx, t->root, ht, rg);
@@ -608,6 +629,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.child_enc_v, child_enc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.up_order_v, up_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_order_v, down_order_v, c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_desc, down_desc, c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
+        (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_dense, rg.node_dense, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_pslot, rg.node_pslot, c->stream)) != hipSuccess ||
@@ -669,6 +693,7 @@ int pm_leaves_upload(pm_ctx* c, int64_t S, const uint8_t* codes4, int64_t row_st
     if (e == hipSuccess && present) e = hipMemcpyAsync(d_present, present, pres_bytes, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(c->leaf_flag, flag.data(), L, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_pack_codes(c, d_codes, row_stride, d_rows, d_present, present_stride);
+    c->leaves_all_present = std::all_of(flag.begin(), flag.end(), [](uint8_t f) { return f == kLeafPresent; });
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(d_codes);
     dev_free(d_rows);
@@ -807,6 +832,7 @@ int pm_synth_columns(pm_ctx* c, int64_t site_begin, int64_t S, uint64_t seed) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "synthetic columns");
     c->has_leaves = c->has_sites = true;
+    c->leaves_all_present = true;
     c->has_forced = false;
     return PM_OK;
 }

@@ -52,6 +52,11 @@ struct DevTree {
     int32_t* child_enc_v = nullptr;   // [E] as child_enc, virtual children tagged kVirtualBit
     int32_t* up_order_v = nullptr;    // [I'] materialised internal nodes by height
     int32_t* down_order_v = nullptr;  // [I'] materialised internal nodes by depth
+    // down-pass item descriptors {node, parent, first child, end child} (int4), in
+    // down_order / down_order_v order, and each virtual node's leaves (int4, -1 padded)
+    int32_t* down_desc = nullptr;
+    int32_t* down_desc_v = nullptr;
+    int32_t* vleaf = nullptr;
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
     int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
@@ -121,6 +126,7 @@ struct pm_ctx {
     uint4* forced = nullptr;          // [W]
     bool has_forced = false;
     bool has_leaves = false;
+    bool leaves_all_present = false;   // every leaf row present at every site
     bool has_sites = false;
 
     // work buffers

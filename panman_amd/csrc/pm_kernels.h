@@ -151,8 +151,10 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 }
 
 struct DownArgs {
-    const int32_t* order;
+    const int4* desc;      // per level item: {node, parent (dense, -1 root), first child, end child}
     int32_t count;
+    const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
+    bool all_present;      // every leaf row fully present: no flag / presence loads
     const int32_t* child_off;
     const int32_t* child_enc;
     const int32_t* parent_dense;
@@ -269,75 +271,132 @@ __device__ __forceinline__ uint32_t emit_at(pm_mut* out, int64_t pos, int64_t ca
     return k;
 }
 
-// A virtual child v of a node with final codes Fn: its final (parent if the parent's code
-// is among its leaves', else the lowest of them -- src/fitchSankoff.cpp:115-123 on the
-// union set), its mutation and its leaf children's mutations, all in code-plane form.
-template <class Sink>
-__device__ __forceinline__ void virtual_child(const DownArgs& a, const Sink& sink, int32_t v, int64_t word,
-                                              uint32_t valid, const uint32_t* Fn) {
-    constexpr int kKeep = 2;   // leaves whose planes stay in registers for the emission loop
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[v]);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[v + 1]);
-    uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
-    uint4 keep[kKeep];
-    uint32_t keep_m[kKeep];
-    for (int32_t e = e0; e < e1; ++e) {
-        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
-        const uint8_t flag = a.leaf_flag[leaf];
-        uint4 L = make_uint4(0, 0, 0, 0);
-        uint32_t m = 0;
-        if (flag != kLeafAbsent) {
-            L = a.leaf_planes[(size_t)leaf * a.wpad + word];
-            m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kKeep; ++k)
-            if (e - e0 == k) { keep[k] = L; keep_m[k] = m; }
-        const uint32_t C[4] = {L.x, L.y, L.z, L.w};
-        hit |= m & ~((C[0] ^ Fn[0]) | (C[1] ^ Fn[1]) | (C[2] ^ Fn[2]) | (C[3] ^ Fn[3]));
-        const uint32_t take = m & (~have | code_less(C, low));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) low[j] = (C[j] & take) | (low[j] & ~take);
-        have |= m;
+// A leaf word for emission: its code planes L and the mask of sites where it can carry a
+// mutation (leaf_diff's rules: absent leaves none -- or, block Sankoff, state 0 everywhere;
+// partially present rows their present sites).  For Fitch the mask is the presence mask.
+template <class Args>
+__device__ __forceinline__ void leaf_fetch(const Args& a, int32_t leaf, int64_t word, uint4& L, uint32_t& mv) {
+    if (a.all_present) {
+        L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+        mv = ~0u;
+        return;
     }
+    const uint8_t flag = a.leaf_flag[leaf];
+    if (flag == kLeafAbsent) {
+        L = make_uint4(0, 0, 0, 0);
+        mv = a.absent_code0 ? ~0u : 0u;
+        return;
+    }
+    L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+    mv = ~0u;
+    if (flag == kLeafPartial) {
+        const uint32_t p = a.leaf_present[(size_t)leaf * a.wpad + word];
+        if (a.absent_code0) {
+            L.x &= p; L.y &= p; L.z &= p; L.w &= p;
+        } else {
+            mv = p;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t diff4(const uint4& L, const uint32_t* F) {
+    return (L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]);
+}
+
+// One of the first two children of a node, fetched before the node's own state is known
+// (leaf: its word; virtual leaf-parent: its first two leaves' words).
+struct Kid {
+    int32_t enc = 0;
+    int4 vl = make_int4(-1, -1, -1, -1);
+    uint4 L0 = make_uint4(0, 0, 0, 0), L1 = make_uint4(0, 0, 0, 0);
+    uint32_t m0 = 0, m1 = 0;
+};
+
+template <Mode M>
+__device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int64_t word, Kid& k) {
+    k.enc = enc;
+    if (enc < 0) {
+        leaf_fetch(a, -enc - 1, word, k.L0, k.m0);
+    } else if (M == Mode::kFitch && (enc & kVirtualBit)) {
+        const int4 vl = a.vleaf[enc & ~kVirtualBit];
+        k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
+                         __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
+        leaf_fetch(a, k.vl.x, word, k.L0, k.m0);
+        if (k.vl.y >= 0) leaf_fetch(a, k.vl.y, word, k.L1, k.m1);
+    }
+}
+
+// Fold one leaf into a virtual node's union / lowest code / "parent code present" masks.
+__device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint32_t* Fn, uint32_t* low, uint32_t& have,
+                                          uint32_t& hit) {
+    const uint32_t C[4] = {L.x, L.y, L.z, L.w};
+    hit |= m & ~((C[0] ^ Fn[0]) | (C[1] ^ Fn[1]) | (C[2] ^ Fn[2]) | (C[3] ^ Fn[3]));
+    const uint32_t take = m & (~have | code_less(C, low));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) low[j] = (C[j] & take) | (low[j] & ~take);
+    have |= m;
+}
+
+// A virtual child (its leaves in k.vl, the first two prefetched) of a node with final codes
+// Fn: its final (parent if the parent's code is among its leaves', else the lowest of them
+// -- src/fitchSankoff.cpp:115-123 on the union set), its mutation and its leaves'.
+template <class Sink>
+__device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
+                                            uint32_t valid, const uint32_t* Fn) {
+    const int32_t v = k.enc & ~kVirtualBit;
+    const int32_t more[2] = {k.vl.z, k.vl.w};
+    uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
+    virt_fold(k.L0, k.m0, Fn, low, have, hit);
+    virt_fold(k.L1, k.m1, Fn, low, have, hit);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        if (more[j] >= 0) {
+            uint4 L;
+            uint32_t m;
+            leaf_fetch(a, more[j], word, L, m);
+            virt_fold(L, m, Fn, low, have, hit);
+        }
     uint32_t F[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
     const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
     emit(sink, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3]);
+    emit(sink, (uint32_t)a.leaf_id[k.vl.x], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
+    if (k.vl.y >= 0)
+        emit(sink, (uint32_t)a.leaf_id[k.vl.y], valid & k.m1 & diff4(k.L1, F), word, F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
 #pragma unroll
-    for (int k = 0; k < kKeep; ++k) {
-        if (e0 + k >= e1) break;
-        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e0 + k]) - 1;
-        const uint4 L = keep[k];
-        const uint32_t d = keep_m[k] & valid & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
-        emit(sink, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
-    }
-    for (int32_t e = e0 + kKeep; e < e1; ++e) {   // further leaves: second touch, cache hits
-        const int32_t leaf = -__builtin_amdgcn_readfirstlane(a.child_enc[e]) - 1;
-        uint4 L;
-        const uint32_t d = leaf_diff(a, leaf, word, valid, F, L);
-        emit(sink, (uint32_t)a.leaf_id[leaf], d, word, F, L.x, L.y, L.z, L.w);
-    }
+    for (int j = 0; j < 2; ++j)
+        if (more[j] >= 0) {   // third / fourth leaf: second touch, cache hits
+            uint4 L;
+            uint32_t m;
+            leaf_fetch(a, more[j], word, L, m);
+            emit(sink, (uint32_t)a.leaf_id[more[j]], valid & m & diff4(L, F), word, F, L.x, L.y, L.z, L.w);
+        }
 }
 
-// Every record of node n's wave: the node itself, its leaf children, its virtual children.
 template <Mode M, class Sink>
-__device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int64_t word,
-                                             uint32_t valid, const uint32_t* pc, const uint32_t* F,
-                                             uint32_t self_diff) {
+__device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
+                                            uint32_t valid, const uint32_t* F) {
+    if (k.enc < 0)
+        emit(sink, (uint32_t)a.leaf_id[-k.enc - 1], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z,
+             k.L0.w);
+    else if (M == Mode::kFitch && (k.enc & kVirtualBit))
+        virtual_kid(a, sink, k, word, valid, F);
+}
+
+// Every record of node n's wave: the node itself and its children (the first two from
+// registers, further ones fetched here).
+template <Mode M, class Sink>
+__device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int32_t e0, int32_t e1,
+                                             const Kid* kids, int64_t word, uint32_t valid, const uint32_t* pc,
+                                             const uint32_t* F, uint32_t self_diff) {
     emit(sink, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
-    for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0) {
-            if (M == Mode::kFitch && (c & kVirtualBit)) virtual_child(a, sink, c & ~kVirtualBit, word, valid, F);
-            continue;
-        }
-        uint4 L;
-        const uint32_t d = leaf_diff(a, -c - 1, word, valid, F, L);
-        emit(sink, (uint32_t)a.leaf_id[-c - 1], d, word, F, L.x, L.y, L.z, L.w);
+    kid_records<M>(a, sink, kids[0], word, valid, F);
+    if (e1 - e0 > 1) kid_records<M>(a, sink, kids[1], word, valid, F);
+    for (int32_t e = e0 + 2; e < e1; ++e) {
+        Kid k;
+        kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), word, k);
+        kid_records<M>(a, sink, k, word, valid, F);
     }
 }
 
@@ -349,6 +408,8 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
 //           one above optimal, Z1); an all-INF subtree (Z0 == 0) stays unresolved (-1).
 // Leaf children keep their own code in both modes.  Mutations (:131-171, :676-703):
 // parent code 0 -> NI, child code 0 -> ND, else NS.
+// Every load that does not depend on the parent's final (own set, parent final, the
+// first two children's words) is issued before any of them is consumed.
 template <Mode M>
 __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
@@ -358,19 +419,26 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;   // whole wave leaves together
     if (lane == 0) stage_cnt[wave] = 0;
-    const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
+    const int4 d = a.desc[item];
+    const int32_t n = __builtin_amdgcn_readfirstlane(d.x);
+    const int32_t parent = __builtin_amdgcn_readfirstlane(d.y);
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(d.z);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(d.w);
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
+    const bool is_root = parent < 0;
 
     uint32_t own[16], P[16], fin[16], pc[4];
-    if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
-    else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
-    const bool is_root = n == a.root_dense;
     {
-        uint4 q = is_root ? a.cons[word] : a.finals[(size_t)a.parent_dense[n] * a.wpad + word];
+        const uint4 q = is_root ? a.cons[word] : a.finals[(size_t)parent * a.wpad + word];
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
+    Kid kids[2];
+    kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0]), word, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0 + 1]), word, kids[1]);
+    if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
+    else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
     onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
     uint32_t pres;
     if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
@@ -427,7 +495,7 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     }
 
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-    node_records<M>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, word, valid, pc, F, self_diff);
+    node_records<M>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
 #ifdef PM_EXP_NOEMIT
     if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
@@ -445,7 +513,8 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
         return;
     }
     if (lane == 0) stage_cnt[wave] = 0;   // overflowed the stage: redo straight into global
-    node_records<M>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, word, valid, pc, F, self_diff);
+    node_records<M>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc,
+                    F, self_diff);
 }
 
 }  // namespace pm

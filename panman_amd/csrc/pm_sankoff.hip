@@ -146,9 +146,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.root_code = c->root_code;
     dn.forced = c->has_forced ? c->forced : nullptr;
     dn.absent_code0 = block;
+    dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
+    dn.all_present = c->leaves_all_present;
     const int D = (int)ht.down_level_off.size() - 1;
     for (int d = 0; d < D; ++d) {
-        dn.order = dt.down_order + ht.down_level_off[d];
+        dn.desc = reinterpret_cast<const int4*>(dt.down_desc) + ht.down_level_off[d];
         dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);

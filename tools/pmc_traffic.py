@@ -19,7 +19,7 @@ import sys
 
 def per_kernel(d, counter):
     agg = collections.defaultdict(lambda: [0, 0.0])
-    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
