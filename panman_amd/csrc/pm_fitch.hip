@@ -20,7 +20,10 @@ __device__ unsigned long long g_exp_words[2];
 #endif
 namespace {
 
-__global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
+#ifndef PM_UP_WAVES
+#define PM_UP_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, PM_UP_WAVES) void k_fitch_up(UpArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;
@@ -165,7 +168,6 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.forced = (c->has_forced && block) ? c->forced : nullptr;
     dn.absent_code0 = false;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
-    dn.all_present = c->leaves_all_present;
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.desc = down_desc + down_off[d];
@@ -173,8 +175,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         if (dn.count == 0) continue;
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
-        if (block) hipLaunchKernelGGL(k_down<Mode::kBlockFitch>, grid, dim3(kBlock), 0, c->stream, dn);
-        else hipLaunchKernelGGL(k_down<Mode::kFitch>, grid, dim3(kBlock), 0, c->stream, dn);
+        const bool ap = c->leaves_all_present;
+        if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (block) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_down<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
     return hipGetLastError();

@@ -154,7 +154,6 @@ struct DownArgs {
     const int4* desc;      // per level item: {node, parent (dense, -1 root), first child, end child}
     int32_t count;
     const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
-    bool all_present;      // every leaf row fully present: no flag / presence loads
     const int32_t* child_off;
     const int32_t* child_enc;
     const int32_t* parent_dense;
@@ -274,9 +273,9 @@ __device__ __forceinline__ uint32_t emit_at(pm_mut* out, int64_t pos, int64_t ca
 // A leaf word for emission: its code planes L and the mask of sites where it can carry a
 // mutation (leaf_diff's rules: absent leaves none -- or, block Sankoff, state 0 everywhere;
 // partially present rows their present sites).  For Fitch the mask is the presence mask.
-template <class Args>
+template <bool AP, class Args>
 __device__ __forceinline__ void leaf_fetch(const Args& a, int32_t leaf, int64_t word, uint4& L, uint32_t& mv) {
-    if (a.all_present) {
+    if (AP) {
         L = a.leaf_planes[(size_t)leaf * a.wpad + word];
         mv = ~0u;
         return;
@@ -312,17 +311,17 @@ struct Kid {
     uint32_t m0 = 0, m1 = 0;
 };
 
-template <Mode M>
+template <Mode M, bool AP>
 __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int64_t word, Kid& k) {
     k.enc = enc;
     if (enc < 0) {
-        leaf_fetch(a, -enc - 1, word, k.L0, k.m0);
+        leaf_fetch<AP>(a, -enc - 1, word, k.L0, k.m0);
     } else if (M == Mode::kFitch && (enc & kVirtualBit)) {
         const int4 vl = a.vleaf[enc & ~kVirtualBit];
         k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                          __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
-        leaf_fetch(a, k.vl.x, word, k.L0, k.m0);
-        if (k.vl.y >= 0) leaf_fetch(a, k.vl.y, word, k.L1, k.m1);
+        leaf_fetch<AP>(a, k.vl.x, word, k.L0, k.m0);
+        if (k.vl.y >= 0) leaf_fetch<AP>(a, k.vl.y, word, k.L1, k.m1);
     }
 }
 
@@ -340,7 +339,7 @@ __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint
 // A virtual child (its leaves in k.vl, the first two prefetched) of a node with final codes
 // Fn: its final (parent if the parent's code is among its leaves', else the lowest of them
 // -- src/fitchSankoff.cpp:115-123 on the union set), its mutation and its leaves'.
-template <class Sink>
+template <bool AP, class Sink>
 __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
                                             uint32_t valid, const uint32_t* Fn) {
     const int32_t v = k.enc & ~kVirtualBit;
@@ -353,7 +352,7 @@ __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink,
         if (more[j] >= 0) {
             uint4 L;
             uint32_t m;
-            leaf_fetch(a, more[j], word, L, m);
+            leaf_fetch<AP>(a, more[j], word, L, m);
             virt_fold(L, m, Fn, low, have, hit);
         }
     uint32_t F[4];
@@ -369,34 +368,34 @@ __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink,
         if (more[j] >= 0) {   // third / fourth leaf: second touch, cache hits
             uint4 L;
             uint32_t m;
-            leaf_fetch(a, more[j], word, L, m);
+            leaf_fetch<AP>(a, more[j], word, L, m);
             emit(sink, (uint32_t)a.leaf_id[more[j]], valid & m & diff4(L, F), word, F, L.x, L.y, L.z, L.w);
         }
 }
 
-template <Mode M, class Sink>
+template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
                                             uint32_t valid, const uint32_t* F) {
     if (k.enc < 0)
         emit(sink, (uint32_t)a.leaf_id[-k.enc - 1], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z,
              k.L0.w);
     else if (M == Mode::kFitch && (k.enc & kVirtualBit))
-        virtual_kid(a, sink, k, word, valid, F);
+        virtual_kid<AP>(a, sink, k, word, valid, F);
 }
 
 // Every record of node n's wave: the node itself and its children (the first two from
 // registers, further ones fetched here).
-template <Mode M, class Sink>
+template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int32_t e0, int32_t e1,
                                              const Kid* kids, int64_t word, uint32_t valid, const uint32_t* pc,
                                              const uint32_t* F, uint32_t self_diff) {
     emit(sink, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_records<M>(a, sink, kids[0], word, valid, F);
-    if (e1 - e0 > 1) kid_records<M>(a, sink, kids[1], word, valid, F);
+    kid_records<M, AP>(a, sink, kids[0], word, valid, F);
+    if (e1 - e0 > 1) kid_records<M, AP>(a, sink, kids[1], word, valid, F);
     for (int32_t e = e0 + 2; e < e1; ++e) {
         Kid k;
-        kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), word, k);
-        kid_records<M>(a, sink, k, word, valid, F);
+        kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), word, k);
+        kid_records<M, AP>(a, sink, k, word, valid, F);
     }
 }
 
@@ -410,8 +409,10 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
 // parent code 0 -> NI, child code 0 -> ND, else NS.
 // Every load that does not depend on the parent's final (own set, parent final, the
 // first two children's words) is issued before any of them is consumed.
-template <Mode M>
-__global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
+// Fitch with all leaves present sits 2 VGPRs over the 8-wave budget; capping it there
+// (3 spilled VGPRs) measured 2 % faster at N*.  The other modes keep their natural size.
+template <Mode M, bool AP>
+__global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_down(DownArgs a) {
     constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
@@ -429,36 +430,47 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     const uint32_t valid = valid_mask(a, word);
     const bool is_root = parent < 0;
 
-    uint32_t own[16], P[16], fin[16], pc[4];
+    uint32_t own[16], pc[4], F[4];
     {
         const uint4 q = is_root ? a.cons[word] : a.finals[(size_t)parent * a.wpad + word];
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
     Kid kids[2];
-    kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0]), word, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0 + 1]), word, kids[1]);
+    kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0]), word, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0 + 1]), word, kids[1]);
     if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
     else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
-    onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
     uint32_t pres;
     if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
-        pres = any_plane(own);   // state 0: subtree absent, skipped (:101-103, :136-138)
-        lowest_code(own, fin);
-        const bool generic = !is_root || M == Mode::kBlockFitch;   // block root: parent & own rule (:249-264)
-        if (generic) {
-            // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:115-123)
-            uint32_t hit = 0;
+        // One sweep over the 16 planes from code 15 down to 0: "parent code in own set"
+        // (hit), any code present, and the lowest present code in code-plane form.
+        const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
+        uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int v = 0; v < 16; ++v) hit |= P[v] & own[v];
+        for (int v = 15; v >= 0; --v) {
+            const uint32_t o = own[v];
+            const uint32_t is_v = ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) & ((v & 4) ? pc[2] : np[2]) &
+                                  ((v & 8) ? pc[3] : np[3]);
+            hit |= is_v & o;
+            any |= o;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) fin[v] = (P[v] & hit) | (fin[v] & ~hit);
+            for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
         }
+        pres = any;   // state 0: subtree absent, skipped (:101-103, :136-138)
+        // root: lowest code of its set; otherwise (and always for blocks, :249-264)
+        // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:98-123)
+        const bool generic = !is_root || M == Mode::kBlockFitch;
+        if (!generic) hit = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
         if (M == Mode::kBlockFitch && is_root && a.forced) {   // defaultValue (:249-250)
             const uint4 f = a.forced[word];
-            onehot_from_code(f.x, f.y, f.z, f.w, ~0u, fin);
+            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
             pres = ~0u;
         }
     } else {
+        uint32_t P[16], fin[16];
+        onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
         if (is_root) {
             if (a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
                 const uint4 f = a.forced[word];
@@ -481,9 +493,8 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
             for (int v = 0; v < 16; ++v) fin[v] = ((P[v] & hit) | (low[v] & ~hit)) & live;
         }
         pres = any_plane(fin);
+        code_from_onehot(fin, F[0], F[1], F[2], F[3]);
     }
-    uint32_t F[4];
-    code_from_onehot(fin, F[0], F[1], F[2], F[3]);
     a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
 
     if (is_root) {
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
     }
 
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-    node_records<M>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
+    node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
 #ifdef PM_EXP_NOEMIT
     if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
@@ -513,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_down(DownArgs a) {
         return;
     }
     if (lane == 0) stage_cnt[wave] = 0;   // overflowed the stage: redo straight into global
-    node_records<M>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc,
+    node_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc,
                     F, self_diff);
 }
 

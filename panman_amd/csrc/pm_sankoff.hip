@@ -147,14 +147,14 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.forced = c->has_forced ? c->forced : nullptr;
     dn.absent_code0 = block;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
-    dn.all_present = c->leaves_all_present;
     const int D = (int)ht.down_level_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.desc = reinterpret_cast<const int4*>(dt.down_desc) + ht.down_level_off[d];
         dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
-        hipLaunchKernelGGL(k_down<Mode::kSankoff>, grid, dim3(kBlock), 0, c->stream, dn);
+        if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_down<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
     return hipGetLastError();
