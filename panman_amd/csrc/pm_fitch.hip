@@ -20,47 +20,40 @@ __device__ unsigned long long g_exp_words[2];
 #endif
 namespace {
 
-#ifndef PM_UP_WAVES
-#define PM_UP_WAVES 1
-#endif
-__global__ __launch_bounds__(kBlock, PM_UP_WAVES) void k_fitch_up(UpArgs a) {
+// One wave = (node, tile).  Children are folded straight into the AND / OR accumulators
+// (src/fitchSankoff.cpp:39-55); the first two children's loads are independent and issued
+// back to back.
+template <bool AP>
+__global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;
-    const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
+    const int4 d = a.desc[item];
+    const int32_t n = __builtin_amdgcn_readfirstlane(d.x);
+    const int32_t e0 = __builtin_amdgcn_readfirstlane(d.y);
+    const int32_t e1 = __builtin_amdgcn_readfirstlane(d.z);
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
-    uint32_t both[16], either[16], s[16];
+    uint32_t both[16], either[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
-    for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        if (c >= 0 && (c & kVirtualBit)) virtual_set16(a, c & ~kVirtualBit, word, s);
-        else if (c >= 0) load_fitch_set(a.sets, a.cmask, c, a.tiles, tile, lane, s);
-        else leaf_set16(a, -c - 1, word, s);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) { both[v] &= s[v]; either[v] |= s[v]; }
-    }
+    for (int32_t e = e0; e < e1; ++e) fold_child<AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), tile, lane, word, both, either);
     // AND if non-empty, else OR (src/fitchSankoff.cpp:48-55)
     const uint32_t nz = any_plane(both);
 #pragma unroll
-    for (int v = 0; v < 16; ++v) s[v] = both[v] | (either[v] & ~nz);
+    for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
     if (n == a.root_dense && a.forced != nullptr) {
         // refState replaces the root's set (src/fitchSankoff.cpp:45-47)
         const uint4 F = a.forced[word];
-        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, s);
+        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    store_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, s);
+    store_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, both);
 #ifdef PM_EXP_COUNT_COMPLEX
     {
         uint32_t one = 0, two = 0;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) { two |= one & s[v]; one |= s[v]; }
-        const int64_t left = a.wpad * 32;   // all lanes in range count
-        (void)left;
+        for (int v = 0; v < 16; ++v) { two |= one & both[v]; one |= both[v]; }
         const bool complex_word = (one != ~0u) || two;
         const unsigned long long m = __ballot(complex_word);
         if (lane == 0) {
@@ -112,7 +105,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     // Fitch (not block Fitch) may skip materialising leaf-parents
     const bool virt = !block && c->virtual_leaf_parents;
     const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
-    const int32_t* up_order = virt ? dt.up_order_v : dt.up_order;
+    const int4* up_desc = reinterpret_cast<const int4*>(virt ? dt.up_desc_v : dt.up_desc);
     const int4* down_desc = reinterpret_cast<const int4*>(virt ? dt.down_desc_v : dt.down_desc);
     const std::vector<int32_t>& up_off = virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
@@ -125,6 +118,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.leaf_present = c->leaf_present;
     up.sets = reinterpret_cast<uint4*>(c->sets);
     up.cmask = c->cmask;
+    up.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     up.forced = (c->has_forced && !block) ? c->forced : nullptr;   // refState (M1); blocks force in backward
     up.absent_code0 = false;
     up.root_dense = dt.root_dense;
@@ -132,12 +126,13 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.wpad = wpad;
     const int H = (int)up_off.size() - 1;
     for (int h = 0; h < H; ++h) {
-        up.order = up_order + up_off[h];
+        up.desc = up_desc + up_off[h];
         up.count = up_off[h + 1] - up_off[h];
         if (up.count == 0) continue;
         dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 0);
-        hipLaunchKernelGGL(k_fitch_up, grid, dim3(kBlock), 0, c->stream, up);
+        if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up<true>, grid, dim3(kBlock), 0, c->stream, up);
+        else hipLaunchKernelGGL(k_fitch_up<false>, grid, dim3(kBlock), 0, c->stream, up);
         timer_end(c, 0);
     }
 

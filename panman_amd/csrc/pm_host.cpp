@@ -61,6 +61,8 @@ void free_tree(DevTree& t) {
     dev_free(t.up_order_v);
     dev_free(t.down_order_v);
     dev_free(t.down_desc);
+    dev_free(t.up_desc);
+    dev_free(t.up_desc_v);
     dev_free(t.down_desc_v);
     dev_free(t.vleaf);
     dev_free(t.rg_node_off);
@@ -603,6 +605,17 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         return desc;
     };
     const std::vector<int32_t> down_desc = make_desc(down_order), down_desc_v = make_desc(down_order_v);
+    auto make_up_desc = [&](const std::vector<int32_t>& order) {
+        std::vector<int32_t> desc(order.size() * 4, 0);
+        for (size_t k = 0; k < order.size(); ++k) {
+            const int32_t d = order[k];
+            desc[4 * k + 0] = d;
+            desc[4 * k + 1] = ht.child_off[d];
+            desc[4 * k + 2] = ht.child_off[d + 1];
+        }
+        return desc;
+    };
+    const std::vector<int32_t> up_desc = make_up_desc(up_order), up_desc_v = make_up_desc(up_order_v);
 
     Regions rg;
     build_regions(bfs, off, idx, t->root, ht, rg);
@@ -630,6 +643,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_order_v, up_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_order_v, down_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc, down_desc, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc, up_desc, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_v, up_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||

@@ -55,6 +55,8 @@ struct DevTree {
     // down-pass item descriptors {node, parent, first child, end child} (int4), in
     // down_order / down_order_v order, and each virtual node's leaves (int4, -1 padded)
     int32_t* down_desc = nullptr;
+    int32_t* up_desc = nullptr;       // {node, first child, end child, 0} in up_order order
+    int32_t* up_desc_v = nullptr;
     int32_t* down_desc_v = nullptr;
     int32_t* vleaf = nullptr;
     // subtree regions for the fused Fitch kernels (pm_fused.hip)

@@ -13,7 +13,9 @@ namespace pm {
 enum class Mode { kFitch, kSankoff, kBlockFitch };
 
 struct UpArgs {
-    const int32_t* order;
+    const int32_t* order;  // Sankoff: level items
+    const int4* desc;      // Fitch: level items {node, first child, end child, -}
+    const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;
     const int32_t* child_enc;
@@ -106,6 +108,122 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, in
         for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
     }
     if (lane == 0) cmask[rec] = m;
+}
+
+// ---- Fitch post-order folding: (both, either) accumulate the AND and the OR of the
+// children's one-hot sets plane by plane, each child expanded from 4 code planes with the
+// lo/hi decomposition of onehot_from_code (8 temporaries instead of a 16-plane set).
+struct LoHi {
+    uint32_t lo[4], hi[4];
+};
+
+__device__ __forceinline__ LoHi lohi_of(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t m) {
+    const uint32_t n0 = ~b0, n1 = ~b1, n2 = ~b2, n3 = ~b3;
+    return LoHi{{n0 & n1, b0 & n1, n0 & b1, b0 & b1}, {n2 & n3 & m, b2 & n3 & m, n2 & b3 & m, b2 & b3 & m}};
+}
+
+__device__ __forceinline__ void fold_set(uint32_t* both, uint32_t* either, const uint32_t* x, int v0, int nv) {
+    for (int v = v0; v < v0 + nv; ++v) {
+        both[v] &= x[v - v0];
+        either[v] |= x[v - v0];
+    }
+}
+
+// A leaf's word: code planes and present mask (absent: mask 0 = empty set).
+template <bool AP, class Args>
+__device__ __forceinline__ void leaf_word(const Args& a, int32_t leaf, int64_t word, uint4& L, uint32_t& m) {
+    if (!AP) {
+        const uint8_t flag = a.leaf_flag[leaf];
+        if (flag == kLeafAbsent) {
+            L = make_uint4(0, 0, 0, 0);
+            m = 0;
+            return;
+        }
+        L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+        m = flag == kLeafPartial ? a.leaf_present[(size_t)leaf * a.wpad + word] : ~0u;
+        return;
+    }
+    L = a.leaf_planes[(size_t)leaf * a.wpad + word];
+    m = ~0u;
+}
+
+// Fold child `c` (child_enc_v encoding) of a Fitch node into (both, either).
+template <bool AP>
+__device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int tile, int lane, int64_t word, uint32_t* both,
+                                           uint32_t* either) {
+    if (c < 0) {   // leaf (src/fitchSankoff.cpp:32-38, absent -> 0)
+        uint4 L;
+        uint32_t m;
+        leaf_word<AP>(a, -c - 1, word, L, m);
+        const LoHi t = lohi_of(L.x, L.y, L.z, L.w, m);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const uint32_t x = t.lo[v & 3] & t.hi[v >> 2];
+            both[v] &= x;
+            either[v] |= x;
+        }
+    } else if (c & kVirtualBit) {   // leaf-parent: the union of its leaves' codes
+        const int4 vl = a.vleaf[c & ~kVirtualBit];
+        const int32_t lv[4] = {__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
+                               __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w)};
+        uint4 L0, L1;
+        uint32_t m0, m1 = 0;
+        leaf_word<AP>(a, lv[0], word, L0, m0);
+        if (lv[1] >= 0) leaf_word<AP>(a, lv[1], word, L1, m1);
+        else L1 = make_uint4(0, 0, 0, 0);
+        if (lv[2] < 0) {   // one or two leaves (cherries): two lo/hi expansions
+            const LoHi t0 = lohi_of(L0.x, L0.y, L0.z, L0.w, m0), t1 = lohi_of(L1.x, L1.y, L1.z, L1.w, m1);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const uint32_t x = (t0.lo[v & 3] & t0.hi[v >> 2]) | (t1.lo[v & 3] & t1.hi[v >> 2]);
+                both[v] &= x;
+                either[v] |= x;
+            }
+        } else {           // three or four leaves: per-plane code matches
+            uint4 L2, L3 = make_uint4(0, 0, 0, 0);
+            uint32_t m2, m3 = 0;
+            leaf_word<AP>(a, lv[2], word, L2, m2);
+            if (lv[3] >= 0) leaf_word<AP>(a, lv[3], word, L3, m3);
+            const uint4 Ls[4] = {L0, L1, L2, L3};
+            const uint32_t ms[4] = {m0, m1, m2, m3};
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    x |= ms[i] & ((v & 1) ? Ls[i].x : ~Ls[i].x) & ((v & 2) ? Ls[i].y : ~Ls[i].y) &
+                         ((v & 4) ? Ls[i].z : ~Ls[i].z) & ((v & 8) ? Ls[i].w : ~Ls[i].w);
+                both[v] &= x;
+                either[v] |= x;
+            }
+        }
+    } else {       // materialised internal child: compressed record
+        const size_t rec = (size_t)c * a.tiles + tile;
+        const uint64_t mk = a.cmask[rec];
+        const uint4* p = a.sets + rec * kFitchRec;
+        if ((mk >> lane) & 1ull) {
+            const uint32_t k = lanes_below(mk);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 w = p[kWave + q * kWave + k];
+                const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    both[4 * q + j] &= x[j];
+                    either[4 * q + j] |= x[j];
+                }
+            }
+        } else {
+            const uint4 w = p[lane];
+            const LoHi t = lohi_of(w.x, w.y, w.z, w.w, ~0u);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const uint32_t x = t.lo[v & 3] & t.hi[v >> 2];
+                both[v] &= x;
+                either[v] |= x;
+            }
+        }
+    }
 }
 
 // Leaf child as a one-hot set: src/fitchSankoff.cpp:32-38 (absent leaf -> 0).
