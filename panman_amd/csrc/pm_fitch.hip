@@ -25,20 +25,25 @@ namespace {
 // back to back.
 template <bool AP>
 __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;
-    const int4 d = a.desc[item];
-    const int32_t n = __builtin_amdgcn_readfirstlane(d.x);
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(d.y);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(d.z);
+    const NodeDesc& d = a.desc[item];
+    const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
     uint32_t both[16], either[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    for (int32_t e = e0; e < e1; ++e) fold_child<AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), tile, lane, word, both, either);
+    fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either);
+    if (e1 - e0 > 1)
+        fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either);
+    for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
+        fold_child<AP>(a, c, vl, tile, lane, word, both, either);
+    }
     // AND if non-empty, else OR (src/fitchSankoff.cpp:48-55)
     const uint32_t nz = any_plane(both);
 #pragma unroll
@@ -105,8 +110,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     // Fitch (not block Fitch) may skip materialising leaf-parents
     const bool virt = !block && c->virtual_leaf_parents;
     const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
-    const int4* up_desc = reinterpret_cast<const int4*>(virt ? dt.up_desc_v : dt.up_desc);
-    const int4* down_desc = reinterpret_cast<const int4*>(virt ? dt.down_desc_v : dt.down_desc);
+    const NodeDesc* up_desc = virt ? dt.up_desc_v : dt.up_desc;
+    const NodeDesc* down_desc = virt ? dt.down_desc_v : dt.down_desc;
     const std::vector<int32_t>& up_off = virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
 

@@ -593,29 +593,30 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         strip(down_order_v, ht.down_level_off_v, false);
     }
 
-    auto make_desc = [&](const std::vector<int32_t>& order) {
-        std::vector<int32_t> desc(order.size() * 4);
+    auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
+        std::vector<NodeDesc> desc(order.size());
         for (size_t k = 0; k < order.size(); ++k) {
             const int32_t d = order[k];
-            desc[4 * k + 0] = d;
-            desc[4 * k + 1] = parent_dense[d];
-            desc[4 * k + 2] = ht.child_off[d];
-            desc[4 * k + 3] = ht.child_off[d + 1];
+            NodeDesc& x = desc[k];
+            x = NodeDesc{};
+            x.node = d;
+            x.parent = parent_dense[d];
+            x.e0 = ht.child_off[d];
+            x.e1 = ht.child_off[d + 1];
+            x.c0 = enc[x.e0];
+            x.c1 = x.e1 - x.e0 > 1 ? enc[x.e0 + 1] : 0;
+            for (int j = 0; j < 4; ++j) {
+                x.vl0[j] = x.c0 >= 0 && (x.c0 & kVirtualBit) ? vleaf[(size_t)(x.c0 & ~kVirtualBit) * 4 + j] : -1;
+                x.vl1[j] = x.e1 - x.e0 > 1 && x.c1 >= 0 && (x.c1 & kVirtualBit)
+                               ? vleaf[(size_t)(x.c1 & ~kVirtualBit) * 4 + j] : -1;
+            }
         }
         return desc;
     };
-    const std::vector<int32_t> down_desc = make_desc(down_order), down_desc_v = make_desc(down_order_v);
-    auto make_up_desc = [&](const std::vector<int32_t>& order) {
-        std::vector<int32_t> desc(order.size() * 4, 0);
-        for (size_t k = 0; k < order.size(); ++k) {
-            const int32_t d = order[k];
-            desc[4 * k + 0] = d;
-            desc[4 * k + 1] = ht.child_off[d];
-            desc[4 * k + 2] = ht.child_off[d + 1];
-        }
-        return desc;
-    };
-    const std::vector<int32_t> up_desc = make_up_desc(up_order), up_desc_v = make_up_desc(up_order_v);
+    const std::vector<NodeDesc> down_desc = make_desc(down_order, ht.child_enc);
+    const std::vector<NodeDesc> down_desc_v = make_desc(down_order_v, child_enc_v);
+    const std::vector<NodeDesc> up_desc = make_desc(up_order, ht.child_enc);
+    const std::vector<NodeDesc> up_desc_v = make_desc(up_order_v, child_enc_v);
 
     Regions rg;
     build_regions(bfs, off, idx, t->root, ht, rg);

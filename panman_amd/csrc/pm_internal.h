@@ -34,6 +34,15 @@ inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
 
+// Level item of the Fitch / Sankoff passes: everything a wave needs to start its loads,
+// in one 64-B scalar load (node, parent, child range, the first two children's encodings
+// and, for virtual leaf-parent children, their leaves).
+struct alignas(64) NodeDesc {
+    int32_t node, parent, e0, e1;
+    int32_t c0, c1, pad0, pad1;
+    int32_t vl0[4], vl1[4];
+};
+
 struct DevTree {
     int32_t num_internal = 0;
     int32_t num_leaves = 0;
@@ -54,10 +63,10 @@ struct DevTree {
     int32_t* down_order_v = nullptr;  // [I'] materialised internal nodes by depth
     // down-pass item descriptors {node, parent, first child, end child} (int4), in
     // down_order / down_order_v order, and each virtual node's leaves (int4, -1 padded)
-    int32_t* down_desc = nullptr;
-    int32_t* up_desc = nullptr;       // {node, first child, end child, 0} in up_order order
-    int32_t* up_desc_v = nullptr;
-    int32_t* down_desc_v = nullptr;
+    NodeDesc* down_desc = nullptr;
+    NodeDesc* up_desc = nullptr;      // in up_order order
+    NodeDesc* up_desc_v = nullptr;
+    NodeDesc* down_desc_v = nullptr;
     int32_t* vleaf = nullptr;
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
@@ -74,6 +83,7 @@ struct DevTree {
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
+
 constexpr int kRegionSlots = 3;   // internal nodes per region (LDS: 4 KiB each per wave)
 constexpr int kRegionStage = 4;   // staged leaves per region (LDS: 1 KiB + 256 B each)
 

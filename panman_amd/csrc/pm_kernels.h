@@ -14,7 +14,7 @@ enum class Mode { kFitch, kSankoff, kBlockFitch };
 
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
-    const int4* desc;      // Fitch: level items {node, first child, end child, -}
+    const NodeDesc* desc;  // Fitch: level items
     const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;
@@ -147,10 +147,10 @@ __device__ __forceinline__ void leaf_word(const Args& a, int32_t leaf, int64_t w
     m = ~0u;
 }
 
-// Fold child `c` (child_enc_v encoding) of a Fitch node into (both, either).
+// Fold child `c` (child_enc_v encoding; `vl` its leaves if virtual) into (both, either).
 template <bool AP>
-__device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int tile, int lane, int64_t word, uint32_t* both,
-                                           uint32_t* either) {
+__device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
+                                           uint32_t* both, uint32_t* either) {
     if (c < 0) {   // leaf (src/fitchSankoff.cpp:32-38, absent -> 0)
         uint4 L;
         uint32_t m;
@@ -163,7 +163,6 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int tile,
             either[v] |= x;
         }
     } else if (c & kVirtualBit) {   // leaf-parent: the union of its leaves' codes
-        const int4 vl = a.vleaf[c & ~kVirtualBit];
         const int32_t lv[4] = {__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                                __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w)};
         uint4 L0, L1;
@@ -269,7 +268,7 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 }
 
 struct DownArgs {
-    const int4* desc;      // per level item: {node, parent (dense, -1 root), first child, end child}
+    const NodeDesc* desc;  // per level item
     int32_t count;
     const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
     const int32_t* child_off;
@@ -430,12 +429,11 @@ struct Kid {
 };
 
 template <Mode M, bool AP>
-__device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int64_t word, Kid& k) {
+__device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 vl, int64_t word, Kid& k) {
     k.enc = enc;
     if (enc < 0) {
         leaf_fetch<AP>(a, -enc - 1, word, k.L0, k.m0);
     } else if (M == Mode::kFitch && (enc & kVirtualBit)) {
-        const int4 vl = a.vleaf[enc & ~kVirtualBit];
         k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                          __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
         leaf_fetch<AP>(a, k.vl.x, word, k.L0, k.m0);
@@ -512,7 +510,9 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
     if (e1 - e0 > 1) kid_records<M, AP>(a, sink, kids[1], word, valid, F);
     for (int32_t e = e0 + 2; e < e1; ++e) {
         Kid k;
-        kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e]), word, k);
+        const int32_t enc = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int4 vl = enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
+        kid_fetch<M, AP>(a, enc, vl, word, k);
         kid_records<M, AP>(a, sink, k, word, valid, F);
     }
 }
@@ -534,15 +534,12 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;   // whole wave leaves together
     if (lane == 0) stage_cnt[wave] = 0;
-    const int4 d = a.desc[item];
-    const int32_t n = __builtin_amdgcn_readfirstlane(d.x);
-    const int32_t parent = __builtin_amdgcn_readfirstlane(d.y);
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(d.z);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(d.w);
+    const NodeDesc& d = a.desc[item];
+    const int32_t n = d.node, parent = d.parent, e0 = d.e0, e1 = d.e1;
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
@@ -554,8 +551,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
     Kid kids[2];
-    kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0]), word, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M, AP>(a, __builtin_amdgcn_readfirstlane(a.child_enc[e0 + 1]), word, kids[1]);
+    kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
     if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
     else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
     uint32_t pres;

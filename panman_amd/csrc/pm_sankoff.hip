@@ -18,7 +18,7 @@ namespace {
 
 template <int B>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;
     const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
@@ -149,7 +149,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     const int D = (int)ht.down_level_off.size() - 1;
     for (int d = 0; d < D; ++d) {
-        dn.desc = reinterpret_cast<const int4*>(dt.down_desc) + ht.down_level_off[d];
+        dn.desc = dt.down_desc + ht.down_level_off[d];
         dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
