@@ -170,6 +170,11 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        # measured HBM bytes (PMC) per launch / launch time: the bandwidth actually drawn.
+        # `achieved` uses the SURVEY §8d state-through-memory byte model, which this layout
+        # beats (compressed set records, virtual leaf-parents), so frac can exceed 1.
+        "traffic_GBs": round(traffic / (dms / dl * 1e-3) / 1e9, 1) if traffic and dl and dms else None,
+        "traffic_frac": round(traffic / (dms / dl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic and dl and dms else None,
         "algorithmic_bytes_per_launch": per_launch,
         "avg_launch_ms": round(dms / dl, 4) if dl else None,
         "launches_per_step": dl,

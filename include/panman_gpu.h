@@ -226,6 +226,16 @@ int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, 
  * id (the reference's order is TBB-scheduled). */
 int pm_reroot(pm_ctx* ctx, const pm_panmat* tree, const char* leaf, pm_panman** out);
 
+/* Drop-in for Tree(pangraph.json, newick, FILE_TYPE::PANGRAPH, reference) (src/panman.cpp:
+ * 820-1273; CLI -P/-N, src/panmanUtils.cpp:1364-1407): the PanGraph model
+ * (src/panman.cpp:6200-6476), block order by chained alignment of the paths
+ * (src/chaining.cpp) and rotation of circular paths (src/rotation.cpp) on the host; block
+ * and nucleotide parsimony for every column on the GPU (Fitch, or Sankoff when the tree
+ * has a polytomy).  `json` and `newick` are file contents; `reference` may be NULL / "".
+ * Without a reference the main-column root forcing follows oneTBB's iteration order of
+ * the per-block sequences.  Result: a one-tree pm_panman. */
+int pm_pangraph_build(pm_ctx* ctx, const char* json, const char* newick, const char* reference, pm_panman** out);
+
 /* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
 /* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes
  * 2*leaves-1 nodes as CSR; leaves are ids [0, leaves), internal nodes follow. */

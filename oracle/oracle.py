@@ -36,6 +36,8 @@ def load() -> "Oracle":
             C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
         lib.oracle_fasta.restype = C.c_void_p
         lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
+        lib.oracle_pangraph.restype = C.c_void_p
+        lib.oracle_pangraph.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
         lib.oracle_reroot.restype = C.c_void_p
         lib.oracle_reroot.argtypes = [C.c_void_p, C.c_char_p]
         _lib = lib
@@ -71,6 +73,12 @@ class Oracle:
         del keep
         text = _take_string(self.lib, p)
         return (text, secs.value) if timed else text
+
+    def pangraph(self, flat: str, newick: str, reference: str = "", tbb_order: bool = True) -> str:
+        """Tree(PanGraph) dump (M3): blocks, then per node its block mutations and NucMuts.
+        tbb_order=False iterates individualSequences as a std::unordered_map instead."""
+        p = self.lib.oracle_pangraph(flat.encode(), newick.encode(), reference.encode(), int(tbb_order))
+        return _take_string(self.lib, p)
 
     def reroot(self, panmat, leaf: str) -> str:
         """Tree::reroot(leaf) dump: the new Newick, then per node (name order) its block

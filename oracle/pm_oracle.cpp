@@ -38,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <set>
@@ -1488,6 +1489,469 @@ char* oracle_reroot(const OraclePanmat* p, const char* leaf) {
     RTree t;
     build_rtree(p, t);
     return dup_string(reroot_dump(t, leaf));
+}
+
+// ------------------------------------------------------------- M3 PanGraph ----
+// Restatement of Tree(json, newick, FILE_TYPE::PANGRAPH, reference) (src/panman.cpp:820-1273)
+// with Pangraph (:6200-6476), chain_align (src/chaining.cpp) and rotate_sample
+// (src/rotation.cpp), on the reference's containers.  The PanGraph JSON arrives flattened
+// by the test (one record per line, see tests/_pangraph.py); oneTBB's concurrent map order
+// of individualSequences is restated as ascending bit-reversed tbb_hasher(name) | 1.
+namespace pgo {
+
+struct Range {
+    std::pair<int, int> point;
+    Range* left = nullptr;
+    Range* right = nullptr;
+};
+
+Range* range_tree(std::vector<std::pair<int, int>>& pts, int a, int b, std::vector<std::unique_ptr<Range>>& own) {
+    if (a > b) return nullptr;
+    std::sort(pts.begin() + a, pts.begin() + b + 1,
+              [](const std::pair<int, int>& x, const std::pair<int, int>& y) { return x.first < y.first; });
+    const int mid = (a + b) / 2;
+    own.push_back(std::make_unique<Range>());
+    Range* r = own.back().get();
+    r->point = pts[mid];
+    r->left = range_tree(pts, a, mid - 1, own);
+    r->right = range_tree(pts, mid + 1, b, own);
+    return r;
+}
+
+void query(Range* r, std::pair<int, int> lo, std::pair<int, int> hi, std::vector<std::pair<int, int>>& out) {
+    if (!r) return;
+    if (r->point.first >= lo.first && r->point.first <= hi.first && r->point.second >= lo.second &&
+        r->point.second <= hi.second)
+        out.push_back(r->point);
+    if (r->left && lo.first <= r->point.first) query(r->left, lo, hi, out);
+    if (r->right && hi.first >= r->point.first) query(r->right, lo, hi, out);
+}
+
+struct PairHash {
+    size_t operator()(const std::pair<int, int>& p) const {
+        const size_t a = std::hash<int>{}(p.first), b = std::hash<int>{}(p.second);
+        return a != b ? a ^ b : a;
+    }
+};
+
+std::vector<std::pair<int, int>> chaining(std::vector<std::string>& cons, std::vector<std::string>& sample) {
+    std::vector<std::pair<int, int>> chain, pts;
+    for (size_t i = 0; i < cons.size(); ++i)
+        for (size_t j = 0; j < sample.size(); ++j)
+            if (cons[i] == sample[j]) pts.emplace_back((int)i, (int)j);
+    std::sort(pts.begin(), pts.end());
+    std::vector<std::unique_ptr<Range>> own;
+    Range* root = range_tree(pts, 0, (int)pts.size() - 1, own);
+    if (pts.empty()) return chain;
+    std::unordered_map<std::pair<int, int>, std::pair<int, std::pair<int, int>>, PairHash> map;
+    const std::pair<int, int> origin(-1, -1);
+    for (auto p : pts) map[p] = {-1, origin};
+    const int K = 4000, match = 50;
+    for (auto point : pts) {
+        if (point.first == 0 && point.second == 0) { map[point] = {match, {-1, -1}}; continue; }
+        std::vector<std::pair<int, int>> res;
+        query(root, {point.first - K > 0 ? point.first - K : 0, point.second - K > 0 ? point.second - K : 0},
+              {point.first - 1, point.second - 1}, res);
+        int score = 10, xb = -1, yb = -1;
+        std::pair<int, int> node = origin;
+        for (auto it = res.rbegin(); it != res.rend(); ++it) {
+            auto p = *it;
+            if (p.first <= xb && p.second <= yb) continue;
+            const int cost = -(point.first - p.first + point.second - p.second);
+            if (cost + map[p].first + match > score) { score = cost + map[p].first + match; node = p; }
+            if (xb < p.first) xb = p.first - 1;
+            if (yb < p.second) yb = p.second - 1;
+        }
+        map[point] = {score, node};
+    }
+    int best = -1;
+    std::pair<int, int> seed{};
+    for (auto& m : map)
+        if (m.second.first > best) { best = m.second.first; seed = m.first; }
+    while (true) {
+        chain.push_back(seed);
+        seed = map[seed].second;
+        if (seed == origin) break;
+    }
+    return chain;
+}
+
+std::pair<int, int> rotate_alignment(const std::vector<std::string>& c, const std::vector<std::string>& s) {
+    std::vector<std::pair<int, int>> score(s.size(), {-1, -1}), next(s.size(), {-1, -1});
+    std::pair<int, int> mx(0, 0);
+    for (size_t i = 0; i < c.size(); ++i) {
+        for (size_t j = 0; j < s.size(); ++j) {
+            const size_t up = j == 0 ? s.size() - 1 : j - 1, diag = up, left = j;
+            int lv = score[left].first - 1, dv = score[diag].first, uv = j == 0 ? -1 : next[up].first - 1;
+            dv = c[i] == s[j] ? dv + 5 : dv - 2;
+            if (dv >= lv) {
+                if (dv >= uv) next[j] = {dv, score[diag].second == -1 ? (int)j : score[diag].second};
+                else next[j] = {uv, j == 0 ? -1 : next[up].second};
+            } else {
+                if (lv >= uv) next[j] = {lv, score[left].second};
+                else next[j] = {uv, j == 0 ? -1 : next[up].second};
+            }
+            if (next[j].first > mx.first) mx = next[j];
+        }
+        for (size_t z = 0; z < s.size(); ++z) score[z] = next[z];
+    }
+    return mx;
+}
+
+uint64_t tbb_key(const std::string& s) {
+    uint64_t h = 0;
+    for (char c : s) h = (uint64_t)(int64_t)c ^ (h * 0x9E3779B97F4A7C15ull);
+    uint64_t r = 0;
+    for (int b = 0; b < 64; ++b) r |= ((h >> b) & 1ull) << (63 - b);
+    return r | 1ull;
+}
+
+std::vector<std::string> split_tabs(const std::string& line) {
+    std::vector<std::string> f;
+    size_t a = 0;
+    for (size_t b; (b = line.find('\t', a)) != std::string::npos; a = b + 1) f.push_back(line.substr(a, b - a));
+    f.push_back(line.substr(a));
+    return f;
+}
+
+using Item = std::pair<char, std::vector<char>>;
+
+std::string build_dump(const std::string& flat, const std::string& newick, const std::string& reference, bool tbb_order) {
+    // --- Pangraph (:6200-6425) ---
+    std::unordered_map<std::string, std::vector<std::string>> paths;
+    std::unordered_map<std::string, std::vector<int>> strand_paths;
+    std::unordered_map<std::string, std::vector<size_t>> block_numbers, int_sequences;
+    std::unordered_map<std::string, int> circular, rotation;
+    std::unordered_map<std::string, bool> inverted;
+    std::unordered_map<std::string, std::string> consensus;
+    std::unordered_map<std::string, std::vector<std::pair<size_t, size_t>>> gaps;
+    std::unordered_map<std::string, std::unordered_map<std::string, std::unordered_map<size_t,
+        std::vector<std::pair<size_t, std::string>>>>> subs;
+    std::unordered_map<std::string, std::unordered_map<std::string, std::unordered_map<size_t,
+        std::vector<std::tuple<size_t, size_t, std::string>>>>> ins;
+    std::unordered_map<std::string, std::unordered_map<std::string, std::unordered_map<size_t,
+        std::vector<std::pair<size_t, size_t>>>>> dels;
+    bool circ = false;
+    std::istringstream in(flat);
+    std::string line;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        const auto f = split_tabs(line);
+        if (f[0] == "P") {
+            for (size_t k = 5; k < f.size(); ++k) {
+                const size_t colon = f[k].rfind(':');
+                paths[f[1]].push_back(f[k].substr(0, colon));
+                strand_paths[f[1]].push_back(f[k].substr(colon + 1) == "1");
+            }
+            if (f[2] == "1") { circ = true; circular[f[1]] = -std::stoi(f[3]); }
+        } else if (f[0] == "B") {
+            consensus[f[1]] = f[2];
+        } else if (f[0] == "G") {
+            gaps[f[1]].emplace_back((size_t)std::stol(f[2]), (size_t)std::stol(f[3]));
+        } else if (f[0] == "S") {
+            subs[f[1]][f[2]][(size_t)std::stol(f[3])].emplace_back((size_t)std::stol(f[4]), f[5]);
+        } else if (f[0] == "I") {
+            ins[f[1]][f[2]][(size_t)std::stol(f[3])].emplace_back((size_t)std::stol(f[4]), (size_t)std::stol(f[5]), f[6]);
+        } else if (f[0] == "D") {
+            dels[f[1]][f[2]][(size_t)std::stol(f[3])].emplace_back((size_t)std::stol(f[4]), (size_t)std::stol(f[5]));
+        }
+    }
+    if (circ) {
+        std::vector<std::string> base;
+        int count = 0;
+        for (auto& p : paths) {
+            std::unordered_map<std::string, size_t> bn;
+            for (auto& b : p.second) { block_numbers[p.first].push_back(bn[b] + 1); bn[b]++; }
+            if (count == 0) {
+                inverted[p.first] = false;
+                rotation[p.first] = 0;
+                base = p.second;
+            } else {
+                auto sample = p.second;
+                const int rot = rotate_alignment(base, sample).second;
+                std::vector<std::string> out;
+                std::vector<int> ns;
+                std::vector<size_t> nn;
+                auto& st = strand_paths[p.first];
+                auto& num = block_numbers[p.first];
+                for (size_t i = 0; i < sample.size(); ++i) {
+                    const size_t k = (i + rot) % sample.size();
+                    out.push_back(sample[k]);
+                    ns.push_back(st[k]);
+                    nn.push_back(num[k]);
+                }
+                st = ns;
+                num = nn;
+                inverted[p.first] = false;
+                rotation[p.first] = (int)((sample.size() - rot) % sample.size());
+                p.second = out;
+            }
+            ++count;
+        }
+    } else {
+        for (auto p : paths) {
+            std::unordered_map<std::string, size_t> bn;
+            inverted[p.first] = false;
+            rotation[p.first] = 0;
+            for (auto& b : p.second) { block_numbers[p.first].push_back(bn[b] + 1); bn[b]++; }
+        }
+    }
+    size_t num_nodes = 0;
+    std::unordered_map<int, std::string> int_to_string;
+    std::vector<std::string> cons;
+    std::vector<size_t> int_cons;
+    int count = 0;
+    for (auto& p : paths) {
+        if (count == 0) {
+            for (auto& b : p.second) {
+                cons.push_back(b);
+                int_to_string[(int)num_nodes] = b;
+                int_sequences[p.first].push_back(num_nodes);
+                int_cons.push_back(num_nodes);
+                ++num_nodes;
+            }
+        } else {
+            std::vector<std::string> sample = p.second, cons_new;
+            std::vector<size_t> int_sample, int_new;
+            auto chain = chaining(cons, sample);
+            int pc = -1, ps = -1;
+            for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+                for (int j = pc + 1; j < it->first; ++j) { cons_new.push_back(cons[j]); int_new.push_back(int_cons[j]); }
+                for (int j = ps + 1; j < it->second; ++j) {
+                    cons_new.push_back(sample[j]);
+                    int_sample.push_back(num_nodes);
+                    int_to_string[(int)num_nodes] = sample[j];
+                    int_new.push_back(num_nodes);
+                    ++num_nodes;
+                }
+                cons_new.push_back(cons[it->first]);
+                int_sample.push_back(int_cons[it->first]);
+                int_new.push_back(int_cons[it->first]);
+                pc = it->first;
+                ps = it->second;
+            }
+            for (int j = pc + 1; j < (int)cons.size(); ++j) { cons_new.push_back(cons[j]); int_new.push_back(int_cons[j]); }
+            for (int j = ps + 1; j < (int)sample.size(); ++j) {
+                cons_new.push_back(sample[j]);
+                int_sample.push_back(num_nodes);
+                int_to_string[(int)num_nodes] = sample[j];
+                int_new.push_back(num_nodes);
+                ++num_nodes;
+            }
+            for (auto b : int_sample) int_sequences[p.first].push_back(b);
+            cons = cons_new;
+            int_cons = int_new;
+        }
+        ++count;
+    }
+    std::unordered_map<int, int> order;
+    std::unordered_map<size_t, std::string> id_of;
+    std::vector<size_t> topo;
+    int reorder = 0;
+    for (auto i : int_cons) {
+        order[(int)i] = reorder;
+        id_of[reorder] = int_to_string[(int)i];
+        topo.push_back(reorder);
+        ++reorder;
+    }
+    for (auto& m : int_sequences)
+        for (auto& x : m.second) x = order[(int)x];
+
+    // --- driver (:820-1273) ---
+    OTree t;
+    std::string err;
+    if (!parse_newick(newick, t, err)) return "#error\t" + err + "\n";
+    std::function<bool(ONode*)> has_polytomy = [&](ONode* n) {
+        if (n->children.size() > 2) return true;
+        for (ONode* c : n->children)
+            if (has_polytomy(c)) return true;
+        return false;
+    };
+    const bool polytomy = has_polytomy(t.root);
+    std::unordered_map<std::string, std::vector<int>> aligned, aligned_strand;
+    for (auto p : int_sequences) {
+        size_t p1 = 0, p2 = 0;
+        while (p1 < topo.size() && p2 < p.second.size()) {
+            if (topo[p1] == p.second[p2]) { aligned[p.first].push_back((int)topo[p1]); ++p2; }
+            else aligned[p.first].push_back(-1);
+            ++p1;
+        }
+        while (aligned[p.first].size() < topo.size()) aligned[p.first].push_back(-1);
+    }
+    for (auto p : int_sequences) {
+        size_t p1 = 0, p2 = 0;
+        while (p1 < topo.size() && p2 < p.second.size()) {
+            if (topo[p1] == p.second[p2]) { aligned_strand[p.first].push_back(strand_paths[p.first][p2]); ++p2; }
+            else aligned_strand[p.first].push_back(-1);
+            ++p1;
+        }
+        while (aligned_strand[p.first].size() < topo.size()) aligned_strand[p.first].push_back(-1);
+    }
+    std::map<std::string, std::vector<RBlockMut>> block_muts;
+    for (size_t i = 0; i < topo.size(); ++i) {
+        if (!polytomy) {
+            StateMap st;
+            BlockMutMap muts;
+            int def = -1;
+            for (auto& u : aligned) {
+                if (reference.length() && u.first.find(reference) != std::string::npos)
+                    def = u.second[i] == -1 ? 1 : (aligned_strand[u.first][i] ? 2 : 4);
+                st[u.first] = u.second[i] == -1 ? 1 : (aligned_strand[u.first][i] ? 2 : 4);
+            }
+            block_fitch_up(t.root, st);
+            block_fitch_down(t.root, t.root, st, 1, def != -1 ? def : kNoDefault);
+            block_fitch_assign(t.root, st, muts, 1);
+            for (auto& m : muts) block_muts[m.first].push_back({(int32_t)i, -1, m.second.first == BI, m.second.second});
+        } else {
+            CostMap cs;
+            StateMap st;
+            BlockMutMap muts;
+            int def = -1;
+            for (auto& u : aligned) {
+                if (reference.length() && u.first.find(reference) != std::string::npos)
+                    def = u.second[i] == -1 ? 0 : (aligned_strand[u.first][i] ? 1 : 2);
+                std::vector<int> v(3, kSankoffInf);
+                v[u.second[i] == -1 ? 0 : (aligned_strand[u.first][i] ? 1 : 2)] = 0;
+                cs[u.first] = v;
+            }
+            block_sankoff_up(t.root, cs);
+            block_sankoff_down(t.root, t.root, cs, st, 0, def != -1 ? def : kNoDefault);
+            block_sankoff_assign(t.root, st, muts, 0);
+            for (auto& m : muts) block_muts[m.first].push_back({(int32_t)i, -1, m.second.first == BI, m.second.second});
+        }
+    }
+    std::unordered_map<std::string, std::vector<size_t>> block_counts;
+    for (auto& u : aligned) {
+        block_counts[u.first].resize(u.second.size(), 0);
+        int ptr = 0;
+        for (size_t i = 0; i < u.second.size(); ++i)
+            if (u.second[i] != -1) block_counts[u.first][i] = block_numbers[u.first][ptr++];
+    }
+    std::map<std::string, std::vector<std::tuple<int, int, int, int, int, int>>> non_gap, gap_m;
+    for (size_t i = 0; i < topo.size(); ++i) {
+        const std::string sid = id_of[topo[i]];
+        const std::string cseq = consensus[sid];
+        std::vector<Item> seq(cseq.size() + 1, {'-', {}});
+        for (size_t j = 0; j < cseq.size(); ++j) seq[j].first = cseq[j];
+        for (auto& g : gaps[sid]) seq[g.first].second.resize(g.second, '-');
+        std::vector<std::pair<std::string, std::vector<Item>>> indiv;   // iterated in TBB order below
+        for (auto& u : aligned) {
+            if (u.second[i] == -1) continue;
+            auto cur = seq;
+            const size_t num = block_counts[u.first][i];
+            for (auto& v : subs[sid][u.first][num]) cur[v.first - 1].first = v.second[0];
+            for (auto& v : ins[sid][u.first][num])
+                for (size_t j = 0; j < std::get<2>(v).size(); ++j) cur[std::get<0>(v)].second[std::get<1>(v) + j] = std::get<2>(v)[j];
+            for (auto& v : dels[sid][u.first][num])
+                for (size_t j = v.first; j < v.first + v.second; ++j) cur[j - 1].first = '-';
+            indiv.emplace_back(u.first, cur);
+        }
+        if (tbb_order) {
+            std::sort(indiv.begin(), indiv.end(), [](const auto& a, const auto& b) { return tbb_key(a.first) < tbb_key(b.first); });
+        } else {   // the survey's serial stand-in: a std::unordered_map filled in alignedSequences order
+            std::unordered_map<std::string, std::vector<Item>> m;
+            for (auto& u : indiv) m[u.first] = u.second;
+            indiv.assign(m.begin(), m.end());
+        }
+        auto state_of = [](char ch) { return ch != '-' ? 1 << code_of(ch) : 1; };
+        for (size_t j = 0; j < seq.size(); ++j) {
+            for (size_t k = 0; k < seq[j].second.size(); ++k) {
+                NucMutMap muts;
+                StateMap st;
+                if (!polytomy) {
+                    int def = -1;
+                    for (auto& u : indiv) {
+                        if (reference.length() && u.first.find(reference) != std::string::npos)
+                            def = state_of(u.second[j].second[k]);
+                        st[u.first] = state_of(u.second[j].second[k]);
+                    }
+                    fitch_up(t.root, st, -1);
+                    const int par = 1 << code_of(seq[j].second[k]);
+                    fitch_down(t.root, t.root, st, par, def != -1 ? def : kNoDefault);
+                    fitch_assign(t.root, st, muts, par);
+                } else {
+                    CostMap cs;
+                    int def = -1;
+                    for (auto& u : indiv) {
+                        const char ch = u.second[j].second[k];
+                        if (reference.length() && u.first.find(reference) != std::string::npos)
+                            def = ch != '-' ? code_of(ch) : 0;
+                        std::vector<int> v(16, kSankoffInf);
+                        v[ch != '-' ? code_of(ch) : 0] = 0;
+                        cs[u.first] = v;
+                    }
+                    sankoff_up(t.root, cs);
+                    sankoff_down(t.root, t.root, cs, st, code_of(seq[j].second[k]), def != -1 ? def : kNoDefault);
+                    sankoff_assign(t.root, st, muts, code_of(seq[j].second[k]));
+                }
+                for (auto& m : muts)
+                    gap_m[m.first].emplace_back((int)i, -1, (int)j, (int)k, m.second.first, code_of(m.second.second));
+            }
+            NucMutMap muts;
+            StateMap st;
+            if (!polytomy) {
+                int def = -1;
+                for (auto& u : indiv) {
+                    if (u.first.find(reference) != std::string::npos) def = state_of(u.second[j].first);   // unguarded
+                    st[u.first] = state_of(u.second[j].first);
+                }
+                fitch_up(t.root, st, -1);
+                const int par = 1 << code_of(seq[j].first);
+                fitch_down(t.root, t.root, st, par, def != -1 ? def : kNoDefault);
+                fitch_assign(t.root, st, muts, par);
+            } else {
+                CostMap cs;
+                int def = -1;
+                for (auto& u : indiv) {
+                    const char ch = u.second[j].first;
+                    if (reference.length() && u.first.find(reference) != std::string::npos)
+                        def = ch != '-' ? code_of(ch) : 0;
+                    std::vector<int> v(16, kSankoffInf);
+                    v[ch != '-' ? code_of(ch) : 0] = 0;
+                    cs[u.first] = v;
+                }
+                sankoff_up(t.root, cs);
+                sankoff_down(t.root, t.root, cs, st, code_of(seq[j].first), def != -1 ? def : kNoDefault);
+                sankoff_assign(t.root, st, muts, code_of(seq[j].first));
+            }
+            for (auto& m : muts)
+                non_gap[m.first].emplace_back((int)i, -1, (int)j, -1, m.second.first, code_of(m.second.second));
+        }
+    }
+    std::map<std::string, std::vector<RNucMut>> nuc;
+    for (auto& kv : non_gap) group6(kv.second, false, nuc[kv.first]);
+    for (auto& kv : gap_m) group6(kv.second, true, nuc[kv.first]);
+    // dump: blocks, then per node (name order) block and nucleotide mutations
+    std::string out;
+    char buf[200];
+    for (size_t i = 0; i < topo.size(); ++i) {
+        const std::string sid = id_of[topo[i]];
+        out += "block\t" + std::to_string(i) + "\t" + consensus[sid];
+        for (auto& g : gaps[sid]) out += "\t" + std::to_string(g.first) + ":" + std::to_string(g.second);
+        out += "\n";
+    }
+    for (auto& kv : t.all) {
+        auto bm = block_muts[kv.first];
+        std::sort(bm.begin(), bm.end(), [](const RBlockMut& a, const RBlockMut& b) { return a.primary < b.primary; });
+        for (auto& m : bm) {
+            std::snprintf(buf, sizeof buf, "\tB\t%d\t%d\t%d\n", m.primary, (int)m.info, (int)m.inversion);
+            out += kv.first + buf;
+        }
+        for (auto& m : nuc[kv.first]) {
+            std::snprintf(buf, sizeof buf, "\tN\t%d\t%d\t%d\t%u\t%06x\n", m.primary, m.pos, m.gap, (unsigned)m.info, m.nucs);
+            out += kv.first + buf;
+        }
+    }
+    return out;
+}
+
+}  // namespace pgo
+
+char* oracle_pangraph(const char* flat, const char* newick, const char* reference, int tbb_order) {
+    std::string nwk(newick);
+    const size_t nl = nwk.find('\n');
+    if (nl != std::string::npos) nwk.resize(nl);
+    return dup_string(pgo::build_dump(flat, nwk, reference ? reference : "", tbb_order != 0));
 }
 
 }  // extern "C"

@@ -71,6 +71,7 @@ _SIGS = {
     "pm_panman_free": (None, [C.c_void_p]),
     "pm_panman_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pm_reroot": (C.c_int, [C.c_void_p, C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "pm_pangraph_build": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 

@@ -1,0 +1,70 @@
+"""GPU PanGraph driver (M3): pm_pangraph_build vs the oracle restatement record for record on
+test/sars_20 (TBB-order contract), plus the end-to-end property that the built PanMAN
+replays every input genome (test/sars_20.fa) exactly."""
+import json
+import os
+
+import pytest
+
+import panman_amd
+from _pangraph import flatten, m3_dump
+from _panmat import parse_records
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = panman_amd.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def sars20():
+    text = open(os.path.join(GOLD, "sars_20.json")).read()
+    return text, json.loads(text), open(os.path.join(GOLD, "sars_20.nwk")).read()
+
+
+def test_sars20_matches_oracle(engine, oracle, sars20):
+    text, d, nwk = sars20
+    f = engine.pangraph_build(text, nwk)
+    try:
+        assert m3_dump(f) == oracle.pangraph(flatten(d), nwk)
+    finally:
+        f.close()
+
+
+def test_sars20_with_reference_matches_oracle(engine, oracle, sars20):
+    text, d, nwk = sars20
+    ref = d["paths"][3]["name"][:12]
+    f = engine.pangraph_build(text, nwk, ref)
+    try:
+        assert m3_dump(f) == oracle.pangraph(flatten(d), nwk, ref)
+    finally:
+        f.close()
+
+
+def test_sars20_replays_input_genomes(engine, sars20, tmp_path):
+    text, d, nwk = sars20
+    f = engine.pangraph_build(text, nwk)
+    path = str(tmp_path / "s.panman")
+    f.write(path)
+    f.close()
+    g = panman_amd.PanmanFile(path)
+    try:
+        got = parse_records(engine.fasta(g.view(0), False))
+    finally:
+        g.close()
+    want = {}
+    name = None
+    for line in open(os.path.join(GOLD, "sars_20.fa")):
+        line = line.strip()
+        if line.startswith(">"):
+            name = line[1:]
+            want[name] = ""
+        elif line:
+            want[name] += line.upper()
+    assert set(got) == set(want)
+    assert got == want
