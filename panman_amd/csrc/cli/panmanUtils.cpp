@@ -41,6 +41,7 @@ const Spec kSpecs[] = {
     {"help", 'h', false, "Print help messages"},
     {"input-panman", 'I', true, "Input PanMAN file path"},
     {"input-msa", 'M', true, "Input MSA file (FASTA format) to build a PanMAN"},
+    {"input-pangraph", 'P', true, "Input PanGraph JSON file to build a PanMAN"},
     {"input-newick", 'N', true, "Input tree topology as Newick string"},
     {"newick", 't', false, "Print newick string of all trees in a PanMAN"},
     {"fasta", 'f', false, "Print tip sequences (FASTA format)"},
@@ -55,7 +56,7 @@ const Spec kSpecs[] = {
 };
 
 // Reference commands outside the accelerated path: recognised so the error is explicit.
-const char* const kOther[] = {"input-pangraph", "input-gfa", "impute", "create-network", "printTips",
+const char* const kOther[] = {"input-gfa", "impute", "create-network", "printTips",
                               "summary", "subnet", "vcf", "gfa", "maf", "annotate",
                               "aa-translation", "extended-newick", "printMutations", "acr", "index",
                               "toUsher"};
@@ -245,6 +246,59 @@ int reroot(const Options& o, const pm_panman* file, int device) {
     return 0;
 }
 
+// -P pangraph.json -N tree.nwk -o out [-n ref] (src/panmanUtils.cpp:1364-1407)
+int build_from_pangraph(const Options& o, int device) {
+    if (!o.has("input-newick")) {
+        print_error("File containing newick string not provided!");
+        return 1;
+    }
+    if (!o.has("output-file")) {
+        print_error("Output file not provided!");
+        usage(std::cout);
+        return 1;
+    }
+    std::string json, newick;
+    if (!read_file(o.get("input-pangraph"), json)) {
+        print_error("cannot read " + o.get("input-pangraph"));
+        return 1;
+    }
+    if (!read_file(o.get("input-newick"), newick)) {
+        print_error("cannot read " + o.get("input-newick"));
+        return 1;
+    }
+    std::cout << "Creating PanMAN from PanGraph and Newick" << std::endl;
+    pm_ctx* ctx = nullptr;
+    if (pm_create(device, &ctx) != PM_OK) {
+        print_error("no HIP device");
+        return 1;
+    }
+    const auto t0 = Clock::now();
+    pm_panman* res = nullptr;
+    const std::string ref = o.has("reference") ? o.get("reference") : "";
+    if (pm_pangraph_build(ctx, json.c_str(), newick.c_str(), ref.c_str(), &res) != PM_OK) {
+        print_error(pm_last_error(ctx));
+        pm_destroy(ctx);
+        return 1;
+    }
+    std::cout << "Data load time: " << ns_since(t0) << " nanoseconds \n";
+    std::cout << "Writing PanMAN" << std::endl;
+    ::mkdir("./panman", 0777);
+    const std::string out = "./panman/" + o.get("output-file") + ".panman";
+    pm_panmat view;
+    pm_panman_tree(res, 0, &view);
+    const pm_panmat* list[1] = {&view};
+    const auto w0 = Clock::now();
+    const int rc = pm_panman_write(out.c_str(), list, 1, 1);
+    std::cout << "\nNetwork Write execution time: " << ns_since(w0) << " nanoseconds\n";
+    pm_panman_free(res);
+    pm_destroy(ctx);
+    if (rc != PM_OK) {
+        print_error("cannot write " + out);
+        return 1;
+    }
+    return 0;
+}
+
 int from_panman(const Options& o, int device) {
     const std::string path = o.get("input-panman");
     std::cout << "starting reading panman" << std::endl;
@@ -325,6 +379,7 @@ int main(int argc, char** argv) {
         return 0;
     }
     const int device = o.has("device") ? std::atoi(o.get("device").c_str()) : 0;
+    if (o.has("input-pangraph")) return build_from_pangraph(o, device);
     if (o.has("input-msa")) return build_from_msa(o, device);
     if (o.has("input-panman")) return from_panman(o, device);
     print_error("no input: give -I <file.panman> or -M <msa> -N <newick>");

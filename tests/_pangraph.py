@@ -62,3 +62,59 @@ def m3_dump(f, i: int = 0) -> str:
             out.append(f"{name}\tN\t{a['nuc_mut_primary'][k]}\t{a['nuc_mut_position'][k]}\t"
                        f"{a['nuc_mut_gap_position'][k]}\t{a['nuc_mut_info'][k]}\t{int(a['nuc_mut_nucs'][k]):06x}")
     return "\n".join(out) + "\n"
+
+
+def random_pangraph(rng, seqs=12, blocks=8, circular=False, dup_rate=0.15, flip_rate=0.1, drop_rate=0.15):
+    """A random, well-formed PanGraph JSON: blocks with gap slots, paths that drop, duplicate
+    and reverse blocks, and per-occurrence substitutions / insertions / deletions."""
+    import json as _json
+    bases = "ACGT"
+    ids = [f"B{k:03d}X" for k in range(blocks)]
+    seq = {b: "".join(rng.choice(list(bases), size=int(rng.integers(12, 60)))) for b in ids}
+    gaps = {}
+    for b in ids:
+        g = {}
+        for p in sorted(set(rng.integers(0, len(seq[b]) + 1, size=int(rng.integers(0, 4))).tolist())):
+            g[str(p)] = int(rng.integers(1, 6))
+        gaps[b] = g
+    names = [f"seq{k}|x/{k}" for k in range(seqs)]
+    paths = []
+    occ = {b: [] for b in ids}
+    for nm in names:
+        order = [b for b in ids if rng.random() > drop_rate] or [ids[0]]
+        if rng.random() < dup_rate:
+            order.insert(int(rng.integers(0, len(order) + 1)), order[int(rng.integers(0, len(order)))])
+        if circular:
+            r = int(rng.integers(0, len(order)))
+            order = order[r:] + order[:r]
+        pb, count = [], {}
+        for b in order:
+            count[b] = count.get(b, 0) + 1
+            strand = bool(rng.random() > flip_rate)
+            pb.append({"id": b, "name": nm, "number": count[b], "strand": strand})
+            occ[b].append((nm, count[b]))
+        paths.append({"name": nm, "offset": int(rng.integers(0, 9)) if circular else None, "circular": circular,
+                      "blocks": pb})
+    out_blocks = []
+    for b in ids:
+        L = len(seq[b])
+        mut, ins, dele = [], [], []
+        for nm, num in occ[b]:
+            who = {"name": nm, "number": num, "strand": True}
+            subs = [[int(p), str(rng.choice(list("ACGTN")))] for p in rng.integers(1, L + 1, size=int(rng.integers(0, 4)))]
+            mut.append([who, subs])
+            ii = []
+            for p, gl in gaps[b].items():
+                if rng.random() < 0.5:
+                    off = int(rng.integers(0, gl))
+                    n = int(rng.integers(1, gl - off + 1))
+                    ii.append([[int(p), off], "".join(rng.choice(list(bases), size=n)).lower()])
+            ins.append([who, ii])
+            dd = []
+            if rng.random() < 0.4:
+                p = int(rng.integers(1, L + 1))
+                dd.append([p, int(rng.integers(1, min(6, L + 2 - p) + 1))])
+            dele.append([who, dd])
+        out_blocks.append({"id": b, "sequence": seq[b].lower() if rng.random() < 0.3 else seq[b], "gaps": gaps[b],
+                           "mutate": mut, "insert": ins, "delete": dele})
+    return _json.dumps({"paths": paths, "blocks": out_blocks}), names

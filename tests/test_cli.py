@@ -130,3 +130,24 @@ def test_reroot_command_arguments(tmp_path):
     assert r.returncode != 0 and "TreeID not provided" in r.stderr
     r = _run(["-I", "in.panman", "--reroot", "-d", "0", "-o", "x"], tmp_path)
     assert r.returncode != 0 and "Refence ID not provided" in r.stderr
+
+
+@pytest.mark.gpu
+def test_pangraph_build_then_fasta(tmp_path):
+    """-P sars_20.json -N sars_20.nwk -o s, then -I ./panman/s.panman --fasta -o s replays
+    the input genomes."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    r = _run(["-P", os.path.join(gold, "sars_20.json"), "-N", os.path.join(gold, "sars_20.nwk"), "-o", "s"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    r = _run(["-I", "panman/s.panman", "-f", "-o", "s"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    got = parse_records(open(tmp_path / "info" / "s_0.fasta").read())
+    want, name = {}, None
+    for line in open(os.path.join(gold, "sars_20.fa")):
+        line = line.strip()
+        if line.startswith(">"):
+            name = line[1:]
+            want[name] = ""
+        elif line:
+            want[name] += line.upper()
+    assert got == want

@@ -68,3 +68,23 @@ def test_sars20_replays_input_genomes(engine, sars20, tmp_path):
             want[name] += line.upper()
     assert set(got) == set(want)
     assert got == want
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_pangraph_matches_oracle(engine, oracle, seed):
+    """Binary trees (Fitch) and polytomies (Sankoff), linear and circular paths, duplicated
+    and reversed blocks, with and without a reference name."""
+    import numpy as np
+    from _pangraph import random_pangraph
+    from _trees import random_tree, to_newick
+    rng = np.random.default_rng(100 + seed)
+    text, names = random_pangraph(rng, seqs=10 + seed, circular=seed % 4 >= 2)
+    off, idx, root = random_tree(len(names), rng, max_children=2 if seed % 2 == 0 else 4, unary=0.0)
+    nm = [names[i] if off[i] == off[i + 1] else "" for i in range(len(off) - 1)]
+    nwk = to_newick(off, idx, root, nm)
+    ref = names[seed % len(names)][:5] if seed % 3 == 0 else ""
+    f = engine.pangraph_build(text, nwk, ref)
+    try:
+        assert m3_dump(f) == oracle.pangraph(flatten(json.loads(text)), nwk, ref)
+    finally:
+        f.close()

@@ -35,3 +35,17 @@ def test_sars20_counts_std_order(oracle, sars20):
 def test_sars20_node_count(oracle, sars20):
     nwk = sars20[1]
     assert nwk.count("(") == 19 and nwk.count(",") == 19   # 20 leaves + 19 internal = 39 nodes
+
+
+def test_random_pangraphs_run_on_oracle(oracle):
+    """The synthetic generator produces inputs the restatement accepts (GPU parity uses them)."""
+    import numpy as np
+    from _pangraph import random_pangraph
+    from _trees import random_tree, to_newick
+    for seed in range(4):
+        rng = np.random.default_rng(seed)
+        text, names = random_pangraph(rng, circular=seed % 2 == 1)
+        off, idx, root = random_tree(len(names), rng, max_children=2 + seed % 2, unary=0.0)
+        nm = [names[i] if off[i] == off[i + 1] else "" for i in range(len(off) - 1)]
+        dump = oracle.pangraph(flatten(json.loads(text)), to_newick(off, idx, root, nm) + ";")
+        assert not dump.startswith("#error") and dump.count("block\t") >= 1
