@@ -14,7 +14,14 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
+
+
+def short(name):
+    """'void pm::k_down<(pm::Mode)0, true>(pm::DownArgs)' -> 'k_down' (the bench's key)."""
+    m = re.search(r"\b(k_\w+)", name)
+    return m.group(1) if m else name
 
 
 def per_kernel(d, counter):
@@ -23,7 +30,7 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            a = agg[r["Kernel_Name"]]
+            a = agg[short(r["Kernel_Name"])]
             a[0] += 1
             a[1] += float(r["Counter_Value"]) * 1024.0
     return agg
