@@ -127,7 +127,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
 int alloc_work(pm_ctx* c, int mode) {
     const int64_t wpad = wpad_of(c);
     const bool fitch = mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH;
-    const size_t planes = fitch ? 20 : 32;   // Fitch record: 5 uint4 per word slot (kFitchRec)
+    const size_t planes = fitch ? 20 : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
     const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * sizeof(uint64_t);
     const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
@@ -138,7 +138,7 @@ int alloc_work(pm_ctx* c, int mode) {
             return fail(c, PM_ERR_OOM, std::string("state sets: ") + hipGetErrorString(e));
         c->sets_bytes = need_sets;
     }
-    if (fitch && need_mask > c->cmask_bytes) {
+    if (need_mask > c->cmask_bytes) {
         dev_free(c->cmask);
         if ((e = hipMalloc(reinterpret_cast<void**>(&c->cmask), need_mask)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));

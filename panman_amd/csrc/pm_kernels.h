@@ -110,6 +110,68 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, in
     if (lane == 0) cmask[rec] = m;
 }
 
+// Sankoff records, compressed the same way: a word is simple when every site has a single
+// optimal code (Z0) and no code one above optimal (Z1 empty) -- for a binary node that is
+// "both children agree" -- and then Z0 is its code; other words keep Z0 and Z1 (8 quads)
+// packed by rank among the complex lanes.
+constexpr int kSankoffRec = 9 * kWave;   // uint4 per (node, tile)
+
+__device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* cmask, int64_t node, int32_t tiles,
+                                             int tile, int lane, uint32_t* z0, uint32_t* z1, bool want_z1) {
+    const size_t rec = (size_t)node * tiles + tile;
+    const uint64_t m = cmask[rec];
+    const uint4* p = sets + rec * kSankoffRec;
+    if ((m >> lane) & 1ull) {
+        const uint32_t k = lanes_below(m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[kWave + q * kWave + k];
+            z0[4 * q + 0] = v.x; z0[4 * q + 1] = v.y; z0[4 * q + 2] = v.z; z0[4 * q + 3] = v.w;
+        }
+        if (want_z1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = p[5 * kWave + q * kWave + k];
+                z1[4 * q + 0] = v.x; z1[4 * q + 1] = v.y; z1[4 * q + 2] = v.z; z1[4 * q + 3] = v.w;
+            }
+        }
+    } else {
+        const uint4 c = p[lane];
+        onehot_from_code(c.x, c.y, c.z, c.w, ~0u, z0);
+        if (want_z1) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) z1[v] = 0u;
+        }
+    }
+}
+
+__device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, int64_t node, int32_t tiles, int tile,
+                                              int lane, const uint32_t* z0, const uint32_t* z1) {
+    uint32_t one = 0, two = 0, any1 = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        two |= one & z0[v];
+        one |= z0[v];
+        any1 |= z1[v];
+    }
+    const bool complex_word = (one != ~0u) || two != 0u || any1 != 0u;
+    const uint64_t m = __ballot(complex_word);
+    const size_t rec = (size_t)node * tiles + tile;
+    uint4* p = sets + rec * kSankoffRec;
+    uint32_t c0, c1, c2, c3;
+    code_from_onehot(z0, c0, c1, c2, c3);
+    p[lane] = make_uint4(c0, c1, c2, c3);
+    if (complex_word) {
+        const uint32_t k = lanes_below(m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(z0[4 * q], z0[4 * q + 1], z0[4 * q + 2], z0[4 * q + 3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            p[5 * kWave + q * kWave + k] = make_uint4(z1[4 * q], z1[4 * q + 1], z1[4 * q + 2], z1[4 * q + 3]);
+    }
+    if (lane == 0) cmask[rec] = m;
+}
+
 // ---- Fitch post-order folding: (both, either) accumulate the AND and the OR of the
 // children's one-hot sets plane by plane, each child expanded from 4 code planes with the
 // lo/hi decomposition of onehot_from_code (8 temporaries instead of a 16-plane set).
@@ -531,7 +593,6 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
 // (3 spilled VGPRs) measured 2 % faster at N*.  The other modes keep their natural size.
 template <Mode M, bool AP>
 __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_down(DownArgs a) {
-    constexpr int Q = M == Mode::kSankoff ? 8 : 4;   // quads per state record
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -553,7 +614,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     Kid kids[2];
     kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
     if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
-    if constexpr (M == Mode::kSankoff) load_set16<Q>(a.sets, n, a.tiles, tile, lane, own);
+    uint32_t z1[16];
+    if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, n, a.tiles, tile, lane, own, z1, !is_root);
     else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
     uint32_t pres;
     if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
@@ -594,8 +656,7 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
                 lowest_code(own, fin);
             }
         } else {
-            uint32_t z1[16], cand[16], low[16];
-            load_set16<Q>(a.sets, n, a.tiles, tile, lane, z1, 4);
+            uint32_t cand[16], low[16];
             uint32_t hit = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -630,8 +691,12 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
     uint32_t base = 0;
+#ifdef PM_EXP_NOATOMIC
+    base = (uint32_t)((item * 64 + tile) % 1024) * 16;
+#else
     if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
     base = __shfl(base, 0, 64);
+#endif
     pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
     if (total <= kStage) {
         for (uint32_t i = lane; i < total; i += kWave)
