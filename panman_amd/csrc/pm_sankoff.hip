@@ -21,7 +21,8 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int32_t item = blockIdx.x * kWavesPerBlock + wave;
     if (item >= a.count) return;
-    const int32_t n = __builtin_amdgcn_readfirstlane(a.order[item]);
+    const NodeDesc& d = a.desc[item];
+    const int32_t n = d.node;
     const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
@@ -31,10 +32,9 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
 #pragma unroll
         for (int b = 0; b < B; ++b) cnt[v][b] = 0;
     uint32_t finite = 0, z[16];
-    const int32_t e0 = __builtin_amdgcn_readfirstlane(a.child_off[n]);
-    const int32_t e1 = __builtin_amdgcn_readfirstlane(a.child_off[n + 1]);
+    const int32_t e0 = d.e0, e1 = d.e1;
     for (int32_t e = e0; e < e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int32_t c = e == e0 ? d.c0 : (e == e0 + 1 ? d.c1 : __builtin_amdgcn_readfirstlane(a.child_enc[e]));
         if (c >= 0) load_sankoff(a.sets, a.cmask, c, a.tiles, tile, lane, z, nullptr, false);   // child's Z0
         else leaf_set16(a, -c - 1, word, z);                            // leaf: {code}, absent: INF
         finite |= any_plane(z);   // an all-INF child adds nothing (:398-400)
@@ -109,7 +109,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             const int32_t b = ht.up_class_off[h * kDegreeClasses + k];
             const int32_t e = ht.up_class_off[h * kDegreeClasses + k + 1];
             if (e == b) continue;
-            up.order = dt.up_order + b;
+            up.desc = dt.up_desc + b;
             up.count = e - b;
             dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
             timer_begin(c, 0);
