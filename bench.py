@@ -337,10 +337,10 @@ def replay_main(args):
         "config": {"workload": f"C5 replay: {leaves} leaves x {cols} aligned columns, "
                                f"{args.replay_blocks} blocks, {edits} edits",
                    "leaves": leaves, "columns": cols, "path_mutation_records": path_recs},
-        "roofline": {"bound": "hbm", "kernel": "k_replay_fill+k_replay_apply", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "algorithmic_bytes_per_launch": alg_bytes / 2,
-                     "avg_launch_ms": round(kms / 2, 4), "launches_per_step": launches[3] / args.steps},
+                     "traffic": None, "algorithmic_bytes_per_launch": alg_bytes,
+                     "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},
         "host_format_s": round(fmt_s, 3),
         "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
         "cpu_baseline": cpu, "parity_sample": parity,

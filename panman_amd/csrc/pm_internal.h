@@ -203,7 +203,13 @@ struct ReplayDev {
     const uint32_t* edit_col = nullptr;
     const uint8_t* edit_chr = nullptr;
     const int32_t* edit_blk = nullptr;
+    // column tiles of kReplayTile bytes: per node, the first edit of each tile
+    int32_t tiles = 0;
+    const int64_t* tile_edit = nullptr;   // [N][tiles + 1]
+    const int64_t* path_off = nullptr;    // [leaves + 1] root-to-leaf node lists
+    const int32_t* path = nullptr;
 };
+constexpr int64_t kReplayTile = 32768;   // leaf-row bytes assembled in LDS per workgroup
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d);
 // rows[leaf][c0 .. c0+n) chars -> packed codes out[leaf][(n+1)/2] ('-', 'x' -> 0)
 hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride, int32_t leaves, int64_t c0,

@@ -207,12 +207,16 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
     r.exists.assign(L, {});
     r.strand.assign(L, {});
     int32_t max_depth = 0;
+    std::vector<int64_t> path_off{0};
+    std::vector<int32_t> path_all;
     const int64_t nb_slots = (int64_t)B + 1;   // blockSequence has blocks.size()+1 entries
     for (int32_t li = 0; li < L; ++li) {
         std::vector<int32_t> path;
         for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path.push_back(n);
         std::reverse(path.begin(), path.end());
         max_depth = std::max(max_depth, (int32_t)path.size());
+        path_all.insert(path_all.end(), path.begin(), path.end());   // root first
+        path_off.push_back((int64_t)path_all.size());
         std::vector<uint8_t> pres(std::max<int64_t>(M, nb_slots), 0), ex(M, 0), st(M, 1);
         for (int32_t n : path)
             for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
@@ -246,8 +250,20 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
         if (p->sequence_inverted) r.inverted[li] = p->sequence_inverted[v];
     }
 
-    // ---- device
+    // ---- column tiles: per node, the first (column-sorted) edit of every tile
     const int64_t stride = (r.columns + 15) / 16 * 16;
+    const int32_t tiles = (int32_t)((stride + kReplayTile - 1) / kReplayTile);
+    std::vector<int64_t> tile_edit((size_t)N * (tiles + 1));
+    for (int32_t v = 0; v < N; ++v) {
+        int64_t e = eoff[v];
+        for (int32_t t = 0; t <= tiles; ++t) {
+            const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
+            while (e < eoff[v + 1] && (int64_t)ecol[e] < c0) ++e;
+            tile_edit[(size_t)v * (tiles + 1) + t] = e;
+        }
+    }
+
+    // ---- device
     std::vector<char> cons_row(stride, '-');
     std::memcpy(cons_row.data(), cons.data(), cons.size());
     hipError_t e;
@@ -257,6 +273,8 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
         (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, presence, c->stream)) != hipSuccess ||
         (e = dput(&r.d_eoff, eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, ecol, c->stream)) != hipSuccess ||
         (e = dput(&r.d_echr, echr, c->stream)) != hipSuccess || (e = dput(&r.d_eblk, eblk, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_tile_edit, tile_edit, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_path_off, path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, path_all, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
     ReplayDev& d = r.dev;
@@ -274,6 +292,10 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
     d.edit_col = r.d_ecol;
     d.edit_chr = r.d_echr;
     d.edit_blk = r.d_eblk;
+    d.tiles = tiles;
+    d.tile_edit = r.d_tile_edit;
+    d.path_off = r.d_path_off;
+    d.path = r.d_path;
     return PM_OK;
 }
 
@@ -357,6 +379,9 @@ void free_replay(pm_ctx* c) {
     dfree(r->d_ecol);
     dfree(r->d_echr);
     dfree(r->d_eblk);
+    dfree(r->d_tile_edit);
+    dfree(r->d_path_off);
+    dfree(r->d_path);
     delete r;
     c->replay = nullptr;
 }
@@ -382,7 +407,6 @@ int pm_replay_run(pm_ctx* c) {
     if (!c->replay) return fail(c, PM_ERR_STATE, "prepare a PanMAT first");
     (void)hipSetDevice(c->device);
     hipError_t e = launch_replay(c, c->replay->dev);
-    if (e == hipErrorNotSupported) return fail(c, PM_ERR_UNSUPPORTED, "tree deeper than 8192 nodes");
     if (e != hipSuccess) return hip_fail(c, e, "replay launch");
     c->replay->ran = true;
     return PM_OK;

@@ -43,6 +43,9 @@ struct ReplayState {
     uint32_t* d_ecol = nullptr;
     uint8_t* d_echr = nullptr;
     int32_t* d_eblk = nullptr;
+    int64_t* d_tile_edit = nullptr;
+    int64_t* d_path_off = nullptr;
+    int32_t* d_path = nullptr;
     bool ran = false;
 };
 

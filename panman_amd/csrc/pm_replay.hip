@@ -6,52 +6,88 @@
 // nucleotide mutations of each node on its root->leaf path in order, only for blocks that
 // are present at the leaf (blockSequence, :1766-1787, :1842).
 //
-//   k_replay_fill   rows[leaf][col] = consensus row; 16 B per lane, HBM-write bound
-//                   (1 B per leaf-column, the replay roofline of SURVEY.md §8d).
-//   k_replay_apply  one workgroup per leaf: the path (parent pointers) is staged in LDS,
-//                   then each path node's edits are written by all lanes, one barrier per
-//                   node so a descendant's write wins (edits of one node are unique per
-//                   column, resolved on the host in list order).
+//   k_replay_tile   one workgroup per (leaf, 32 KiB column tile): consensus tile -> LDS,
+//                   the path nodes' edits inside the tile applied root first (edits of one
+//                   node are unique per column and sorted by column on the host, so a
+//                   per-(node, tile) offset table bounds each node's slice), one coalesced
+//                   write of the tile: 1 B per leaf-column to HBM, the replay roofline of
+//                   SURVEY.md §8d.
 #include "pm_internal.h"
 
 namespace pm {
 namespace {
 
-__global__ __launch_bounds__(256) void k_replay_fill(char* rows, const char* cons_row, int64_t stride, int32_t leaves) {
-    const int64_t vec = stride / 16;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= vec * leaves) return;
-    const int64_t leaf = t / vec, k = t % vec;
-    reinterpret_cast<uint4*>(rows + leaf * stride)[k] = reinterpret_cast<const uint4*>(cons_row)[k];
-}
-
-constexpr int kMaxDepth = 8192;
-
-__global__ __launch_bounds__(256) void k_replay_apply(ReplayDev d) {
-    __shared__ int32_t path[kMaxDepth];
-    __shared__ int32_t depth;
+// One workgroup = (leaf, tile of kReplayTile columns): the tile of the leaf's row is
+// assembled in LDS -- consensus copy, then each path node's edits that fall in the tile,
+// root first, one barrier per node with edits (a descendant's write wins) -- and leaves as
+// one coalesced write.  Each row byte is written to HBM once.
+__global__ __launch_bounds__(256) void k_replay_tile(ReplayDev d) {
+    __shared__ uint4 tile_buf[kReplayTile / 16];
+    char* buf = reinterpret_cast<char*>(tile_buf);
     const int32_t leaf = blockIdx.x;
-    if (threadIdx.x == 0) {
-        int32_t n = d.leaf_node[leaf], k = 0;
-        while (n >= 0 && k < kMaxDepth) {
-            path[k++] = n;
-            n = d.parent[n];
-        }
-        depth = k;
-    }
+    const int32_t t = blockIdx.y;
+    const int64_t c0 = (int64_t)t * kReplayTile;
+    const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
+    const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
+    for (int64_t k = threadIdx.x; k < n / 16; k += blockDim.x) tile_buf[k] = src[k];
     __syncthreads();
     const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
-    char* row = d.rows + (size_t)leaf * d.row_stride;
-    for (int32_t k = depth - 1; k >= 0; --k) {   // root first
-        const int32_t n = path[k];
-        const int64_t e0 = d.edit_off[n], e1 = d.edit_off[n + 1];
-        if (e0 == e1) continue;   // uniform: no barrier needed
-        for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-            const int32_t b = d.edit_blk[e];
-            if ((pres[b >> 5] >> (b & 31)) & 1u) row[d.edit_col[e]] = (char)d.edit_chr[e];
+    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
+    // The path's edit slices for this tile, 256 nodes at a time: slice bounds and their
+    // prefix sums in LDS, then every thread loads its share of ALL the chunk's edits at
+    // once (one round of memory latency instead of one per node), then the edits are
+    // written node by node, root first, with a barrier between nodes.
+    constexpr int kPer = 8;   // edits per thread per round
+    __shared__ int64_t lo[256], pre[257];
+    for (int64_t q = p0; q < p1; q += 256) {
+        const int cnt = (int)min((int64_t)256, p1 - q);
+        if ((int)threadIdx.x < cnt) {
+            const int64_t* te = d.tile_edit + (size_t)d.path[q + threadIdx.x] * (d.tiles + 1) + t;
+            lo[threadIdx.x] = te[0];
+            pre[threadIdx.x + 1] = te[1] - te[0];
         }
+        if (threadIdx.x == 0) pre[0] = 0;
         __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 1; k <= cnt; ++k) pre[k] += pre[k - 1];
+        __syncthreads();
+        const int64_t total = pre[cnt];
+        for (int64_t base = 0; base < total; base += (int64_t)kPer * blockDim.x) {
+            int node[kPer];
+            uint32_t col[kPer];
+            char chr[kPer];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                node[j] = -1;
+                const int64_t g = base + threadIdx.x + (int64_t)j * blockDim.x;
+                if (g >= total) continue;
+                int lo_k = 0, hi_k = cnt - 1;   // last node with pre[k] <= g
+                while (lo_k < hi_k) {
+                    const int mid = (lo_k + hi_k + 1) >> 1;
+                    if (pre[mid] <= g) lo_k = mid;
+                    else hi_k = mid - 1;
+                }
+                const int64_t e = lo[lo_k] + (g - pre[lo_k]);
+                const int32_t b = d.edit_blk[e];
+                if ((pres[b >> 5] >> (b & 31)) & 1u) {
+                    node[j] = lo_k;
+                    col[j] = d.edit_col[e];
+                    chr[j] = (char)d.edit_chr[e];
+                }
+            }
+            const int64_t hi_g = min(total, base + (int64_t)kPer * blockDim.x);
+            for (int k = 0; k < cnt; ++k) {   // root first
+                if (pre[k + 1] <= base || pre[k] >= hi_g) continue;   // uniform: no edits this round
+#pragma unroll
+                for (int j = 0; j < kPer; ++j)
+                    if (node[j] == k) buf[col[j] - c0] = chr[j];
+                __syncthreads();
+            }
+        }
+        __syncthreads();   // lo / pre are reused by the next chunk
     }
+    uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
+    for (int64_t k = threadIdx.x; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
 }
 
 // getCodeFromNucleotide (src/panman.cpp:78-113) for the replayed characters; the reroot
@@ -92,12 +128,8 @@ hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride,
 
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;
-    if (d.max_depth > kMaxDepth) return hipErrorNotSupported;
-    const int64_t n = d.row_stride / 16 * d.leaves;
     timer_begin(c, 3);
-    hipLaunchKernelGGL(k_replay_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d.rows, d.cons_row,
-                       d.row_stride, d.leaves);
-    hipLaunchKernelGGL(k_replay_apply, dim3(d.leaves), dim3(256), 0, c->stream, d);
+    hipLaunchKernelGGL(k_replay_tile, dim3((unsigned)d.leaves, (unsigned)d.tiles), dim3(256), 0, c->stream, d);
     timer_end(c, 3);
     return hipGetLastError();
 }

@@ -195,7 +195,6 @@ int reroot(pm_ctx* c, const pm_panmat* p, const std::string& leaf_name, PanmanTr
         if (!r.is_block[id])
             return fail(c, PM_ERR_ARG, "Block with id " + std::to_string(id) + " -1 not found!");
     hipError_t e = launch_replay(c, r.dev);
-    if (e == hipErrorNotSupported) return fail(c, PM_ERR_UNSUPPORTED, "tree deeper than 8192 nodes");
     if (e != hipSuccess) return hip_fail(c, e, "replay launch");
     r.ran = true;
     std::vector<int32_t> li_of(N, -1);
