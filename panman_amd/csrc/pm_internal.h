@@ -210,6 +210,33 @@ struct ReplayDev {
     const int32_t* path = nullptr;
 };
 constexpr int64_t kReplayTile = 32768;   // leaf-row bytes assembled in LDS per workgroup
+
+// FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
+// segment per (leaf, print position) -- a block read forward or reverse-complemented from
+// the leaf's row, or a run of dashes for an absent block (aligned output).
+struct FmtSeg {
+    int64_t src;     // first row column of the block, -1 for a dash run
+    int64_t width;   // columns of the block, or the dash count
+    int32_t rev;     // reverse strand: read backwards, complemented
+    int32_t pad;
+};
+struct FmtArgs {
+    const char* rows;
+    int64_t row_stride;
+    int32_t positions;        // print positions per leaf
+    bool aligned;
+    const FmtSeg* seg;        // [leaves][positions]
+    int64_t* seg_len;         // [leaves][positions] chars each segment prints
+    const int64_t* seg_off;   // [leaves][positions] offset in the leaf's line
+    const int64_t* line_len;  // [leaves]
+    const int64_t* start;     // [leaves] rotation of the line (circular offset)
+    const int64_t* text_off;  // [leaves] byte offset of the leaf's record
+    const int64_t* name_off;  // [leaves + 1] into names
+    const char* names;
+    char* text;
+};
+hipError_t launch_fmt_count(pm_ctx* c, const FmtArgs& f, int32_t leaves);
+hipError_t launch_fmt_write(pm_ctx* c, const FmtArgs& f, int32_t leaves);
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d);
 // rows[leaf][c0 .. c0+n) chars -> packed codes out[leaf][(n+1)/2] ('-', 'x' -> 0)
 hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride, int32_t leaves, int64_t c0,

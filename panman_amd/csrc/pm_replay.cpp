@@ -30,16 +30,6 @@ char nuc_char(int code) {
     return tab[code & 15];
 }
 
-char complement(char c) {
-    switch (c) {
-        case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
-        case 'R': return 'Y'; case 'Y': return 'R'; case 'S': return 'S'; case 'W': return 'W';
-        case 'K': return 'M'; case 'M': return 'K'; case 'B': return 'V'; case 'D': return 'H';
-        case 'H': return 'D'; case 'V': return 'B';
-        default: return 'N';
-    }
-}
-
 template <class T>
 void dfree(T*& p) {
     if (p) (void)hipFree(p);
@@ -301,70 +291,6 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
 
 namespace {
 
-// printSequenceLinesNew for one leaf, from its replayed canonical row.
-void format_leaf(const ReplayState& r, int32_t li, const char* row, bool aligned, std::string& out) {
-    const int32_t M = r.max_id + 1;
-    std::vector<int32_t> order(M);
-    for (int32_t i = 0; i < M; ++i) order[i] = i;
-    const auto& ex = r.exists[li];
-    if (r.rotation[li] != 0) {   // rotate to the rotationIndexes-th existing block (:1950-1964)
-        int32_t ctr = -1, at = 0;
-        for (int32_t i = 0; i < M; ++i) {
-            if (ex[i]) ++ctr;
-            if (ctr == r.rotation[li]) { at = i; break; }
-        }
-        std::rotate(order.begin(), order.begin() + at, order.end());
-    }
-    if (r.inverted[li]) std::reverse(order.begin(), order.end());
-    std::string line;
-    for (int32_t i = 0; i < M; ++i) {
-        const int32_t id = order[i];
-        if (ex[id]) {
-            const char* seg = row + r.col_start[id];
-            const int64_t w = r.width[id];
-            if (r.strand[li][id]) {
-                for (int64_t k = 0; k < w; ++k) {
-                    const char ch = seg[k];
-                    if (ch == 'x') continue;
-                    if (ch != '-') line += ch;
-                    else if (aligned) line += '-';
-                }
-            } else {
-                for (int64_t k = w - 1; k >= 0; --k) {
-                    const char ch = seg[k];
-                    if (ch == 'x') continue;
-                    if (ch != '-') line += complement(ch);
-                    else if (aligned) line += '-';
-                }
-            }
-        } else if (aligned) {
-            // blockLengths is indexed by print position i, not by the block printed there
-            const int64_t dash = (r.is_block[i] && !r.present[li][i]) ? r.absent_len[i] : 0;
-            line.append((size_t)dash, '-');
-        }
-    }
-    size_t start = 0;
-    const int32_t offset = aligned ? 0 : std::max(0, r.circular[li]);
-    if (offset != 0) {
-        for (size_t i = 0; i < line.size(); ++i)
-            if (line[i] != '-') {
-                if (start == (size_t)offset) { start = i; break; }
-                ++start;
-            }
-    }
-    out += '>';
-    out += r.names[r.leaves[li]];
-    out += '\n';
-    size_t col = 0;
-    auto put = [&](char ch) {
-        out += ch;
-        if (++col == 70) { out += '\n'; col = 0; }
-    };
-    for (size_t i = start; i < line.size(); ++i) put(line[i]);
-    for (size_t i = 0; i < start; ++i) put(line[i]);
-    out += '\n';
-}
-
 }  // namespace
 
 void free_replay(pm_ctx* c) {
@@ -420,38 +346,127 @@ int pm_replay_shape(pm_ctx* c, int64_t* leaves, int64_t* columns, int64_t* edits
     return PM_OK;
 }
 
+// printFASTAUltraFast's output stage (src/fasta.cpp:1944-1975, 2089-2094) and
+// printSequenceLinesNew (:155-254) on the device: per leaf the blocks in print order
+// (rotation to the rotationIndexes-th existing block, reversal when inverted), forward or
+// reverse-complemented, '-' dropped when unaligned, absent blocks as blockLengths dashes
+// (indexed by print position, as the reference does), the line rotated by the circular
+// offset (unaligned only) and wrapped at 70 columns.  Host work: segment table, scans.
 int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     if (!c || !text || !length) return PM_ERR_ARG;
     if (!c->replay || !c->replay->ran) return fail(c, PM_ERR_STATE, "run the replay first");
     (void)hipSetDevice(c->device);
     const ReplayState& r = *c->replay;
     const int32_t L = (int32_t)r.leaves.size();
-    const int64_t stride = r.dev.row_stride;
-    std::vector<char> rows((size_t)L * stride);
-    hipError_t e = hipMemcpyAsync(rows.data(), r.d_rows, rows.size(), hipMemcpyDeviceToHost, c->stream);
+    const int32_t M = r.max_id + 1;
+    std::vector<FmtSeg> seg((size_t)L * M);
+    std::vector<int32_t> order(M);
+    for (int32_t li = 0; li < L; ++li) {
+        for (int32_t i = 0; i < M; ++i) order[i] = i;
+        const auto& ex = r.exists[li];
+        if (r.rotation[li] != 0) {   // rotate to the rotationIndexes-th existing block (:1950-1964)
+            int32_t ctr = -1, at = 0;
+            for (int32_t i = 0; i < M; ++i) {
+                if (ex[i]) ++ctr;
+                if (ctr == r.rotation[li]) { at = i; break; }
+            }
+            std::rotate(order.begin(), order.begin() + at, order.end());
+        }
+        if (r.inverted[li]) std::reverse(order.begin(), order.end());
+        for (int32_t i = 0; i < M; ++i) {
+            const int32_t id = order[i];
+            FmtSeg& sg = seg[(size_t)li * M + i];
+            if (ex[id]) {
+                sg = FmtSeg{r.col_start[id], r.width[id], r.strand[li][id] ? 0 : 1, 0};
+            } else {   // blockLengths is indexed by print position i, not by the block printed there
+                sg = FmtSeg{-1, (r.is_block[i] && !r.present[li][i]) ? r.absent_len[i] : 0, 0, 0};
+            }
+        }
+    }
+    std::vector<int64_t> name_off(L + 1, 0);
+    std::string names;
+    for (int32_t li = 0; li < L; ++li) {
+        names += r.names[r.leaves[li]];
+        name_off[li + 1] = (int64_t)names.size();
+    }
+    const size_t NS = (size_t)L * M;
+    FmtSeg* d_seg = nullptr;
+    int64_t *d_len = nullptr, *d_off = nullptr, *d_line = nullptr, *d_start = nullptr, *d_text_off = nullptr,
+            *d_name_off = nullptr;
+    char *d_names = nullptr, *d_text = nullptr;
+    auto cleanup = [&]() {
+        dfree(d_seg); dfree(d_len); dfree(d_off); dfree(d_line); dfree(d_start); dfree(d_text_off);
+        dfree(d_name_off); dfree(d_names); dfree(d_text);
+    };
+    hipError_t e = dput(&d_seg, seg, c->stream);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_len), sizeof(int64_t) * std::max<size_t>(NS, 1));
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(c, PM_ERR_OOM, "FASTA segments");
+    }
+    FmtArgs f{};
+    f.rows = r.d_rows;
+    f.row_stride = r.dev.row_stride;
+    f.positions = M;
+    f.aligned = aligned != 0;
+    f.seg = d_seg;
+    f.seg_len = d_len;
+    std::vector<int64_t> len(NS);
+    e = launch_fmt_count(c, f, L);
+    if (e == hipSuccess && NS) e = hipMemcpyAsync(len.data(), d_len, sizeof(int64_t) * NS, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) return hip_fail(c, e, "replay download");
-    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::string> parts(T);
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t)
-        pool.emplace_back([&, t] {
-            const int32_t a = (int32_t)((int64_t)L * t / T), b = (int32_t)((int64_t)L * (t + 1) / T);
-            for (int32_t li = a; li < b; ++li) format_leaf(r, li, rows.data() + (size_t)li * stride, aligned != 0, parts[t]);
-        });
-    for (auto& th : pool) th.join();
-    size_t total = 0;
-    for (auto& s : parts) total += s.size();
-    char* out = static_cast<char*>(std::malloc(total + 1));
-    if (!out) return fail(c, PM_ERR_OOM, "FASTA text");
-    size_t at = 0;
-    for (auto& s : parts) {
-        std::memcpy(out + at, s.data(), s.size());
-        at += s.size();
+    if (e != hipSuccess) {
+        cleanup();
+        return hip_fail(c, e, "FASTA segment count");
+    }
+    std::vector<int64_t> off(NS), line(L), start(L), text_off(L + 1, 0);
+    for (int32_t li = 0; li < L; ++li) {
+        int64_t p = 0;
+        for (int32_t i = 0; i < M; ++i) {
+            off[(size_t)li * M + i] = p;
+            p += len[(size_t)li * M + i];
+        }
+        line[li] = p;
+        // circular offset, unaligned only: the line holds no '-' then, so the offset-th
+        // character starts the record (or the line is printed as is when it is shorter)
+        const int64_t o = aligned ? 0 : std::max(0, r.circular[li]);
+        start[li] = o < p ? o : 0;
+        const int64_t hdr = name_off[li + 1] - name_off[li] + 2;
+        text_off[li + 1] = text_off[li] + hdr + p + p / 70 + 1;
+    }
+    const int64_t total = text_off[L];
+    char* out = static_cast<char*>(std::malloc((size_t)total + 1));
+    if (!out) {
+        cleanup();
+        return fail(c, PM_ERR_OOM, "FASTA text");
+    }
+    if ((e = dput(&d_off, off, c->stream)) != hipSuccess || (e = dput(&d_line, line, c->stream)) != hipSuccess ||
+        (e = dput(&d_start, start, c->stream)) != hipSuccess || (e = dput(&d_text_off, text_off, c->stream)) != hipSuccess ||
+        (e = dput(&d_name_off, name_off, c->stream)) != hipSuccess ||
+        (e = dput(&d_names, std::vector<char>(names.begin(), names.end()), c->stream)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&d_text), (size_t)std::max<int64_t>(total, 1))) != hipSuccess) {
+        std::free(out);
+        cleanup();
+        return fail(c, PM_ERR_OOM, "FASTA buffers");
+    }
+    f.seg_off = d_off;
+    f.line_len = d_line;
+    f.start = d_start;
+    f.text_off = d_text_off;
+    f.name_off = d_name_off;
+    f.names = d_names;
+    f.text = d_text;
+    e = launch_fmt_write(c, f, L);
+    if (e == hipSuccess && total) e = hipMemcpyAsync(out, d_text, (size_t)total, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    cleanup();
+    if (e != hipSuccess) {
+        std::free(out);
+        return hip_fail(c, e, "FASTA write");
     }
     out[total] = 0;
     *text = out;
-    *length = (int64_t)total;
+    *length = total;
     return PM_OK;
 }
 

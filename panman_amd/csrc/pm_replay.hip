@@ -115,6 +115,103 @@ __global__ __launch_bounds__(256) void k_rows_to_codes(const char* rows, int64_t
     out[leaf * out_stride + b] = (uint8_t)v;
 }
 
+__device__ __forceinline__ char complement_of(char c) {   // getComplementCharacter (src/panman.cpp:171-204)
+    switch (c) {
+        case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+        case 'R': return 'Y'; case 'Y': return 'R'; case 'S': return 'S'; case 'W': return 'W';
+        case 'K': return 'M'; case 'M': return 'K'; case 'B': return 'V'; case 'D': return 'H';
+        case 'H': return 'D'; case 'V': return 'B';
+        default: return 'N';
+    }
+}
+
+__device__ __forceinline__ bool fmt_keep(char ch, bool aligned) { return ch != 'x' && (aligned || ch != '-'); }
+
+// Block-wide sum / exclusive scan over 256 threads (4 waves).
+__device__ __forceinline__ int64_t block_sum(int64_t v, int64_t* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const int64_t t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+
+// chars each (leaf, print position) segment prints
+__global__ __launch_bounds__(256) void k_fmt_count(FmtArgs f) {
+    __shared__ int64_t red[4];
+    const int32_t leaf = blockIdx.y, pos = blockIdx.x;
+    const size_t k = (size_t)leaf * f.positions + pos;
+    const FmtSeg sg = f.seg[k];
+    if (sg.src < 0) {
+        if (threadIdx.x == 0) f.seg_len[k] = f.aligned ? sg.width : 0;
+        return;
+    }
+    const char* row = f.rows + (size_t)leaf * f.row_stride + sg.src;
+    int64_t n = 0;
+    for (int64_t j = threadIdx.x; j < sg.width; j += blockDim.x) n += fmt_keep(row[j], f.aligned);
+    n = block_sum(n, red);
+    if (threadIdx.x == 0) f.seg_len[k] = n;
+}
+
+// write every segment's chars at their wrapped, rotated place in the leaf's record
+__global__ __launch_bounds__(256) void k_fmt_write(FmtArgs f) {
+    __shared__ int64_t red[4];
+    __shared__ int64_t wsum[4];
+    const int32_t leaf = blockIdx.y, pos = blockIdx.x;
+    const size_t k = (size_t)leaf * f.positions + pos;
+    const FmtSeg sg = f.seg[k];
+    const int64_t L = f.line_len[leaf], st = f.start[leaf];
+    const int64_t n0 = f.name_off[leaf], n1 = f.name_off[leaf + 1];
+    char* rec = f.text + f.text_off[leaf];
+    const int64_t hdr = (n1 - n0) + 2;   // '>' name '\n'
+    if (pos == 0) {
+        if (threadIdx.x == 0) {
+            rec[0] = '>';
+            rec[hdr - 1] = '\n';
+            rec[hdr + L + L / 70] = '\n';   // the caller's final newline (src/fasta.cpp:2094)
+        }
+        for (int64_t j = threadIdx.x; j < n1 - n0; j += blockDim.x) rec[1 + j] = f.names[n0 + j];
+    }
+    auto place = [&](int64_t p, char ch) {
+        const int64_t q = L ? (p - st + L) % L : 0;
+        const int64_t o = hdr + q + q / 70;
+        rec[o] = ch;
+        if (q % 70 == 69) rec[o + 1] = '\n';
+    };
+    const int64_t base = f.seg_off[k];
+    if (sg.src < 0) {
+        if (!f.aligned) return;
+        for (int64_t j = threadIdx.x; j < sg.width; j += blockDim.x) place(base + j, '-');
+        return;
+    }
+    const char* row = f.rows + (size_t)leaf * f.row_stride + sg.src;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t done = 0;
+    for (int64_t j0 = 0; j0 < sg.width; j0 += blockDim.x) {
+        const int64_t j = j0 + threadIdx.x;
+        char ch = 0;
+        bool keep = false;
+        if (j < sg.width) {
+            ch = sg.rev ? row[sg.width - 1 - j] : row[j];
+            keep = fmt_keep(ch, f.aligned);
+            if (sg.rev && ch != '-') ch = complement_of(ch);
+        }
+        const uint64_t m = __ballot(keep);
+        const int64_t below = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __popcll(m);
+        __syncthreads();
+        int64_t before = 0;
+        for (int w = 0; w < wave; ++w) before += wsum[w];
+        const int64_t chunk = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (keep) place(base + done + before + below, ch);
+        done += chunk;
+        __syncthreads();
+    }
+    (void)red;
+}
+
 }  // namespace
 
 hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride, int32_t leaves, int64_t c0, int64_t n,
@@ -123,6 +220,18 @@ hipError_t launch_rows_to_codes(pm_ctx* c, const char* rows, int64_t row_stride,
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_rows_to_codes, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, rows, row_stride,
                        leaves, c0, n, out, out_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_fmt_count(pm_ctx* c, const FmtArgs& f, int32_t leaves) {
+    if (leaves == 0 || f.positions == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fmt_count, dim3((unsigned)f.positions, (unsigned)leaves), dim3(256), 0, c->stream, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_fmt_write(pm_ctx* c, const FmtArgs& f, int32_t leaves) {
+    if (leaves == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fmt_write, dim3((unsigned)std::max(f.positions, 1), (unsigned)leaves), dim3(256), 0, c->stream, f);
     return hipGetLastError();
 }
 
