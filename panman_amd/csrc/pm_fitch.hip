@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    store_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, both);
+    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
 #ifdef PM_EXP_COUNT_COMPLEX
     {
         uint32_t one = 0, two = 0;
@@ -124,6 +124,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.sets = reinterpret_cast<uint4*>(c->sets);
     up.cmask = c->cmask;
     up.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
+    up.cons = c->cons;
     up.forced = (c->has_forced && !block) ? c->forced : nullptr;   // refState (M1); blocks force in backward
     up.absent_code0 = false;
     up.root_dense = dt.root_dense;

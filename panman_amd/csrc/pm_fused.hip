@@ -122,7 +122,7 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             } else if (kind == 2) {
                 slot_load(val, lane, x);
             } else {
-                load_fitch_set(a.sets, a.cmask, val, a.tiles, tile, lane, x);
+                load_fitch_set(a.sets, a.cmask, a.cons, val, a.tiles, tile, lane, word, x);
             }
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] &= x[v]; either[v] |= x[v]; }
@@ -135,7 +135,7 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             const uint4 F = a.forced[word];
             onehot_from_code(F.x, F.y, F.z, F.w, ~0u, x);
         }
-        if (e == n1 - 1 && root_to_hbm) store_fitch_set(a.sets, a.cmask, dense, a.tiles, tile, lane, x);
+        if (e == n1 - 1 && root_to_hbm) store_fitch_set(a.sets, a.cmask, a.cons, dense, a.tiles, tile, lane, word, x);
         else slot_store(e - n0, lane, x);
     }
 }

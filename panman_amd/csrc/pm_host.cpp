@@ -129,7 +129,7 @@ int alloc_work(pm_ctx* c, int mode) {
     const bool fitch = mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH;
     const size_t planes = fitch ? 20 : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
-    const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * sizeof(uint64_t);
+    const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * 2 * sizeof(uint64_t);
     const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
     hipError_t e;
     if (need_sets > c->sets_bytes) {

@@ -23,7 +23,8 @@ struct UpArgs {
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
     uint4* sets;
-    uint64_t* cmask;       // Fitch record masks (see store_fitch_set)
+    uint64_t* cmask;       // record class masks, 2 per (node, tile) (see rec_store_head)
+    const uint4* cons;     // consensus codes (the "consensus" record class)
     const uint4* forced;   // nullable
     int32_t root_dense;
     int32_t tiles;
@@ -54,25 +55,56 @@ __device__ __forceinline__ void store_set16(uint4* sets, int64_t node, int32_t t
     for (int q = 0; q < 4; ++q) p[q * 64] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
 }
 
-// Fitch set records, compressed.  Per (node, 64-word tile): 64 entries of 4 code planes
-// (uint4 per lane, 1 KiB) for words whose 32 sets are all single codes -- the common case
-// -- and, for the other ("complex") words only, the 16 one-hot planes packed densely by
-// rank among the complex lanes (4 x 64 uint4 reserved, quad-major so each quad of the
-// complex lanes is one contiguous run).  A 64-bit mask per (node, tile) marks the complex
-// lanes.  Traffic per record: 1 KiB + 64 B per complex word instead of 4 KiB.
-constexpr int kFitchRec = 5 * kWave;   // uint4 per (node, tile)
+// Set records, compressed.  Per (node, 64-word tile) a word is one of three classes:
+//   consensus -- every site a single code equal to the block consensus: nothing stored;
+//   simple    -- every site a single code: 4 code planes (16 B), packed by rank among the
+//                simple lanes at the front of the record;
+//   complex   -- an empty or multi-code set somewhere: the full planes (Fitch: 16 one-hot
+//                planes; Sankoff: Z0 and Z1), packed by rank among the complex lanes,
+//                quad-major so each quad of the complex lanes is one contiguous run.
+// Two u64 ballots per (node, tile) mark the complex and simple lanes (mbcnt gives a lane
+// its rank).  Traffic per record: 16 B per simple and 64 / 128 B per complex word
+// instead of 64 / 128 B for every word.  (At N*, 93 % of Fitch words are single-code.)
+constexpr int kFitchRec = 5 * kWave;     // uint4 per (node, tile)
+constexpr int kSankoffRec = 9 * kWave;   // uint4 per (node, tile)
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t* cmask, int64_t node, int32_t tiles,
-                                               int tile, int lane, uint32_t* s) {
+struct RecMask {
+    uint64_t x, s;   // complex lanes, simple (non-consensus) lanes
+};
+
+__device__ __forceinline__ RecMask rec_mask(const uint64_t* cm, size_t rec) { return RecMask{cm[2 * rec], cm[2 * rec + 1]}; }
+
+// Code planes of a non-complex lane: stored (simple) or the consensus word.
+__device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
+    if ((m.s >> lane) & 1ull) return p[lanes_below(m.s)];
+    return cons[word];
+}
+
+// Classify a word from its single-code test and code planes, write code / masks.
+__device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t rec, int lane, bool complex_word,
+                                               const uint32_t* code, const uint4* cons, int64_t word, uint64_t& mx) {
+    const uint4 cw = cons[word];
+    const bool same = !complex_word && code[0] == cw.x && code[1] == cw.y && code[2] == cw.z && code[3] == cw.w;
+    mx = __ballot(complex_word);
+    const uint64_t ms = __ballot(!complex_word && !same);
+    if (!complex_word && !same) p[lanes_below(ms)] = make_uint4(code[0], code[1], code[2], code[3]);
+    if (lane == 0) {
+        cm[2 * rec] = mx;
+        cm[2 * rec + 1] = ms;
+    }
+}
+
+__device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t* cmask, const uint4* cons, int64_t node,
+                                               int32_t tiles, int tile, int lane, int64_t word, uint32_t* s) {
     const size_t rec = (size_t)node * tiles + tile;
-    const uint64_t m = cmask[rec];
+    const RecMask m = rec_mask(cmask, rec);
     const uint4* p = sets + rec * kFitchRec;
-    if ((m >> lane) & 1ull) {
-        const uint32_t k = lanes_below(m);
+    if ((m.x >> lane) & 1ull) {
+        const uint32_t k = lanes_below(m.x);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint4 v = p[kWave + q * kWave + k];
@@ -82,13 +114,13 @@ __device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t
             s[4 * q + 3] = v.w;
         }
     } else {
-        const uint4 c = p[lane];
+        const uint4 c = rec_code(p, m, lane, cons, word);
         onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
     }
 }
 
-__device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, int64_t node, int32_t tiles, int tile,
-                                                int lane, const uint32_t* s) {
+__device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
+                                                int32_t tiles, int tile, int lane, int64_t word, const uint32_t* s) {
     uint32_t one = 0, two = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -96,33 +128,29 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, in
         one |= s[v];
     }
     const bool complex_word = (one != ~0u) || two != 0u;   // an empty or multi-code set
-    const uint64_t m = __ballot(complex_word);
     const size_t rec = (size_t)node * tiles + tile;
     uint4* p = sets + rec * kFitchRec;
-    uint32_t c0, c1, c2, c3;
-    code_from_onehot(s, c0, c1, c2, c3);
-    p[lane] = make_uint4(c0, c1, c2, c3);   // every lane: whole lines written
+    uint32_t code[4];
+    code_from_onehot(s, code[0], code[1], code[2], code[3]);
+    uint64_t mx;
+    rec_store_head(p, cmask, rec, lane, complex_word, code, cons, word, mx);
     if (complex_word) {
-        const uint32_t k = lanes_below(m);
+        const uint32_t k = lanes_below(mx);
 #pragma unroll
         for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
     }
-    if (lane == 0) cmask[rec] = m;
 }
 
-// Sankoff records, compressed the same way: a word is simple when every site has a single
-// optimal code (Z0) and no code one above optimal (Z1 empty) -- for a binary node that is
-// "both children agree" -- and then Z0 is its code; other words keep Z0 and Z1 (8 quads)
-// packed by rank among the complex lanes.
-constexpr int kSankoffRec = 9 * kWave;   // uint4 per (node, tile)
-
-__device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* cmask, int64_t node, int32_t tiles,
-                                             int tile, int lane, uint32_t* z0, uint32_t* z1, bool want_z1) {
+// Sankoff: a word is single-code when every site has one optimal code (Z0) and no code
+// one above optimal (Z1 empty) -- for a binary node, "both children agree".
+__device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* cmask, const uint4* cons, int64_t node,
+                                             int32_t tiles, int tile, int lane, int64_t word, uint32_t* z0, uint32_t* z1,
+                                             bool want_z1) {
     const size_t rec = (size_t)node * tiles + tile;
-    const uint64_t m = cmask[rec];
+    const RecMask m = rec_mask(cmask, rec);
     const uint4* p = sets + rec * kSankoffRec;
-    if ((m >> lane) & 1ull) {
-        const uint32_t k = lanes_below(m);
+    if ((m.x >> lane) & 1ull) {
+        const uint32_t k = lanes_below(m.x);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint4 v = p[kWave + q * kWave + k];
@@ -136,7 +164,7 @@ __device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* 
             }
         }
     } else {
-        const uint4 c = p[lane];
+        const uint4 c = rec_code(p, m, lane, cons, word);
         onehot_from_code(c.x, c.y, c.z, c.w, ~0u, z0);
         if (want_z1) {
 #pragma unroll
@@ -145,8 +173,9 @@ __device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* 
     }
 }
 
-__device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, int64_t node, int32_t tiles, int tile,
-                                              int lane, const uint32_t* z0, const uint32_t* z1) {
+__device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
+                                              int32_t tiles, int tile, int lane, int64_t word, const uint32_t* z0,
+                                              const uint32_t* z1) {
     uint32_t one = 0, two = 0, any1 = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -155,21 +184,20 @@ __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, int6
         any1 |= z1[v];
     }
     const bool complex_word = (one != ~0u) || two != 0u || any1 != 0u;
-    const uint64_t m = __ballot(complex_word);
     const size_t rec = (size_t)node * tiles + tile;
     uint4* p = sets + rec * kSankoffRec;
-    uint32_t c0, c1, c2, c3;
-    code_from_onehot(z0, c0, c1, c2, c3);
-    p[lane] = make_uint4(c0, c1, c2, c3);
+    uint32_t code[4];
+    code_from_onehot(z0, code[0], code[1], code[2], code[3]);
+    uint64_t mx;
+    rec_store_head(p, cmask, rec, lane, complex_word, code, cons, word, mx);
     if (complex_word) {
-        const uint32_t k = lanes_below(m);
+        const uint32_t k = lanes_below(mx);
 #pragma unroll
         for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(z0[4 * q], z0[4 * q + 1], z0[4 * q + 2], z0[4 * q + 3]);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             p[5 * kWave + q * kWave + k] = make_uint4(z1[4 * q], z1[4 * q + 1], z1[4 * q + 2], z1[4 * q + 3]);
     }
-    if (lane == 0) cmask[rec] = m;
 }
 
 // ---- Fitch post-order folding: (both, either) accumulate the AND and the OR of the
@@ -260,10 +288,10 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
         }
     } else {       // materialised internal child: compressed record
         const size_t rec = (size_t)c * a.tiles + tile;
-        const uint64_t mk = a.cmask[rec];
+        const RecMask mk = rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * kFitchRec;
-        if ((mk >> lane) & 1ull) {
-            const uint32_t k = lanes_below(mk);
+        if ((mk.x >> lane) & 1ull) {
+            const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint4 w = p[kWave + q * kWave + k];
@@ -275,7 +303,7 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
                 }
             }
         } else {
-            const uint4 w = p[lane];
+            const uint4 w = rec_code(p, mk, lane, a.cons, word);
             const LoHi t = lohi_of(w.x, w.y, w.z, w.w, ~0u);
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -615,8 +643,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
     if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
     uint32_t z1[16];
-    if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, n, a.tiles, tile, lane, own, z1, !is_root);
-    else load_fitch_set(a.sets, a.cmask, n, a.tiles, tile, lane, own);
+    if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
+    else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
     uint32_t pres;
     if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
         // One sweep over the 16 planes from code 15 down to 0: "parent code in own set"

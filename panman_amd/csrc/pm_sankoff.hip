@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     const int32_t e0 = d.e0, e1 = d.e1;
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = e == e0 ? d.c0 : (e == e0 + 1 ? d.c1 : __builtin_amdgcn_readfirstlane(a.child_enc[e]));
-        if (c >= 0) load_sankoff(a.sets, a.cmask, c, a.tiles, tile, lane, z, nullptr, false);   // child's Z0
+        if (c >= 0) load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);   // child's Z0
         else leaf_set16(a, -c - 1, word, z);                            // leaf: {code}, absent: INF
         finite |= any_plane(z);   // an all-INF child adds nothing (:398-400)
 #pragma unroll
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
         z0[v] = cand[v] & finite;
         z1[v] = eq;
     }
-    store_sankoff(a.sets, a.cmask, n, a.tiles, tile, lane, z0, z1);
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1);
 }
 
 }  // namespace
@@ -99,6 +99,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.leaf_present = c->leaf_present;
     up.sets = reinterpret_cast<uint4*>(c->sets);
     up.cmask = c->cmask;
+    up.cons = c->cons;
     up.forced = nullptr;   // Sankoff forces the root in the backward pass only
     up.absent_code0 = block;
     up.root_dense = dt.root_dense;
