@@ -563,7 +563,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         for (int32_t d = 0; d < I; ++d) {
             if (ht.internal_id[d] == t->root) continue;
             const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
-            bool all_leaves = deg <= 4;
+            bool all_leaves = deg <= 2;   // one or two leaves: Fitch and Sankoff evaluate them inline
             for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1] && all_leaves; ++e) all_leaves = ht.child_enc[e] < 0;
             virt[d] = all_leaves;
             ht.num_virtual += all_leaves;
@@ -574,23 +574,28 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             if (virt[d])
                 for (int32_t e = ht.child_off[d], k = 0; e < ht.child_off[d + 1]; ++e, ++k)
                     vleaf[(size_t)d * 4 + k] = -ht.child_enc[e] - 1;
-        bucket(H, I, [&](int32_t d) { return virt[d] ? H - 1 : height[ht.internal_id[d]] - 1; }, ht.up_level_off_v,
-               up_order_v);
-        bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
-        // drop virtual nodes from the level lists (kept stable within levels)
-        auto strip = [&](std::vector<int32_t>& order, std::vector<int32_t>& offs, bool up) {
+        // levels keep their (height, degree class) buckets; virtual nodes are dropped
+        auto drop = [&](std::vector<int32_t>& order, std::vector<int32_t>& offs) {
             std::vector<int32_t> o2, f2{0};
             for (size_t k = 0; k + 1 < offs.size(); ++k) {
                 for (int32_t i = offs[k]; i < offs[k + 1]; ++i)
                     if (!virt[order[i]]) o2.push_back(order[i]);
-                if ((int32_t)o2.size() > f2.back()) f2.push_back((int32_t)o2.size());   // skip empty levels
-                (void)up;
+                f2.push_back((int32_t)o2.size());
             }
             order.swap(o2);
             offs.swap(f2);
         };
-        strip(up_order_v, ht.up_level_off_v, true);
-        strip(down_order_v, ht.down_level_off_v, false);
+        bucket(H * kDegreeClasses, I,
+               [&](int32_t d) {
+                   return (height[ht.internal_id[d]] - 1) * kDegreeClasses +
+                          degree_class(ht.child_off[d + 1] - ht.child_off[d]);
+               },
+               ht.up_class_off_v, up_order_v);
+        drop(up_order_v, ht.up_class_off_v);
+        ht.up_level_off_v.assign(H + 1, 0);
+        for (int32_t h = 0; h <= H; ++h) ht.up_level_off_v[h] = ht.up_class_off_v[h * kDegreeClasses];
+        bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
+        drop(down_order_v, ht.down_level_off_v);
     }
 
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {

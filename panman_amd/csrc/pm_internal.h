@@ -101,6 +101,7 @@ struct HostTree {
     std::vector<int32_t> child_off;       // dense CSR (host copy)
     std::vector<int32_t> child_enc;
     std::vector<int32_t> up_level_off_v;    // levels of up_order_v / down_order_v
+    std::vector<int32_t> up_class_off_v;    // [4H+1] (level, degree class) buckets of up_order_v
     std::vector<int32_t> down_level_off_v;
     int64_t num_virtual = 0;
     std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels

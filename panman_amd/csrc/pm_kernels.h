@@ -15,7 +15,7 @@ enum class Mode { kFitch, kSankoff, kBlockFitch };
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
     const NodeDesc* desc;  // Fitch: level items
-    const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
+    const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;
     const int32_t* child_enc;
@@ -252,39 +252,18 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
             both[v] &= x;
             either[v] |= x;
         }
-    } else if (c & kVirtualBit) {   // leaf-parent: the union of its leaves' codes
-        const int32_t lv[4] = {__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
-                               __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w)};
-        uint4 L0, L1;
+    } else if (c & kVirtualBit) {   // leaf-parent (one or two leaves): the union of their codes
+        const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
+        uint4 L0, L1 = make_uint4(0, 0, 0, 0);
         uint32_t m0, m1 = 0;
-        leaf_word<AP>(a, lv[0], word, L0, m0);
-        if (lv[1] >= 0) leaf_word<AP>(a, lv[1], word, L1, m1);
-        else L1 = make_uint4(0, 0, 0, 0);
-        if (lv[2] < 0) {   // one or two leaves (cherries): two lo/hi expansions
-            const LoHi t0 = lohi_of(L0.x, L0.y, L0.z, L0.w, m0), t1 = lohi_of(L1.x, L1.y, L1.z, L1.w, m1);
+        leaf_word<AP>(a, l0, word, L0, m0);
+        if (l1 >= 0) leaf_word<AP>(a, l1, word, L1, m1);
+        const LoHi t0 = lohi_of(L0.x, L0.y, L0.z, L0.w, m0), t1 = lohi_of(L1.x, L1.y, L1.z, L1.w, m1);
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const uint32_t x = (t0.lo[v & 3] & t0.hi[v >> 2]) | (t1.lo[v & 3] & t1.hi[v >> 2]);
-                both[v] &= x;
-                either[v] |= x;
-            }
-        } else {           // three or four leaves: per-plane code matches
-            uint4 L2, L3 = make_uint4(0, 0, 0, 0);
-            uint32_t m2, m3 = 0;
-            leaf_word<AP>(a, lv[2], word, L2, m2);
-            if (lv[3] >= 0) leaf_word<AP>(a, lv[3], word, L3, m3);
-            const uint4 Ls[4] = {L0, L1, L2, L3};
-            const uint32_t ms[4] = {m0, m1, m2, m3};
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    x |= ms[i] & ((v & 1) ? Ls[i].x : ~Ls[i].x) & ((v & 2) ? Ls[i].y : ~Ls[i].y) &
-                         ((v & 4) ? Ls[i].z : ~Ls[i].z) & ((v & 8) ? Ls[i].w : ~Ls[i].w);
-                both[v] &= x;
-                either[v] |= x;
-            }
+        for (int v = 0; v < 16; ++v) {
+            const uint32_t x = (t0.lo[v & 3] & t0.hi[v >> 2]) | (t1.lo[v & 3] & t1.hi[v >> 2]);
+            both[v] &= x;
+            either[v] |= x;
         }
     } else {       // materialised internal child: compressed record
         const size_t rec = (size_t)c * a.tiles + tile;
@@ -360,7 +339,7 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 struct DownArgs {
     const NodeDesc* desc;  // per level item
     int32_t count;
-    const int4* vleaf;     // virtual node -> its (up to 4) leaves, -1 padded
+    const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     const int32_t* child_off;
     const int32_t* child_enc;
     const int32_t* parent_dense;
@@ -523,7 +502,7 @@ __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 v
     k.enc = enc;
     if (enc < 0) {
         leaf_fetch<AP>(a, -enc - 1, word, k.L0, k.m0);
-    } else if (M == Mode::kFitch && (enc & kVirtualBit)) {
+    } else if (M != Mode::kBlockFitch && (enc & kVirtualBit)) {
         k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                          __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
         leaf_fetch<AP>(a, k.vl.x, word, k.L0, k.m0);
@@ -542,25 +521,30 @@ __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint
     have |= m;
 }
 
-// A virtual child (its leaves in k.vl, the first two prefetched) of a node with final codes
-// Fn: its final (parent if the parent's code is among its leaves', else the lowest of them
-// -- src/fitchSankoff.cpp:115-123 on the union set), its mutation and its leaves'.
-template <bool AP, class Sink>
+// A virtual child (one or two leaves, prefetched) of a node with final codes Fn: its
+// final, its mutation and its leaves'.
+//   Fitch   (src/fitchSankoff.cpp:115-123 on the union set): Fn if among the leaves'
+//           codes, else the lowest of them.
+//   Sankoff (:513-530): the optimal codes are the present leaves' codes; every other code
+//           is one above optimal unless both leaves are present with one code (then two
+//           above).  So Fn wins if among the leaves' codes, otherwise the lowest of them
+//           and -- when Fn is one above optimal -- Fn (ties go to the lowest index).
+template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
                                             uint32_t valid, const uint32_t* Fn) {
     const int32_t v = k.enc & ~kVirtualBit;
-    const int32_t more[2] = {k.vl.z, k.vl.w};
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
     virt_fold(k.L0, k.m0, Fn, low, have, hit);
     virt_fold(k.L1, k.m1, Fn, low, have, hit);
+    if (M == Mode::kSankoff) {
+        // Fn is one above optimal (in Z1) unless both leaves are present with equal codes
+        const uint32_t z1_has_fn =
+            (k.m0 ^ k.m1) |
+            (k.m0 & k.m1 & ((k.L0.x ^ k.L1.x) | (k.L0.y ^ k.L1.y) | (k.L0.z ^ k.L1.z) | (k.L0.w ^ k.L1.w)));
+        const uint32_t take = z1_has_fn & code_less(Fn, low);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-        if (more[j] >= 0) {
-            uint4 L;
-            uint32_t m;
-            leaf_fetch<AP>(a, more[j], word, L, m);
-            virt_fold(L, m, Fn, low, have, hit);
-        }
+        for (int j = 0; j < 4; ++j) low[j] = (Fn[j] & take) | (low[j] & ~take);
+    }
     uint32_t F[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
@@ -569,14 +553,6 @@ __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink,
     emit(sink, (uint32_t)a.leaf_id[k.vl.x], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
     if (k.vl.y >= 0)
         emit(sink, (uint32_t)a.leaf_id[k.vl.y], valid & k.m1 & diff4(k.L1, F), word, F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-        if (more[j] >= 0) {   // third / fourth leaf: second touch, cache hits
-            uint4 L;
-            uint32_t m;
-            leaf_fetch<AP>(a, more[j], word, L, m);
-            emit(sink, (uint32_t)a.leaf_id[more[j]], valid & m & diff4(L, F), word, F, L.x, L.y, L.z, L.w);
-        }
 }
 
 template <Mode M, bool AP, class Sink>
@@ -585,8 +561,8 @@ __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink,
     if (k.enc < 0)
         emit(sink, (uint32_t)a.leaf_id[-k.enc - 1], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z,
              k.L0.w);
-    else if (M == Mode::kFitch && (k.enc & kVirtualBit))
-        virtual_kid<AP>(a, sink, k, word, valid, F);
+    else if (M != Mode::kBlockFitch && (k.enc & kVirtualBit))
+        virtual_kid<M, AP>(a, sink, k, word, valid, F);
 }
 
 // Every record of node n's wave: the node itself and its children (the first two from

@@ -35,8 +35,22 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     const int32_t e0 = d.e0, e1 = d.e1;
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t c = e == e0 ? d.c0 : (e == e0 + 1 ? d.c1 : __builtin_amdgcn_readfirstlane(a.child_enc[e]));
-        if (c >= 0) load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);   // child's Z0
-        else leaf_set16(a, -c - 1, word, z);                            // leaf: {code}, absent: INF
+        if (c >= 0 && (c & kVirtualBit)) {   // one or two leaves: Z0 = their codes (:376-402)
+            const int4 vl = e == e0 ? make_int4(d.vl0[0], d.vl0[1], -1, -1)
+                                    : (e == e0 + 1 ? make_int4(d.vl1[0], d.vl1[1], -1, -1) : a.vleaf[c & ~kVirtualBit]);
+            const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
+            uint32_t x[16];
+            leaf_set16(a, l0, word, z);
+            if (l1 >= 0) {
+                leaf_set16(a, l1, word, x);
+#pragma unroll
+                for (int v = 0; v < 16; ++v) z[v] |= x[v];
+            }
+        } else if (c >= 0) {
+            load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);   // child's Z0
+        } else {
+            leaf_set16(a, -c - 1, word, z);   // leaf: {code}, absent: INF
+        }
         finite |= any_plane(z);   // an all-INF child adds nothing (:398-400)
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
@@ -91,9 +105,17 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const int H = (int)ht.up_level_off.size() - 1;
     if (c->max_degree > 4095) return hipErrorNotSupported;   // 12-bit counters cover 4095 children
 
+    // nucleotide Sankoff evaluates leaf-parents of one or two leaves inline, like Fitch
+    const bool virt = !block && c->virtual_leaf_parents;
+    const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
+    const NodeDesc* up_desc = virt ? dt.up_desc_v : dt.up_desc;
+    const NodeDesc* down_desc = virt ? dt.down_desc_v : dt.down_desc;
+    const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
+    const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
     UpArgs up{};
     up.child_off = dt.child_off;
-    up.child_enc = dt.child_enc;
+    up.child_enc = child_enc;
+    up.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     up.leaf_flag = c->leaf_flag;
     up.leaf_planes = c->leaf_planes;
     up.leaf_present = c->leaf_present;
@@ -107,10 +129,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.wpad = wpad;
     for (int h = 0; h < H; ++h) {
         for (int k = 0; k < kDegreeClasses; ++k) {
-            const int32_t b = ht.up_class_off[h * kDegreeClasses + k];
-            const int32_t e = ht.up_class_off[h * kDegreeClasses + k + 1];
+            const int32_t b = class_off[h * kDegreeClasses + k];
+            const int32_t e = class_off[h * kDegreeClasses + k + 1];
             if (e == b) continue;
-            up.desc = dt.up_desc + b;
+            up.desc = up_desc + b;
             up.count = e - b;
             dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
             timer_begin(c, 0);
@@ -126,7 +148,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     if (err != hipSuccess) return err;
     DownArgs dn{};
     dn.child_off = dt.child_off;
-    dn.child_enc = dt.child_enc;
+    dn.child_enc = child_enc;
     dn.parent_dense = dt.parent_dense;
     dn.internal_id = dt.internal_id;
     dn.leaf_id = dt.leaf_id;
@@ -149,10 +171,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.forced = c->has_forced ? c->forced : nullptr;
     dn.absent_code0 = block;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
-    const int D = (int)ht.down_level_off.size() - 1;
+    const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
-        dn.desc = dt.down_desc + ht.down_level_off[d];
-        dn.count = ht.down_level_off[d + 1] - ht.down_level_off[d];
+        dn.desc = down_desc + down_off[d];
+        dn.count = down_off[d + 1] - down_off[d];
+        if (dn.count == 0) continue;
         dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
         timer_begin(c, 1);
         if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
