@@ -70,7 +70,7 @@ def test_sars20_replays_input_genomes(engine, sars20, tmp_path):
     assert got == want
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(16))
 def test_random_pangraph_matches_oracle(engine, oracle, seed):
     """Binary trees (Fitch) and polytomies (Sankoff), linear and circular paths, duplicated
     and reversed blocks, with and without a reference name."""
