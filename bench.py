@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each step's launch sequence from a hipGraph (PM_OPT_GRAPH); "
+                        "per-kernel times then come from an extra untimed eager pass")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--replay-leaves", type=int, default=1000)
     p.add_argument("--replay-blocks", type=int, default=500)
@@ -103,7 +106,10 @@ def main():
     muts = eng.mutation_count()   # sizes the record buffers (re-runs once if a shard overflowed)
     torch.cuda.synchronize()
 
-    eng.set_profiling(True)
+    if args.graph:
+        eng.set_graph(True)
+        step()   # capture outside the timed region
+    eng.set_profiling(not args.graph)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -114,6 +120,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    if args.graph:   # per-kernel durations for the roofline: same steps, eager, untimed
+        eng.set_graph(False)
+        eng.set_profiling(True)
+        for _ in range(args.steps):
+            eng.run(mode)
+        torch.cuda.synchronize()
     ms, launches = eng.kernel_times(3)
     eng.set_profiling(False)
     if world > 1:
@@ -211,6 +223,7 @@ def main():
                 "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
                 "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
                 "mutations_total": muts_total,
+                "launch": "hipGraph replay" if args.graph else "eager per-level launches",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -85,10 +85,15 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 /* Options (results are identical either way):
  *   PM_OPT_FUSED   (default 0): Fitch on subtree regions with intermediate sets in LDS
  *                  (experimental; slower than the level kernels on MI355X so far).
- *   PM_OPT_VIRTUAL (default 1): Fitch level kernels evaluate internal nodes whose children
- *                  are all leaves inline in their parent instead of materialising them. */
+ *   PM_OPT_VIRTUAL (default 1): the level kernels evaluate internal nodes whose children
+ *                  are one or two leaves inline in their parent instead of materialising them.
+ *   PM_OPT_GRAPH   (default 0): pm_run captures its launch sequence (per-level kernels,
+ *                  memsets) into a hipGraph once and replays it while the tree, columns,
+ *                  mode and buffers stay the same; kernel_times then reports the whole run
+ *                  as class 4. */
 #define PM_OPT_FUSED 1
 #define PM_OPT_VIRTUAL 2
+#define PM_OPT_GRAPH 3
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);
@@ -129,7 +134,8 @@ int pm_site_results(pm_ctx* ctx, int32_t* score, uint8_t* root_code);
  * collective can gather them without a host round trip. */
 int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_device);
 /* Accumulated device milliseconds and launch counts per kernel class since the last
- * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram, 3 replay. */
+ * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram, 3 replay,
+ * 4 whole pm_run replayed from a hipGraph (PM_OPT_GRAPH). */
 int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
 
 /* ---- column drivers ------------------------------------------------------------------ */

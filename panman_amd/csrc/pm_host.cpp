@@ -78,7 +78,14 @@ void free_tree(DevTree& t) {
     t = DevTree{};
 }
 
+void drop_graph(pm_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    c->graph_exec = nullptr;
+    c->graph_key = 0;
+}
+
 void free_columns(pm_ctx* c) {
+    drop_graph(c);
     dev_free(c->leaf_planes);
     dev_free(c->leaf_present);
     dev_free(c->leaf_flag);
@@ -91,6 +98,7 @@ void free_columns(pm_ctx* c) {
 }
 
 void free_work(pm_ctx* c) {
+    drop_graph(c);
     dev_free(c->sets);
     dev_free(c->cmask);
     dev_free(c->finals);
@@ -163,16 +171,66 @@ int alloc_work(pm_ctx* c, int mode) {
     return PM_OK;
 }
 
-int run_once(pm_ctx* c, int mode) {
+hipError_t launch_all(pm_ctx* c, int mode) {
     const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
     const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
-    if (sankoff && c->max_degree > 4095)
-        return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
     hipError_t e = sankoff ? launch_sankoff(c, block)
                            : (mode == PM_MODE_FITCH && c->fused) ? launch_fitch_fused(c) : launch_fitch(c, block);
-    if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
-    e = launch_score(c);
-    if (e != hipSuccess) return hip_fail(c, e, "score launch");
+    if (e == hipSuccess) e = launch_score(c);
+    return e;
+}
+
+// Everything a captured run depends on: a different value means a different graph.
+uint64_t graph_key_of(const pm_ctx* c, int mode) {
+    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents,
+                              (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
+                              (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
+                              (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals,
+                              (uint64_t)(uintptr_t)c->leaf_planes, (uint64_t)(uintptr_t)c->leaf_present,
+                              (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
+                              (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
+                              (uint64_t)(uintptr_t)c->root_code, (uint64_t)(uintptr_t)c->shard_cnt,
+                              (uint64_t)(uintptr_t)c->dt.child_off, (uint64_t)(uintptr_t)c->stream};
+    uint64_t h = 1469598103934665603ull;
+    for (uint64_t v : parts) h = (h ^ v) * 1099511628211ull;
+    return h | 1;
+}
+
+int run_once(pm_ctx* c, int mode) {
+    const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
+    if (sankoff && c->max_degree > 4095)
+        return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
+    hipError_t e;
+    if (!c->use_graph) {
+        e = launch_all(c, mode);
+        if (e != hipSuccess) return hip_fail(c, e, "parsimony launch");
+    } else {
+        const uint64_t key = graph_key_of(c, mode);
+        if (key != c->graph_key) {
+            drop_graph(c);
+            const bool prof = c->profiling;
+            c->profiling = false;   // per-kernel events are not part of the graph
+            hipGraph_t g = nullptr;
+            e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                const hipError_t le = launch_all(c, mode);
+                e = hipStreamEndCapture(c->stream, &g);
+                if (e == hipSuccess) e = le;
+            }
+            c->profiling = prof;
+            if (e == hipSuccess) e = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+            if (e != hipSuccess) {
+                drop_graph(c);
+                return hip_fail(c, e, "graph capture");
+            }
+            c->graph_key = key;
+        }
+        timer_begin(c, 4);
+        e = hipGraphLaunch(c->graph_exec, c->stream);
+        timer_end(c, 4);
+        if (e != hipSuccess) return hip_fail(c, e, "graph launch");
+    }
     c->ran = true;
     c->last_mode = mode;
     return PM_OK;
@@ -446,6 +504,11 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     }
     if (option == PM_OPT_VIRTUAL) {
         c->virtual_leaf_parents = value != 0;
+        return PM_OK;
+    }
+    if (option == PM_OPT_GRAPH) {
+        c->use_graph = value != 0;
+        if (!c->use_graph) drop_graph(c);
         return PM_OK;
     }
     return fail(c, PM_ERR_ARG, "unknown option");

@@ -28,7 +28,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
-constexpr int kClasses = 4;
+constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
@@ -160,7 +160,13 @@ struct pm_ctx {
     // profiling
     bool profiling = false;
     std::vector<pm::Timer> timers[pm::kClasses];
-    size_t timers_used[pm::kClasses] = {0, 0, 0, 0};
+    size_t timers_used[pm::kClasses] = {0, 0, 0, 0, 0};
+
+    // hipGraph of one pm_run (PM_OPT_GRAPH): captured on first use, replayed while the
+    // launch sequence and every buffer it touches stay the same (graph_key)
+    bool use_graph = false;
+    hipGraphExec_t graph_exec = nullptr;
+    uint64_t graph_key = 0;
 
     // replay (pm_replay.cpp)
     pm::ReplayState* replay = nullptr;
