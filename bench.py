@@ -45,6 +45,8 @@ def parse():
                    help="replay each step's launch sequence from a hipGraph (PM_OPT_GRAPH); "
                         "per-kernel times then come from an extra untimed eager pass")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
+    p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
+                   help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
     p.add_argument("--replay-leaves", type=int, default=1000)
     p.add_argument("--replay-blocks", type=int, default=500)
     p.add_argument("--replay-block-len", type=int, default=10_000)
@@ -77,9 +79,12 @@ def main():
     lo, hi = shard_range(rank, world, S)
     s_local = hi - lo
     t0 = time.time()
-    off, idx, root = panman_amd.random_join_tree(L, seed=1)
-    n_nodes = 2 * L - 1
-    n_int = L - 1
+    if args.tree == "random-join":
+        off, idx, root = panman_amd.random_join_tree(L, seed=1)
+    else:
+        off, idx, root = panman_amd.sars_like_tree(L, seed=1)
+    n_nodes = off.shape[0] - 1
+    n_int = n_nodes - L
     log(rank, f"[bench] tree: {L} leaves, {n_nodes} nodes ({time.time() - t0:.1f}s)")
 
     eng = panman_amd.Engine(local)
@@ -217,9 +222,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u32 bit-planes (16-bit one-hot state sets)" if mode == panman_amd.MODE_FITCH
             else "u32 bit-planes (Z0/Z1 optimal-code sets, exact unit-cost Sankoff)",
-            "data": "synthetic (seeded on-device tree-evolved columns, random-join tree)",
+            "data": f"synthetic (seeded on-device tree-evolved columns, {args.tree} tree)",
             "config": {
-                "workload": f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)",
+                "workload": (f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)"
+                             if args.tree == "random-join" else
+                             f"{args.mode}: {L} leaves x {S} sites sars-like tree (T2; C3 at 100k leaves)"),
+                "tree": args.tree,
                 "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
                 "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
                 "mutations_total": muts_total,

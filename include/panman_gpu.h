@@ -247,6 +247,13 @@ int pm_pangraph_build(pm_ctx* ctx, const char* json, const char* newick, const c
  * 2*leaves-1 nodes as CSR; leaves are ids [0, leaves), internal nodes follow. */
 int pm_synth_tree_random_join(int64_t leaves, uint64_t seed, int32_t* child_offsets,
                               int32_t* child_index, int32_t* root);
+/* "SARS-like" tree (SURVEY.md §8d family T2): ladderised sequential insertion (leaf i
+ * splits the pendant edge of leaf i-1 with p = 0.9, else of a uniform earlier leaf), then
+ * 10 % of the internal nodes contracted into polytomies of 3-64 children.  Buffers must
+ * hold 2*leaves-1 nodes (child_offsets 2*leaves entries, child_index 2*leaves-2); the
+ * node count written is returned in *num_nodes; leaves are ids [0, leaves). */
+int pm_synth_tree_sars_like(int64_t leaves, uint64_t seed, int32_t* child_offsets, int32_t* child_index,
+                            int32_t* root, int64_t* num_nodes);
 /* Evolve columns [site_begin, site_begin + num_sites) of a seeded alignment down the
  * uploaded tree on the device and install them as the leaf columns plus the consensus
  * (the root sequence).  Identical global sites give identical columns on every rank. */

@@ -51,6 +51,8 @@ _SIGS = {
     "pm_site_results": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_site_results_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_kernel_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "pm_synth_tree_sars_like": (C.c_int, [C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]),
     "pm_synth_tree_random_join": (C.c_int, [C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p,
                                             C.POINTER(C.c_int32)]),
     "pm_synth_columns": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]),

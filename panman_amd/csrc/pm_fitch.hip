@@ -183,6 +183,18 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
+    dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
+    dn.count = virt ? ht.num_tail_v : ht.num_tail;
+    if (dn.count > 0) {
+        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        const bool ap = c->leaves_all_present;
+        timer_begin(c, 1);
+        if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        timer_end(c, 1);
+    }
     return hipGetLastError();
 }
 

@@ -64,6 +64,8 @@ void free_tree(DevTree& t) {
     dev_free(t.up_desc);
     dev_free(t.up_desc_v);
     dev_free(t.down_desc_v);
+    dev_free(t.tail_desc);
+    dev_free(t.tail_desc_v);
     dev_free(t.vleaf);
     dev_free(t.rg_node_off);
     dev_free(t.rg_node_dense);
@@ -685,6 +687,24 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const std::vector<NodeDesc> down_desc_v = make_desc(down_order_v, child_enc_v);
     const std::vector<NodeDesc> up_desc = make_desc(up_order, ht.child_enc);
     const std::vector<NodeDesc> up_desc_v = make_desc(up_order_v, child_enc_v);
+    auto make_tail = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
+        std::vector<TailDesc> tail;
+        for (int32_t d : order)
+            for (int32_t e = ht.child_off[d] + 2; e < ht.child_off[d + 1]; ++e) {
+                const int32_t x = enc[e];
+                if (x >= 0 && !(x & kVirtualBit)) continue;   // materialised child: its own wave
+                TailDesc t{};
+                t.parent = d;
+                t.enc = x;
+                for (int j = 0; j < 4; ++j) t.vl[j] = x >= 0 ? vleaf[(size_t)(x & ~kVirtualBit) * 4 + j] : -1;
+                tail.push_back(t);
+            }
+        return tail;
+    };
+    const std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
+    const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
+    ht.num_tail = (int32_t)tail_desc.size();
+    ht.num_tail_v = (int32_t)tail_desc_v.size();
 
     Regions rg;
     build_regions(bfs, off, idx, t->root, ht, rg);
@@ -716,6 +736,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_desc_v, up_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
+        (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
+        (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_dense, rg.node_dense, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_pslot, rg.node_pslot, c->stream)) != hipSuccess ||
@@ -979,6 +1001,76 @@ int pm_synth_tree_random_join(int64_t leaves, uint64_t seed, int32_t* child_offs
     }
     (void)N;
     *root = pool[0];
+    return PM_OK;
+}
+
+int pm_synth_tree_sars_like(int64_t leaves, uint64_t seed, int32_t* child_offsets, int32_t* child_index,
+                            int32_t* root, int64_t* num_nodes) {
+    // SURVEY.md §8d family T2: ladderised sequential insertion -- leaf i splits the pendant
+    // edge of leaf i-1 with p = 0.9, else of a uniform earlier leaf -- then 10 % of the
+    // internal nodes are merged away (edge contraction) into polytomies of 3-64 children.
+    if (leaves < 2 || leaves > (int64_t)1 << 29 || !child_offsets || !child_index || !root || !num_nodes)
+        return PM_ERR_ARG;
+    std::mt19937_64 rng(seed);
+    auto uniform = [&](uint64_t n) { return (uint64_t)((unsigned __int128)rng() * n >> 64); };
+    auto coin = [&](double p) { return (double)(rng() >> 11) * 0x1.0p-53 < p; };
+    const int64_t L = leaves, N0 = 2 * leaves - 1;
+    std::vector<int32_t> par(N0, -1);
+    std::vector<std::vector<int32_t>> kids(N0);
+    int32_t next = (int32_t)L;
+    const int32_t r = next++;
+    kids[r] = {0, 1};
+    par[0] = par[1] = r;
+    for (int64_t i = 2; i < L; ++i) {
+        const int32_t t = coin(0.9) ? (int32_t)(i - 1) : (int32_t)uniform((uint64_t)i);
+        const int32_t q = par[t], v = next++;
+        for (int32_t& k : kids[q])
+            if (k == t) k = v;
+        par[v] = q;
+        kids[v] = {t, (int32_t)i};
+        par[t] = par[i] = v;
+    }
+    // polytomies: visit internal non-root nodes in random order; a visited node absorbs
+    // internal children (its own kids first) until it has k ~ U[3,64] children, never more
+    // than 64, until 10 % of the internal nodes are gone
+    std::vector<int32_t> perm;
+    for (int32_t v = (int32_t)L + 1; v < next; ++v) perm.push_back(v);
+    for (size_t i = perm.size(); i > 1; --i) std::swap(perm[i - 1], perm[uniform(i)]);
+    std::vector<uint8_t> dead(N0, 0);
+    int64_t budget = (int64_t)(0.1 * (double)(next - L));
+    for (int32_t v : perm) {
+        if (budget <= 0) break;
+        if (dead[v]) continue;
+        const size_t k = 3 + (size_t)uniform(62);
+        size_t scan = 0;
+        while (kids[v].size() < k && budget > 0 && scan < kids[v].size()) {
+            const int32_t c = kids[v][scan];
+            if (c < L || kids[v].size() - 1 + kids[c].size() > 64) {
+                ++scan;
+                continue;
+            }
+            std::vector<int32_t> g = std::move(kids[c]);
+            kids[v].erase(kids[v].begin() + scan);
+            kids[v].insert(kids[v].begin() + scan, g.begin(), g.end());
+            for (int32_t x : g) par[x] = v;
+            dead[c] = 1;
+            --budget;
+        }
+    }
+    // compact ids: leaves keep [0, L), surviving internal nodes follow in creation order
+    std::vector<int32_t> id(N0, -1);
+    int32_t n = 0;
+    for (int32_t v = 0; v < next; ++v)
+        if (!dead[v]) id[v] = n++;
+    int64_t e = 0;
+    child_offsets[0] = 0;
+    for (int32_t v = 0; v < next; ++v) {
+        if (dead[v]) continue;
+        for (int32_t c : kids[v]) child_index[e++] = id[c];
+        child_offsets[id[v] + 1] = (int32_t)e;
+    }
+    *root = id[r];
+    *num_nodes = n;
     return PM_OK;
 }
 

@@ -43,6 +43,14 @@ struct alignas(64) NodeDesc {
     int32_t vl0[4], vl1[4];
 };
 
+// A leaf or virtual child beyond a node's first two (polytomies): its records need only
+// the parent's final, so they are emitted by one flat launch after the pre-order levels
+// instead of serially inside the parent's wave.
+struct alignas(32) TailDesc {
+    int32_t parent, enc, pad0, pad1;
+    int32_t vl[4];
+};
+
 struct DevTree {
     int32_t num_internal = 0;
     int32_t num_leaves = 0;
@@ -68,6 +76,8 @@ struct DevTree {
     NodeDesc* up_desc_v = nullptr;
     NodeDesc* down_desc_v = nullptr;
     int32_t* vleaf = nullptr;
+    TailDesc* tail_desc = nullptr;     // tails over child_enc
+    TailDesc* tail_desc_v = nullptr;   // tails over child_enc_v
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
     int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
@@ -104,6 +114,7 @@ struct HostTree {
     std::vector<int32_t> up_class_off_v;    // [4H+1] (level, degree class) buckets of up_order_v
     std::vector<int32_t> down_level_off_v;
     int64_t num_virtual = 0;
+    int32_t num_tail = 0, num_tail_v = 0;
     std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
     std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
 };

@@ -338,6 +338,7 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 
 struct DownArgs {
     const NodeDesc* desc;  // per level item
+    const TailDesc* tail;  // k_tail items
     int32_t count;
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     const int32_t* child_off;
@@ -565,8 +566,8 @@ __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink,
         virtual_kid<M, AP>(a, sink, k, word, valid, F);
 }
 
-// Every record of node n's wave: the node itself and its children (the first two from
-// registers, further ones fetched here).
+// Every record of node n's wave: the node itself and its first two children (prefetched
+// in registers).  Leaf / virtual children beyond the second are k_tail's items.
 template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int32_t e0, int32_t e1,
                                              const Kid* kids, int64_t word, uint32_t valid, const uint32_t* pc,
@@ -574,13 +575,25 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
     emit(sink, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
     kid_records<M, AP>(a, sink, kids[0], word, valid, F);
     if (e1 - e0 > 1) kid_records<M, AP>(a, sink, kids[1], word, valid, F);
-    for (int32_t e = e0 + 2; e < e1; ++e) {
-        Kid k;
-        const int32_t enc = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        const int4 vl = enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-        kid_fetch<M, AP>(a, enc, vl, word, k);
-        kid_records<M, AP>(a, sink, k, word, valid, F);
-    }
+}
+
+// Move a wave's staged records to one of the kShards record shards (one global atomic);
+// returns false, with the reserved base in `base`, when the stage overflowed and the
+// caller must redo its records into global memory.
+__device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* stage, uint32_t total, uint32_t shard,
+                                            int lane, int item, int tile, uint32_t& base, pm_mut*& out) {
+    base = 0;
+#ifdef PM_EXP_NOATOMIC
+    base = (uint32_t)((item * 64 + tile) % 1024) * 16;
+#else
+    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
+    base = __shfl(base, 0, 64);
+#endif
+    out = a.recs + (size_t)shard * a.shard_cap;
+    if (total > kStage) return false;
+    for (uint32_t i = lane; i < total; i += kWave)
+        if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[i];
+    return true;
 }
 
 // Pre-order + assignment for one node and its leaf children.  Final state:
@@ -694,22 +707,41 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
 #endif
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
-    uint32_t base = 0;
-#ifdef PM_EXP_NOATOMIC
-    base = (uint32_t)((item * 64 + tile) % 1024) * 16;
-#else
-    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
-    base = __shfl(base, 0, 64);
-#endif
-    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
-    if (total <= kStage) {
-        for (uint32_t i = lane; i < total; i += kWave)
-            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
-        return;
-    }
+    uint32_t base;
+    pm_mut* out;
+    if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
     if (lane == 0) stage_cnt[wave] = 0;   // overflowed the stage: redo straight into global
     node_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc,
                     F, self_diff);
+}
+
+// Records of the leaf / virtual children beyond a node's second (polytomies), after the
+// pre-order levels: wave = (tail item, tile), parent final read back from `finals`.
+template <Mode M, bool AP>
+__global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
+    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    __shared__ uint32_t stage_cnt[kWavesPerBlock];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    if (item >= a.count) return;
+    if (lane == 0) stage_cnt[wave] = 0;
+    const TailDesc& t = a.tail[item];
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint32_t valid = valid_mask(a, word);
+    Kid k;
+    kid_fetch<M, AP>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, k);
+    const uint4 q = a.finals[(size_t)t.parent * a.wpad + word];
+    const uint32_t F[4] = {q.x, q.y, q.z, q.w};
+    kid_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
+    const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+    if (total == 0) return;
+    const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
+    uint32_t base;
+    pm_mut* out;
+    if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
+    if (lane == 0) stage_cnt[wave] = 0;
+    kid_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
 }
 
 }  // namespace pm

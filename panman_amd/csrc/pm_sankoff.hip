@@ -182,6 +182,15 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
+    dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
+    dn.count = virt ? ht.num_tail_v : ht.num_tail;
+    if (dn.count > 0) {
+        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        timer_begin(c, 1);
+        if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        timer_end(c, 1);
+    }
     return hipGetLastError();
 }
 

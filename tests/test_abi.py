@@ -3,6 +3,8 @@ symbol include/panman_gpu.h declares (no compute calls without a GPU)."""
 import ctypes
 import subprocess
 
+import numpy as np
+
 import panman_amd
 
 
@@ -37,6 +39,36 @@ def test_random_join_tree_shape():
     assert sorted(idx.tolist() + [root]) == list(range(n))
     assert all(off[i + 1] - off[i] in (0, 2) for i in range(n))
     off2, idx2, root2 = panman_amd.random_join_tree(1000, seed=1)
+    assert (off == off2).all() and (idx == idx2).all() and root == root2
+
+
+def _height(off, idx, root):
+    order, i = [root], 0
+    while i < len(order):
+        v = order[i]
+        i += 1
+        order.extend(idx[off[v]:off[v + 1]].tolist())
+    h = {}
+    for v in reversed(order):
+        h[v] = 1 + max(h[c] for c in idx[off[v]:off[v + 1]]) if off[v + 1] > off[v] else 0
+    return h[root], len(order)
+
+
+def test_sars_like_tree_shape():
+    L = 5000
+    off, idx, root = panman_amd.sars_like_tree(L, seed=1)
+    n = off.shape[0] - 1
+    deg = np.diff(off)
+    assert (deg[:L] == 0).all() and (deg[L:] >= 2).all() and deg.max() <= 64
+    assert sorted(idx.tolist() + [root]) == list(range(n))   # every node once, a tree
+    internal = n - L
+    assert internal <= L - 1 and internal >= 0.85 * (L - 1)   # ~10 % contracted
+    assert (deg > 2).sum() > 0
+    h, reach = _height(off, idx, root)
+    assert reach == n
+    hj, _ = _height(*panman_amd.random_join_tree(L, seed=1))
+    assert h > 3 * hj   # ladderised: much deeper than random-join
+    off2, idx2, root2 = panman_amd.sars_like_tree(L, seed=1)
     assert (off == off2).all() and (idx == idx2).all() and root == root2
 
 

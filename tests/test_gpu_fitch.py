@@ -177,3 +177,29 @@ def test_msa_driver_m1_vs_oracle(oracle, with_ref):
     got = panman_amd.msa_build(nwk, msa, ref, panman_amd.MODE_FITCH)
     assert not want.startswith("#error"), want
     assert got == want
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_sars_like_tree_vs_oracle(engine, oracle, variant):
+    """SURVEY.md §8d family T2 (deep ladder + polytomies up to 64) with tree-evolved columns."""
+    leaves, sites = 6000, 2500
+    off, idx, root = panman_amd.sars_like_tree(leaves, seed=5)
+    n = off.shape[0] - 1
+    _variant(engine, variant)
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, sites, seed=2)
+    engine.run(panman_amd.MODE_FITCH)
+    got = engine.mutations()
+    score, rootc = engine.site_results()
+    sample = slice(700, 956)
+    codes = engine.leaf_codes(sample.start, sample.stop - sample.start, leaves)
+    cons = engine.consensus(sample.start, sample.stop - sample.start)
+    node_row = np.full(n, -1, np.int32)
+    node_row[:leaves] = np.arange(leaves)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, None,
+                                            algo=0, threads=8, with_root=True)
+    want[:, 1] += sample.start
+    sel = got[(got[:, 1] >= sample.start) & (got[:, 1] < sample.stop)]
+    assert sel.shape == want.shape and (sel == want).all()
+    assert (rootc[sample] == want_root).all()
+    assert (score == np.bincount(got[got[:, 0] != root][:, 1], minlength=sites)).all()

@@ -127,3 +127,26 @@ def test_star_polytomy_vs_oracle(engine, oracle, mode, width):
                                             algo=mode, threads=8, with_root=True)
     assert got.shape == want.shape and (got == want).all()
     assert (engine.site_results()[1] == want_root).all()
+
+
+def test_sankoff_sars_like_tree_vs_oracle(engine, oracle):
+    """SURVEY.md §8d family T2 (deep ladder + polytomies up to 64) with tree-evolved columns."""
+    leaves, sites = 6000, 2500
+    off, idx, root = panman_amd.sars_like_tree(leaves, seed=6)
+    n = off.shape[0] - 1
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, sites, seed=2)
+    engine.run(panman_amd.MODE_SANKOFF)
+    got = engine.mutations()
+    _, rootc = engine.site_results()
+    sample = slice(1200, 1456)
+    codes = engine.leaf_codes(sample.start, sample.stop - sample.start, leaves)
+    cons = engine.consensus(sample.start, sample.stop - sample.start)
+    node_row = np.full(n, -1, np.int32)
+    node_row[:leaves] = np.arange(leaves)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, None,
+                                            algo=1, threads=8, with_root=True)
+    want[:, 1] += sample.start
+    sel = got[(got[:, 1] >= sample.start) & (got[:, 1] < sample.stop)]
+    assert sel.shape == want.shape and (sel == want).all()
+    assert (rootc[sample] == want_root).all()
