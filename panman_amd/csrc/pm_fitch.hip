@@ -69,6 +69,134 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
 #endif
 }
 
+// Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
+// round-robin to its 4 waves.  Each wave loads 64 child encodings (and virtual children's
+// leaves) with one vector load, then fetches two children before folding either, so the
+// chain of dependent loads per node shrinks ~8x; the waves' (both, either) accumulators
+// are combined through LDS (AND / OR are associative: src/fitchSankoff.cpp:39-55).
+struct UpFetch {
+    uint32_t w[16];
+    bool complex_lane;
+};
+
+template <bool AP>
+__device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
+                                         UpFetch& f) {
+    f.complex_lane = false;
+    if (c < 0) {
+        uint4 L;
+        leaf_word<AP>(a, -c - 1, word, L, f.w[4]);
+        f.w[0] = L.x; f.w[1] = L.y; f.w[2] = L.z; f.w[3] = L.w;
+    } else if (c & kVirtualBit) {
+        uint4 L0, L1 = make_uint4(0, 0, 0, 0);
+        f.w[9] = 0;
+        leaf_word<AP>(a, vl.x, word, L0, f.w[4]);
+        if (vl.y >= 0) leaf_word<AP>(a, vl.y, word, L1, f.w[9]);
+        f.w[0] = L0.x; f.w[1] = L0.y; f.w[2] = L0.z; f.w[3] = L0.w;
+        f.w[5] = L1.x; f.w[6] = L1.y; f.w[7] = L1.z; f.w[8] = L1.w;
+    } else {
+        const size_t rec = (size_t)c * a.tiles + tile;
+        const RecMask mk = rec_mask(a.cmask, rec);
+        const uint4* p = a.sets + rec * kFitchRec;
+        f.complex_lane = (mk.x >> lane) & 1ull;
+        if (f.complex_lane) {
+            const uint32_t k = lanes_below(mk.x);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 w = p[kWave + q * kWave + k];
+                f.w[4 * q] = w.x; f.w[4 * q + 1] = w.y; f.w[4 * q + 2] = w.z; f.w[4 * q + 3] = w.w;
+            }
+        } else {
+            const uint4 w = rec_code(p, mk, lane, a.cons, word);
+            f.w[0] = w.x; f.w[1] = w.y; f.w[2] = w.z; f.w[3] = w.w;
+        }
+    }
+}
+
+__device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* both, uint32_t* either) {
+    uint32_t x[16];
+    if (c >= 0 && !(c & kVirtualBit) && f.complex_lane) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) x[v] = f.w[v];
+    } else {
+        const bool leafish = c < 0 || (c & kVirtualBit);
+        const LoHi t = lohi_of(f.w[0], f.w[1], f.w[2], f.w[3], leafish ? f.w[4] : ~0u);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
+        if (c >= 0 && (c & kVirtualBit)) {
+            const LoHi u = lohi_of(f.w[5], f.w[6], f.w[7], f.w[8], f.w[9]);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        both[v] &= x[v];
+        either[v] |= x[v];
+    }
+}
+
+template <bool AP>
+__global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
+    __shared__ uint32_t part[kWavesPerBlock - 1][32][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const NodeDesc& d = a.desc[blockIdx.x];
+    const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+
+    uint32_t both[16], either[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
+    for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
+        const int32_t my = base + kWavesPerBlock * lane;
+        const int32_t enc = my < e1 ? a.child_enc[my] : 0;
+        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+                                                                   : make_int4(-1, -1, -1, -1);
+        const int cnt = min(kWave, (e1 - base + kWavesPerBlock - 1) / kWavesPerBlock);
+        for (int k = 0; k < cnt; k += 2) {
+            const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
+            const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
+            UpFetch f0, f1;
+            up_fetch<AP>(a, c0, v0, tile, lane, word, f0);
+            const bool two = k + 1 < cnt;
+            int32_t c1 = 0;
+            if (two) {
+                c1 = __builtin_amdgcn_readlane(enc, k + 1);
+                const int4 v1 = make_int4(__builtin_amdgcn_readlane(vl.x, k + 1),
+                                          __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1);
+                up_fetch<AP>(a, c1, v1, tile, lane, word, f1);
+            }
+            up_fold(c0, f0, both, either);
+            if (two) up_fold(c1, f1, both, either);
+        }
+    }
+    if (wave > 0) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            part[wave - 1][v][lane] = both[v];
+            part[wave - 1][16 + v][lane] = either[v];
+        }
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock - 1; ++w)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            both[v] &= part[w][v][lane];
+            either[v] |= part[w][16 + v][lane];
+        }
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
+    if (n == a.root_dense && a.forced != nullptr) {
+        const uint4 F = a.forced[word];
+        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
+    }
+    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
+}
+
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
 // LDS (sites fit) or straight into global counters.
 __global__ __launch_bounds__(kBlock) void k_site_score(const pm_mut* recs, const uint32_t* shard_cnt,
@@ -130,16 +258,30 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
+    const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
     const int H = (int)up_off.size() - 1;
     for (int h = 0; h < H; ++h) {
-        up.desc = up_desc + up_off[h];
-        up.count = up_off[h + 1] - up_off[h];
-        if (up.count == 0) continue;
-        dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
-        timer_begin(c, 0);
-        if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up<true>, grid, dim3(kBlock), 0, c->stream, up);
-        else hipLaunchKernelGGL(k_fitch_up<false>, grid, dim3(kBlock), 0, c->stream, up);
-        timer_end(c, 0);
+        // out-degree <= 3: one wave per (node, tile); wider: one workgroup per (node, tile)
+        const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
+                      e = class_off[(h + 1) * kDegreeClasses];
+        if (m > b) {
+            up.desc = up_desc + b;
+            up.count = m - b;
+            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+            timer_begin(c, 0);
+            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up<true>, grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL(k_fitch_up<false>, grid, dim3(kBlock), 0, c->stream, up);
+            timer_end(c, 0);
+        }
+        if (e > m) {
+            up.desc = up_desc + m;
+            up.count = e - m;
+            dim3 grid(up.count, tiles);
+            timer_begin(c, 0);
+            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL(k_fitch_up_wide<false>, grid, dim3(kBlock), 0, c->stream, up);
+            timer_end(c, 0);
+        }
     }
 
     hipError_t e = hipMemsetAsync(c->shard_cnt, 0, sizeof(uint32_t) * kShards, c->stream);
