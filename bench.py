@@ -41,6 +41,10 @@ def parse():
     p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--e2e", action="store_true",
+                   help="also time the end-to-end path (H2D of the packed leaf matrix, the run, D2H of "
+                        "every mutation record) on the same workload (SURVEY.md §8d), N=1 only")
+    p.add_argument("--cpu-sites-1t", type=int, default=4, help="columns timed on the 1-thread CPU baseline")
     p.add_argument("--graph", action="store_true",
                    help="replay each step's launch sequence from a hipGraph (PM_OPT_GRAPH); "
                         "per-kernel times then come from an extra untimed eager pass")
@@ -203,10 +207,17 @@ def main():
     if mode == panman_amd.MODE_SANKOFF:
         roofline["survey_contract_GBs"] = round(s_local * (1.5 * L + 97.0 * n_int) / (ms_step * 1e-3) / 1e9, 1)
 
+    copy_gbs = hbm_copy_bandwidth() if rank == 0 else None
+    roofline["measured_copy_GBs"] = copy_gbs
+    roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode)
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e:
+        e2e = end_to_end(eng, L, S, n_nodes, mode)
 
     if rank == 0:
         out = {
@@ -236,10 +247,66 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_sample": parity,
+            "end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def hbm_copy_bandwidth(gib: int = 4, reps: int = 10) -> float:
+    """Device-to-device copy rate (read + write bytes / s) of a `gib` GiB buffer: the
+    achievable-bandwidth reference beside the 8 TB/s spec."""
+    n = gib << 30
+    a = torch.empty(n, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del a, b
+    torch.cuda.empty_cache()
+    return round(2.0 * n * reps / dt / 1e9, 1)
+
+
+def end_to_end(eng, L, S, n_nodes, mode):
+    """End-to-end rate: the packed leaf matrix (0.5 B per leaf-site) goes
+    host -> device through pm_leaves_upload, the full run, then every mutation record
+    device -> host, sorted by (node, site).  The host matrix is built untimed from the
+    device-generated columns."""
+    import ctypes as C
+    stride = (S + 1) // 2
+    packed = np.empty((L, stride), np.uint8)
+    chunk = 2048
+    for s0 in range(0, S, chunk):
+        ns = min(chunk, S - s0)
+        codes = eng.leaf_codes(s0, ns, L)
+        packed[:, s0 // 2:(s0 + ns + 1) // 2] = panman_amd.pack_codes(codes)
+        del codes
+    cons = eng.consensus(0, S)
+    node_row = np.full(n_nodes, -1, np.int32)
+    node_row[:L] = np.arange(L, dtype=np.int32)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng._check(eng.lib.pm_leaves_upload(eng.ctx, S, packed.ctypes.data, stride, node_row.ctypes.data, None, 0),
+               "pm_leaves_upload")
+    eng.sites_upload(cons)
+    t1 = time.perf_counter()
+    eng.run(mode)
+    n = eng.mutation_count()
+    t2 = time.perf_counter()
+    buf = np.empty(2 * max(n, 1), np.uint32)
+    got = C.c_int64(0)
+    eng._check(eng.lib.pm_mutations_fetch(eng.ctx, buf.ctypes.data, n, C.byref(got)), "pm_mutations_fetch")
+    t3 = time.perf_counter()
+    total = t3 - t0
+    return {"seconds": round(total, 3), "value": S * n_nodes / total, "unit": "site*node updates/s",
+            "h2d_s": round(t1 - t0, 3), "run_s": round(t2 - t1, 3), "d2h_s": round(t3 - t2, 3),
+            "h2d_bytes": int(packed.nbytes), "d2h_bytes": int(8 * got.value), "records": int(got.value),
+            "note": "pageable host buffers; records sorted by (node, site) inside pm_mutations_fetch"}
 
 
 def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
@@ -257,10 +324,24 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     o = orc.load()
     secs, want = o.csr_columns(off, idx, root, names, codes, node_row, cons, None, algo=mode, threads=threads)
+    n1 = max(1, min(args.cpu_sites_1t, ns))
+    secs1, _ = o.csr_columns(off, idx, root, names, codes[:, :n1], node_row, cons[:n1], None, algo=mode, threads=1)
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     cpu = {"value": ns * n_nodes / secs, "unit": "site*node updates/s", "cores": threads,
            "kind": "port",
            "sample": f"first {ns} of the same columns, {L} leaves x {ns} sites, {threads} threads "
-                     f"({secs:.1f}s), oracle/pm_oracle.cpp faithful per-column loop"}
+                     f"({secs:.1f}s), oracle/pm_oracle.cpp faithful per-column loop",
+           "single_thread_value": n1 * n_nodes / secs1,
+           "single_thread_sample": f"first {n1} columns, 1 thread ({secs1:.1f}s): the reference M1 driver's "
+                                   f"sequential loop (src/panman.cpp:1380-1381)",
+           "host": {"nproc": os.cpu_count(), "cpu_model": model, "threads_used": threads}}
     # GPU on the identical sample columns (same kernels, separate context)
     e2 = panman_amd.Engine(0)
     e2.tree_upload(off, idx, root)
@@ -282,35 +363,53 @@ def replay_main(args):
 
     from panman_amd.synth import c5_panmat
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != 1:
-        raise SystemExit("replay mode runs on one GPU (leaf shards are independent replicas)")
-    torch.cuda.set_device(0)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     t0 = time.time()
-    pm = c5_panmat(leaves=args.replay_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len)
-    eng = panman_amd.Engine(0)
+    # weak scaling over leaves: N x replay-leaves leaves, rank r replays
+    # its contiguous share; tree and mutations are replicated, no collective
+    total_leaves = args.replay_leaves * world
+    pm = c5_panmat(leaves=total_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len)
+    off = pm.child_offsets
+    leaf_nodes = [i for i in range(pm.num_nodes) if off[i] == off[i + 1]]
+    lo, hi = shard_range(rank, world, len(leaf_nodes))
+    eng = panman_amd.Engine(local)
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    eng.replay_prepare(pm)
+    eng.replay_prepare(pm, (lo, hi) if world > 1 else None)
     leaves, cols, edits = eng.replay_shape()
-    print(f"[bench] replay PanMAT {leaves} leaves x {cols} columns, {edits} edits ({time.time() - t0:.1f}s)",
-          file=sys.stderr, flush=True)
+    log(rank, f"[bench] replay PanMAT {leaves} of {total_leaves} leaves x {cols} columns, {edits} edits "
+              f"({time.time() - t0:.1f}s)")
     for _ in range(max(1, args.warmup)):
         eng.replay_run()
     torch.cuda.synchronize()
     eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.replay_run()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t_start
     ms, launches = eng.kernel_times(4)
     eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     units = float(leaves) * cols
-    value = units * args.steps / elapsed
+    value = float(total_leaves) * cols * args.steps / elapsed
     # path mutation records per leaf (8 B each in the SURVEY.md §8d replay model)
     a = pm._arrays
     per_node = np.diff(a["nuc_mut_offsets"])
     parent = np.full(pm.num_nodes, -1, np.int64)
-    off = pm.child_offsets
     for v in range(pm.num_nodes):
         parent[pm.child_index[off[v]:off[v + 1]]] = v
     acc = per_node.astype(np.int64).copy()
@@ -323,7 +422,7 @@ def replay_main(args):
     for v in order:
         if parent[v] >= 0:
             acc[v] += acc[parent[v]]
-    path_recs = float(acc[[i for i in range(pm.num_nodes) if off[i] == off[i + 1]]].sum())
+    path_recs = float(acc[leaf_nodes[lo:hi]].sum())
     alg_bytes = units * 1.5 + 8.0 * path_recs
     kms = ms[3] / args.steps
     achieved = alg_bytes / (kms * 1e-3) / 1e9
@@ -335,7 +434,7 @@ def replay_main(args):
     text = C.string_at(ptr, n.value)
     eng.lib.pm_free(ptr)
     cpu = parity = None
-    if not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         import oracle as orc
         k = args.cpu_leaves
         want, secs = orc.load().fasta(pm, True, leaf_limit=k, timed=True)
@@ -351,13 +450,15 @@ def replay_main(args):
                          f"({secs:.1f}s, 1 thread; the reference's tbb::parallel_for_each body)"}
     out = {
         "metric": "FASTA replay leaf*column/s (aligned, GPU replay kernels)",
-        "value": value, "unit": "leaf*column/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "value": value, "unit": "leaf*column/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8 (ASCII IUPAC)",
         "data": "synthetic C5-like PanMAT (seeded: random-join tree, blocks, gap slots, block and nuc mutations)",
-        "config": {"workload": f"C5 replay: {leaves} leaves x {cols} aligned columns, "
+        "config": {"workload": f"C5 replay: {total_leaves} leaves x {cols} aligned columns, "
                                f"{args.replay_blocks} blocks, {edits} edits",
-                   "leaves": leaves, "columns": cols, "path_mutation_records": path_recs},
+                   "leaves": total_leaves, "leaves_per_gpu": leaves, "columns": cols,
+                   "path_mutation_records_rank0": path_recs,
+                   "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
         "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "algorithmic_bytes_per_launch": alg_bytes,
@@ -366,7 +467,10 @@ def replay_main(args):
         "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
         "cpu_baseline": cpu, "parity_sample": parity,
     }
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

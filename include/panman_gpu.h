@@ -153,6 +153,11 @@ void pm_free(void* p);
  * src/panmanUtils.cpp:1409-1465, :271-299): one tree, one block. */
 int pm_msa_to_panman(const char* newick, const char* msa_text, const char* reference, int mode, int device,
                      const char* out_path, char* err, int64_t err_len);
+/* The same with the columns split into contiguous ranges over `devices` (one host thread
+ * and context each; entries may repeat); records are merged by (node, site) on the host,
+ * so the file is byte-identical to the single-device build. */
+int pm_msa_to_panman_multi(const char* newick, const char* msa_text, const char* reference, int mode,
+                           const int* devices, int num_devices, const char* out_path, char* err, int64_t err_len);
 
 /* ---- root-to-leaf mutation replay (FASTA extraction) ---------------------------------- */
 /* PanMAT fields used by printFASTAUltraFast (src/panman.hpp:520-543 Block / GapList,
@@ -196,9 +201,17 @@ typedef struct pm_panmat {
  * Replay runs on the GPU (consensus expansion + path mutations per leaf); block order,
  * strands, rotation, circular offset and line wrapping are applied by the host formatter. */
 int pm_fasta(pm_ctx* ctx, const pm_panmat* panmat, int aligned, char** text, int64_t* length);
+/* pm_fasta over several devices: leaves split into contiguous ranges, one host thread and
+ * context per entry of `devices` (entries may repeat), texts concatenated in leaf order --
+ * byte-identical to pm_fasta.  On failure `err` receives the first shard's reason. */
+int pm_fasta_multi(const pm_panmat* panmat, int aligned, const int* devices, int num_devices, char** text,
+                   int64_t* length, char* err, int64_t err_len);
 /* The same in stages: prepare (host flattening + upload), run (GPU replay, async on the
  * ctx stream; profiling class 3), format (download + text). */
 int pm_replay_prepare(pm_ctx* ctx, const pm_panmat* panmat);
+/* Prepare only leaves [leaf_begin, leaf_end) of the PanMAT (leaves in node-id order): one
+ * GPU's shard when FASTA extraction is split by leaves. */
+int pm_replay_prepare_range(pm_ctx* ctx, const pm_panmat* panmat, int64_t leaf_begin, int64_t leaf_end);
 int pm_replay_run(pm_ctx* ctx);
 int pm_replay_format(pm_ctx* ctx, int aligned, char** text, int64_t* length);
 /* Canonical aligned columns per leaf of the prepared PanMAT (gap slots before each main

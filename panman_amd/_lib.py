@@ -63,6 +63,11 @@ _SIGS = {
     "pm_msa_to_panman": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_char_p,
                                    C.c_char_p, C.c_int64]),
     "pm_fasta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pm_fasta_multi": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p),
+                                 C.POINTER(C.c_int64), C.c_char_p, C.c_int64]),
+    "pm_msa_to_panman_multi": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_void_p, C.c_int,
+                                         C.c_char_p, C.c_char_p, C.c_int64]),
+    "pm_replay_prepare_range": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
     "pm_replay_prepare": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pm_replay_run": (C.c_int, [C.c_void_p]),
     "pm_replay_format": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),

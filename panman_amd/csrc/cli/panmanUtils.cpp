@@ -52,7 +52,9 @@ const Spec kSpecs[] = {
     {"reference", 'n', true, "Identifier of reference sequence for PanMAN construction (optional) or reroot (required)"},
     {"output-file", 'o', true, "Prefix of the output file name"},
     {"threads", 0, true, "Accepted for compatibility (the build runs on the GPU)"},
-    {"device", 0, true, "HIP device ordinal (default 0)"},
+    {"device", 0, true, "First HIP device ordinal (default 0)"},
+    {"gpus", 0, true, "Number of GPUs (devices device..device+N-1): MSA columns / FASTA leaves are split across them"},
+    {"backend", 0, true, "Compute backend: hip (the only one; there is no CPU product path)"},
 };
 
 // Reference commands outside the accelerated path: recognised so the error is explicit.
@@ -148,7 +150,7 @@ bool read_file(const std::string& path, std::string& out) {
 
 void print_error(const std::string& e) { std::cerr << "\033[1;31mError: " << e << "\033[0m\n"; }
 
-int build_from_msa(const Options& o, int device) {
+int build_from_msa(const Options& o, const std::vector<int>& devices) {
     if (!o.has("input-newick")) {
         print_error("File containing newick string not provided!");
         return 1;
@@ -174,8 +176,8 @@ int build_from_msa(const Options& o, int device) {
     const std::string out = "./panman/" + o.get("output-file") + ".panman";
     const auto t0 = Clock::now();
     char err[512] = {0};
-    const int rc = pm_msa_to_panman(newick.c_str(), msa.c_str(), ref.c_str(), mode, device, out.c_str(), err,
-                                    sizeof err);
+    const int rc = pm_msa_to_panman_multi(newick.c_str(), msa.c_str(), ref.c_str(), mode, devices.data(),
+                                          (int)devices.size(), out.c_str(), err, sizeof err);
     if (rc != PM_OK) {
         print_error(err[0] ? err : "PanMAN construction failed");
         return 1;
@@ -299,7 +301,8 @@ int build_from_pangraph(const Options& o, int device) {
     return 0;
 }
 
-int from_panman(const Options& o, int device) {
+int from_panman(const Options& o, const std::vector<int>& devices) {
+    const int device = devices[0];
     const std::string path = o.get("input-panman");
     std::cout << "starting reading panman" << std::endl;
     const auto t0 = Clock::now();
@@ -338,19 +341,16 @@ int from_panman(const Options& o, int device) {
     }
     for (int aligned = 0; aligned < 2 && status == 0; ++aligned) {
         if (!o.has(aligned ? "fasta-aligned" : "fasta")) continue;
-        pm_ctx* ctx = nullptr;
-        if (pm_create(device, &ctx) != PM_OK) {
-            print_error("no HIP device");
-            status = 1;
-            break;
-        }
         const auto f0 = Clock::now();
         for (int i = 0; i < trees && status == 0; ++i) {
             pm_panmat view;
             char* text = nullptr;
             int64_t len = 0;
-            if (pm_panman_tree(file, i, &view) != PM_OK || pm_fasta(ctx, &view, aligned, &text, &len) != PM_OK) {
-                print_error(pm_last_error(ctx));
+            char err[512] = {0};
+            if (pm_panman_tree(file, i, &view) != PM_OK ||
+                pm_fasta_multi(&view, aligned, devices.data(), (int)devices.size(), &text, &len, err, sizeof err) !=
+                    PM_OK) {
+                print_error(err[0] ? err : "FASTA extraction failed");
                 status = 1;
                 break;
             }
@@ -358,7 +358,6 @@ int from_panman(const Options& o, int device) {
             pm_free(text);
         }
         std::cout << "\nFASTA execution time: " << ns_since(f0) << " nanoseconds\n";
-        pm_destroy(ctx);
     }
     pm_panman_free(file);
     return status;
@@ -378,10 +377,21 @@ int main(int argc, char** argv) {
         usage(std::cout);
         return 0;
     }
+    if (o.has("backend") && o.get("backend") != "hip") {
+        print_error("--backend " + o.get("backend") + ": this build computes on the GPU only (use --backend hip)");
+        return 1;
+    }
     const int device = o.has("device") ? std::atoi(o.get("device").c_str()) : 0;
+    const int gpus = o.has("gpus") ? std::atoi(o.get("gpus").c_str()) : 1;
+    if (gpus < 1 || gpus > 64) {
+        print_error("--gpus must be between 1 and 64");
+        return 1;
+    }
+    std::vector<int> devices;
+    for (int g = 0; g < gpus; ++g) devices.push_back(device + g);
     if (o.has("input-pangraph")) return build_from_pangraph(o, device);
-    if (o.has("input-msa")) return build_from_msa(o, device);
-    if (o.has("input-panman")) return from_panman(o, device);
+    if (o.has("input-msa")) return build_from_msa(o, devices);
+    if (o.has("input-panman")) return from_panman(o, devices);
     print_error("no input: give -I <file.panman> or -M <msa> -N <newick>");
     usage(std::cerr);
     return 1;

@@ -864,6 +864,10 @@ int pm_mutations_fetch(pm_ctx* c, pm_mut* out, int64_t cap, int64_t* count) {
     *count = n;
     if (!out) return PM_OK;
     if (cap < n) return fail(c, PM_ERR_ARG, "output capacity too small");
+    if (n <= INT32_MAX) {   // device radix sort (pm_sort.hip), one D2H copy
+        const hipError_t e = sort_records_to_host(c, counts, n, out);
+        return e == hipSuccess ? PM_OK : hip_fail(c, e, "record sort");
+    }
     int64_t at = 0;
     for (int s = 0; s < kShards; ++s) {
         if (!counts[s]) continue;

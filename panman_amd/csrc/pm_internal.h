@@ -195,6 +195,9 @@ void timer_end(pm_ctx* c, int cls);
 hipError_t launch_fitch(pm_ctx* c, bool block);
 hipError_t launch_fitch_fused(pm_ctx* c);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
+// Records of the last run, sorted by (node, site) on the device, copied to host `out`.
+hipError_t sort_records_to_host(pm_ctx* c, const std::vector<uint32_t>& counts, int64_t n, pm_mut* out);
+static_assert(sizeof(pm_mut) == 8, "pm_mut is {node, site_info}");
 hipError_t launch_score(pm_ctx* c);
 hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_stride, const int32_t* d_row_of_leaf,
                              const uint8_t* d_present, int64_t present_stride);

@@ -14,6 +14,7 @@
 #include <sstream>
 #include <stack>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pm_internal.h"
@@ -99,7 +100,8 @@ struct MsaResult {
 };
 
 // The constructor body: returns the tree, consensus block and per-node NucMut lists.
-MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_c, int mode, int device) {
+MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_c, int mode,
+                       const std::vector<int>& devices) {
     MsaResult res;
     std::string newick(newick_c), err;
     const size_t nl = newick.find('\n');
@@ -184,19 +186,49 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
         for (int64_t s = 0; s < S; ++s) force4[s / 2] |= (uint8_t)(nuc_code((*ref_row)[s]) << (4 * (s & 1)));
     }
 
-    CtxGuard g;
-    int rc = pm_create(device, &g.c);
-    if (rc != PM_OK) return dump_error("no HIP device");
-    pm_tree tree{N, t.root, off.data(), idx.data()};
-    if ((rc = pm_tree_upload(g.c, &tree)) != PM_OK ||
-        (rc = pm_leaves_upload(g.c, S, codes.data(), stride, node_row.data(), nullptr, 0)) != PM_OK ||
-        (rc = pm_sites_upload(g.c, cons4.data(), ref_row ? force4.data() : nullptr)) != PM_OK ||
-        (rc = pm_run(g.c, mode)) != PM_OK)
-        return dump_error(pm_last_error(g.c));
-    int64_t n = 0;
-    if ((rc = pm_mutation_count(g.c, &n)) != PM_OK) return dump_error(pm_last_error(g.c));
-    std::vector<pm_mut> recs((size_t)std::max<int64_t>(n, 1));
-    if ((rc = pm_mutations_fetch(g.c, recs.data(), n, &n)) != PM_OK) return dump_error(pm_last_error(g.c));
+    // columns split into contiguous even-aligned ranges, one host thread + context per
+    // device; each range's records are (node, site)-sorted, so appending
+    // the ranges in site order and stable-sorting by node gives the global (node, site) order
+    const int G = (int)devices.size();
+    std::vector<std::vector<pm_mut>> part(G);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> th;
+    std::vector<int64_t> lo(G + 1);
+    for (int g = 0; g <= G; ++g) lo[g] = std::min<int64_t>(S, (S * g / G + 1) / 2 * 2);
+    lo[G] = S;
+    for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g]() {
+            const int64_t a = lo[g], ns = lo[g + 1] - lo[g];
+            if (ns <= 0) return;
+            CtxGuard cg;
+            if (pm_create(devices[g], &cg.c) != PM_OK) {
+                msg[g] = "no HIP device " + std::to_string(devices[g]);
+                return;
+            }
+            pm_tree tree{N, t.root, off.data(), idx.data()};
+            int64_t n = 0;
+            if (pm_tree_upload(cg.c, &tree) != PM_OK ||
+                pm_leaves_upload(cg.c, ns, codes.data() + a / 2, stride, node_row.data(), nullptr, 0) != PM_OK ||
+                pm_sites_upload(cg.c, cons4.data() + a / 2, ref_row ? force4.data() + a / 2 : nullptr) != PM_OK ||
+                pm_run(cg.c, mode) != PM_OK || pm_mutation_count(cg.c, &n) != PM_OK) {
+                msg[g] = pm_last_error(cg.c);
+                return;
+            }
+            part[g].resize((size_t)std::max<int64_t>(n, 1));
+            if (pm_mutations_fetch(cg.c, part[g].data(), n, &n) != PM_OK) {
+                msg[g] = pm_last_error(cg.c);
+                return;
+            }
+            part[g].resize((size_t)n);
+            for (pm_mut& m : part[g]) m.site_info += (uint32_t)a << 8;
+        });
+    for (auto& x : th) x.join();
+    for (int g = 0; g < G; ++g)
+        if (!msg[g].empty()) return dump_error(msg[g]);
+    std::vector<pm_mut> recs;
+    for (auto& v : part) recs.insert(recs.end(), v.begin(), v.end());
+    if (G > 1) std::stable_sort(recs.begin(), recs.end(), [](const pm_mut& x, const pm_mut& y) { return x.node < y.node; });
+    const int64_t n = (int64_t)recs.size();
 
     for (int64_t a = 0; a < n;) {
         int64_t b = a;
@@ -208,7 +240,7 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
 }
 
 std::string build(const char* newick_c, const char* msa_c, const char* ref_c, int mode, int device) {
-    MsaResult r = build_result(newick_c, msa_c, ref_c, mode, device);
+    MsaResult r = build_result(newick_c, msa_c, ref_c, mode, {device});
     if (!r.err.empty()) return dump_error(r.err);
     std::string dump = "#consensus\t" + r.consensus + "\n";
     dump += "#blockmut\t" + r.t.name[r.t.root] + "\t0\t-1\t1\t0\n";
@@ -255,14 +287,21 @@ void pm_free(void* p) { std::free(p); }
 
 int pm_msa_to_panman(const char* newick, const char* msa_text, const char* reference, int mode, int device,
                      const char* out_path, char* err, int64_t err_len) {
+    return pm_msa_to_panman_multi(newick, msa_text, reference, mode, &device, 1, out_path, err, err_len);
+}
+
+int pm_msa_to_panman_multi(const char* newick, const char* msa_text, const char* reference, int mode,
+                           const int* devices, int num_devices, const char* out_path, char* err, int64_t err_len) {
     auto set_err = [&](const std::string& e) {
         if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
     };
-    if (!newick || !msa_text || !out_path || (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF)) {
+    if (!newick || !msa_text || !out_path || (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF) || !devices ||
+        num_devices < 1) {
         set_err("bad arguments");
         return PM_ERR_ARG;
     }
-    pm::MsaResult r = pm::build_result(newick, msa_text, reference, mode, device);
+    pm::MsaResult r = pm::build_result(newick, msa_text, reference, mode,
+                                       std::vector<int>(devices, devices + num_devices));
     if (!r.err.empty()) {
         set_err(r.err);
         return PM_ERR_ARG;

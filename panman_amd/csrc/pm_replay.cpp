@@ -12,6 +12,7 @@
 // drops '-' (unaligned) and the 'x' sentinels, rotates by the circular offset and wraps
 // at 70 columns.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -45,7 +46,7 @@ hipError_t dput(T** dst, const std::vector<T>& v, hipStream_t s) {
 
 }  // namespace
 
-int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
+int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin, int64_t leaf_end) {
     const int32_t N = p->num_nodes;
     if (N < 1 || p->root < 0 || p->root >= N || !p->child_offsets || !p->names)
         return fail(c, PM_ERR_ARG, "bad PanMAT topology");
@@ -67,6 +68,11 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r) {
     for (int32_t i = 0; i < N; ++i) {
         if (r.parent[i] == -2) return fail(c, PM_ERR_ARG, "node unreachable from the root");
         if (p->child_offsets[i] == p->child_offsets[i + 1]) r.leaves.push_back(i);
+    }
+    if (leaf_begin >= 0 || leaf_end >= 0) {   // a shard of the leaves
+        if (leaf_begin < 0 || leaf_end < leaf_begin || leaf_end > (int64_t)r.leaves.size())
+            return fail(c, PM_ERR_ARG, "leaf range outside [0, leaves]");
+        r.leaves = std::vector<int32_t>(r.leaves.begin() + leaf_begin, r.leaves.begin() + leaf_end);
     }
 
     // ---- blocks (vector order defines blockLengths resets; ids must be unique)
@@ -318,15 +324,17 @@ using namespace pm;
 
 extern "C" {
 
-int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) {
+int pm_replay_prepare_range(pm_ctx* c, const pm_panmat* p, int64_t leaf_begin, int64_t leaf_end) {
     if (!c || !p) return PM_ERR_ARG;
     (void)hipSetDevice(c->device);
     free_replay(c);
     c->replay = new ReplayState();
-    int rc = replay_prepare(c, p, *c->replay);
+    int rc = replay_prepare(c, p, *c->replay, leaf_begin, leaf_end);
     if (rc != PM_OK) free_replay(c);
     return rc;
 }
+
+int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) { return pm_replay_prepare_range(c, p, -1, -1); }
 
 int pm_replay_run(pm_ctx* c) {
     if (!c) return PM_ERR_ARG;
@@ -475,6 +483,68 @@ int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* l
     if (rc == PM_OK) rc = pm_replay_run(c);
     if (rc == PM_OK) rc = pm_replay_format(c, aligned, text, length);
     return rc;
+}
+
+int pm_fasta_multi(const pm_panmat* p, int aligned, const int* devices, int num_devices, char** text,
+                   int64_t* length, char* err, int64_t err_len) {
+    auto set_err = [&](const std::string& e) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+    };
+    if (!p || !devices || num_devices < 1 || !text || !length || p->num_nodes < 1 || !p->child_offsets) {
+        set_err("bad arguments");
+        return PM_ERR_ARG;
+    }
+    int64_t L = 0;
+    for (int32_t i = 0; i < p->num_nodes; ++i) L += p->child_offsets[i] == p->child_offsets[i + 1];
+    // leaves split into contiguous ranges, one host thread + context per device; the
+    // ranges' texts concatenate to the single-device text
+    const int G = num_devices;
+    std::vector<char*> part(G, nullptr);
+    std::vector<int64_t> plen(G, 0);
+    std::vector<int> rc(G, PM_OK);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g]() {
+            const int64_t lo = L * g / G, hi = L * (g + 1) / G;
+            if (hi == lo) return;   // more devices than leaves
+            pm_ctx* c = nullptr;
+            if ((rc[g] = pm_create(devices[g], &c)) != PM_OK) {
+                msg[g] = "no HIP device " + std::to_string(devices[g]);
+                return;
+            }
+            rc[g] = pm_replay_prepare_range(c, p, lo, hi);
+            if (rc[g] == PM_OK) rc[g] = pm_replay_run(c);
+            if (rc[g] == PM_OK) rc[g] = pm_replay_format(c, aligned, &part[g], &plen[g]);
+            if (rc[g] != PM_OK) msg[g] = pm_last_error(c);
+            pm_destroy(c);
+        });
+    for (auto& t : th) t.join();
+    int64_t total = 0;
+    for (int g = 0; g < G; ++g) {
+        if (rc[g] != PM_OK) {
+            for (char* x : part) std::free(x);
+            set_err(msg[g]);
+            return rc[g];
+        }
+        total += plen[g];
+    }
+    char* out = static_cast<char*>(std::malloc((size_t)total + 1));
+    if (!out) {
+        for (char* x : part) std::free(x);
+        set_err("FASTA text");
+        return PM_ERR_OOM;
+    }
+    int64_t at = 0;
+    for (int g = 0; g < G; ++g) {
+        if (plen[g]) std::memcpy(out + at, part[g], (size_t)plen[g]);
+        at += plen[g];
+        std::free(part[g]);
+    }
+    out[total] = 0;
+    *text = out;
+    *length = total;
+    return PM_OK;
 }
 
 }  // extern "C"

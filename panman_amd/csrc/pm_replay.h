@@ -51,6 +51,7 @@ struct ReplayState {
 
 // Flatten a PanMAT for the GPU (canonical columns, per-node edits, per-leaf block state)
 // and upload it; the rows are produced by launch_replay(c, r.dev).
-int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r);
+// Leaves [leaf_begin, leaf_end) of the PanMAT's leaves in node-id order (-1, -1: all).
+int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin = -1, int64_t leaf_end = -1);
 
 }  // namespace pm

@@ -31,6 +31,13 @@ def test_help_and_unknown_commands(tmp_path):
     assert r.returncode != 0 and "newick string not provided" in r.stderr
 
 
+def test_backend_and_gpus_arguments(tmp_path):
+    r = _run(["--backend", "cpu", "-I", "x.panman"], tmp_path)
+    assert r.returncode == 1 and "GPU only" in r.stderr
+    r = _run(["--gpus", "0", "-I", "x.panman"], tmp_path)
+    assert r.returncode == 1 and "--gpus" in r.stderr
+
+
 def test_newick_to_info_file_and_stdout(tmp_path):
     rng = np.random.default_rng(3)
     off, idx, root = random_tree(25, rng, max_children=3)

@@ -119,3 +119,37 @@ def test_c5_like_panmat_vs_oracle(engine, oracle, aligned):
     from panman_amd.synth import c5_panmat
     pm = c5_panmat(leaves=120, blocks=40, mean_len=1500, seed=11)
     assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_fasta_multi_device_matches_single(engine, aligned):
+    """Leaf-sharded FASTA: several contexts (here on one GPU) give the
+    single-context text byte for byte, including more shards than leaves."""
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=37, blocks=12, mean_len=900, seed=5)
+    want = engine.fasta(pm, aligned)
+    for devices in ([0, 0], [0, 0, 0], [0] * 50):
+        assert panman_amd.fasta_multi(pm, aligned, devices) == want
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_msa_build_multi_device_matches_single(tmp_path, mode):
+    """Column-sharded MSA construction writes the same file as the one-context build."""
+    rng = np.random.default_rng(300 + mode)
+    off, idx, root = random_tree(80, rng, max_children=5)
+    names = names_for(off)
+    nwk = to_newick(off, idx, root, names)
+    base = rng.choice(list("ACGT"), size=1999)
+    rows = {}
+    for i in range(len(names)):
+        if off[i] == off[i + 1]:
+            s = base.copy()
+            f = rng.random(1999) < 0.08
+            s[f] = rng.choice(list("ACGTRN-"), size=f.sum())
+            rows[names[i]] = "".join(s)
+    msa = "".join(f">{k}\n{v}\n" for k, v in rows.items())
+    ref = next(iter(rows)) if mode == panman_amd.MODE_SANKOFF else ""
+    one, many = str(tmp_path / "one.panman"), str(tmp_path / "many.panman")
+    panman_amd.msa_to_panman(nwk, msa, one, ref, mode)
+    panman_amd.msa_to_panman(nwk, msa, many, ref, mode, devices=[0, 0, 0])
+    assert open(one, "rb").read() == open(many, "rb").read()
