@@ -90,10 +90,15 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_GRAPH   (default 0): pm_run captures its launch sequence (per-level kernels,
  *                  memsets) into a hipGraph once and replays it while the tree, columns,
  *                  mode and buffers stay the same; kernel_times then reports the whole run
- *                  as class 4. */
+ *                  as class 4.
+ *   PM_OPT_CHAINS  (default 0): Fitch passes walk heavy-path chains (one launch per chain
+ *                  rank, ~log2 N of them) instead of one launch per tree level
+ *                  (experimental: each chain step is a serial chain of dependent loads, so
+ *                  it is slower than the level kernels on MI355X so far). */
 #define PM_OPT_FUSED 1
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
+#define PM_OPT_CHAINS 4
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

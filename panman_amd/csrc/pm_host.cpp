@@ -66,6 +66,12 @@ void free_tree(DevTree& t) {
     dev_free(t.down_desc_v);
     dev_free(t.tail_desc);
     dev_free(t.tail_desc_v);
+    for (int v = 0; v < 2; ++v) {
+        dev_free(t.up_chain_desc[v]);
+        dev_free(t.down_chain_desc[v]);
+        dev_free(t.up_chain_off[v]);
+        dev_free(t.down_chain_off[v]);
+    }
     dev_free(t.vleaf);
     dev_free(t.rg_node_off);
     dev_free(t.rg_node_dense);
@@ -184,7 +190,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
-    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents,
+    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->chains,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
                               (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals,
@@ -508,6 +514,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->virtual_leaf_parents = value != 0;
         return PM_OK;
     }
+    if (option == PM_OPT_CHAINS) {
+        c->chains = value != 0;
+        return PM_OK;
+    }
     if (option == PM_OPT_GRAPH) {
         c->use_graph = value != 0;
         if (!c->use_graph) drop_graph(c);
@@ -621,10 +631,41 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 
+    // heavy child first: the internal child with the largest subtree (a materialised one
+    // on ties) leads its parent's child list, so it is the next node down the parent's
+    // chain in both the plain and the virtual-leaf-parent form (children order is free:
+    // every pass combines children commutatively and records are sorted on fetch)
+    auto is_virtual = [&](int32_t d) {
+        if (ht.internal_id[d] == t->root) return false;
+        const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
+        if (deg > 2) return false;
+        for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e)
+            if (ht.child_enc[e] >= 0) return false;
+        return true;
+    };
+    {
+        std::vector<int64_t> sub(N, 1);
+        for (int32_t k = N - 1; k >= 0; --k) {
+            const int32_t u = bfs[k];
+            for (int32_t e = off[u]; e < off[u + 1]; ++e) sub[u] += sub[idx[e]];
+        }
+        for (int32_t d = 0; d < I; ++d) {
+            int32_t best = -1;
+            int64_t best_key = -1;
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                const int32_t x = ht.child_enc[e];
+                if (x < 0) continue;
+                const int64_t key = sub[ht.internal_id[x]] * 2 + (is_virtual(x) ? 0 : 1);
+                if (key > best_key) { best_key = key; best = e; }
+            }
+            if (best > ht.child_off[d]) std::swap(ht.child_enc[best], ht.child_enc[ht.child_off[d]]);
+        }
+    }
+
     // virtual leaf-parents (Fitch level kernels)
     std::vector<int32_t> child_enc_v(ht.child_enc), up_order_v, down_order_v, vleaf((size_t)I * 4, -1);
+    std::vector<uint8_t> virt(I, 0);
     {
-        std::vector<uint8_t> virt(I, 0);
         for (int32_t d = 0; d < I; ++d) {
             if (ht.internal_id[d] == t->root) continue;
             const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
@@ -701,6 +742,64 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             }
         return tail;
     };
+    // heavy-path chains over the materialised nodes of each form
+    std::vector<NodeDesc> up_chain_desc[2], down_chain_desc[2];
+    std::vector<int32_t> up_chain_off[2], down_chain_off[2];
+    for (int v = 0; v < 2; ++v) {
+        const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
+        auto mat = [&](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
+        std::vector<int32_t> first(I, -1);   // next node down the chain
+        std::vector<uint8_t> live(I, 0);
+        for (int32_t d = 0; d < I; ++d) {
+            live[d] = v ? !virt[d] : 1;
+            if (mat(enc[ht.child_off[d]])) first[d] = enc[ht.child_off[d]];
+        }
+        std::vector<int32_t> rank(I, 0);
+        for (int32_t k = N - 1; k >= 0; --k) {
+            const int32_t u = bfs[k];
+            const int32_t d = ht.dense_of[u];
+            if (d < 0 || !live[d]) continue;
+            int32_t r = first[d] >= 0 ? rank[first[d]] : 0;
+            for (int32_t e = ht.child_off[d] + 1; e < ht.child_off[d + 1]; ++e)
+                if (mat(enc[e])) r = std::max(r, rank[enc[e]] + 1);
+            rank[d] = r;
+        }
+        struct Chain { int32_t bottom, top, len, rank; };
+        std::vector<Chain> chains;
+        for (int32_t d = 0; d < I; ++d) {
+            if (!live[d] || first[d] >= 0) continue;   // chains start at their bottom node
+            int32_t cur = d, len = 1;
+            while (parent_dense[cur] >= 0 && first[parent_dense[cur]] == cur) {
+                cur = parent_dense[cur];
+                ++len;
+            }
+            chains.push_back({d, cur, len, rank[cur]});
+        }
+        int32_t R = 0;
+        for (const Chain& ch : chains) R = std::max(R, ch.rank + 1);
+        auto by = [](bool asc) {
+            return [asc](const Chain& x, const Chain& y) {
+                if (x.rank != y.rank) return asc ? x.rank < y.rank : x.rank > y.rank;
+                return x.len > y.len;   // long chains dispatched first within a launch
+            };
+        };
+        for (int dir = 0; dir < 2; ++dir) {   // 0: up (bottom-up nodes), 1: down (top-down)
+            std::sort(chains.begin(), chains.end(), by(dir == 0));
+            std::vector<int32_t> nodes, coff{0}, roff(R + 1, 0);
+            for (const Chain& ch : chains) {
+                const size_t at = nodes.size();
+                for (int32_t cur = ch.bottom, k = 0; k < ch.len; ++k, cur = parent_dense[cur]) nodes.push_back(cur);
+                if (dir == 1) std::reverse(nodes.begin() + at, nodes.end());
+                coff.push_back((int32_t)nodes.size());
+                ++roff[(dir == 0 ? ch.rank : R - 1 - ch.rank) + 1];
+            }
+            for (int32_t r = 0; r < R; ++r) roff[r + 1] += roff[r];
+            (dir == 0 ? up_chain_desc[v] : down_chain_desc[v]) = make_desc(nodes, enc);
+            (dir == 0 ? up_chain_off[v] : down_chain_off[v]) = coff;
+            (dir == 0 ? ht.up_rank_off[v] : ht.down_rank_off[v]) = roff;
+        }
+    }
+
     const std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
     const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
@@ -736,6 +835,14 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_desc_v, up_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_chain_desc[0], up_chain_desc[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_chain_desc[1], up_chain_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_chain_desc[0], down_chain_desc[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_chain_desc[1], down_chain_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_chain_off[0], up_chain_off[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_chain_off[1], up_chain_off[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_chain_off[0], down_chain_off[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_chain_off[1], down_chain_off[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||

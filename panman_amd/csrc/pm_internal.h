@@ -78,6 +78,13 @@ struct DevTree {
     int32_t* vleaf = nullptr;
     TailDesc* tail_desc = nullptr;     // tails over child_enc
     TailDesc* tail_desc_v = nullptr;   // tails over child_enc_v
+    // heavy-path chains ([0] over child_enc, [1] over child_enc_v): the materialised
+    // internal nodes split into chains, each node's first child being the next node down
+    // its chain; descriptors bottom-up (up) / top-down (down), chain c at [off[c], off[c+1])
+    NodeDesc* up_chain_desc[2] = {nullptr, nullptr};
+    NodeDesc* down_chain_desc[2] = {nullptr, nullptr};
+    int32_t* up_chain_off[2] = {nullptr, nullptr};
+    int32_t* down_chain_off[2] = {nullptr, nullptr};
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
     int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
@@ -115,6 +122,9 @@ struct HostTree {
     std::vector<int32_t> down_level_off_v;
     int64_t num_virtual = 0;
     int32_t num_tail = 0, num_tail_v = 0;
+    // chains per rank: up launches rank 0.. (chains of rank r hang only rank < r chains off
+    // their nodes), down launches in the reverse order; [variant][rank + 1] chain offsets
+    std::vector<int32_t> up_rank_off[2], down_rank_off[2];
     std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
     std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
 };
@@ -139,6 +149,7 @@ struct pm_ctx {
     int32_t max_degree = 0;
     bool fused = false;               // Fitch: subtree-region kernels (PM_OPT_FUSED, experimental)
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
+    bool chains = false;              // heavy-path chain kernels instead of per-level ones (PM_OPT_CHAINS)
 
     // column shard
     int64_t num_sites = 0;

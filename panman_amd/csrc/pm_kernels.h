@@ -14,7 +14,9 @@ enum class Mode { kFitch, kSankoff, kBlockFitch };
 
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
-    const NodeDesc* desc;  // Fitch: level items
+    const NodeDesc* desc;  // Fitch: level items (chain kernels: all chains' descriptors)
+    const int32_t* chain_off;  // chain kernels: chain c's descriptors at [chain_off[c], chain_off[c+1])
+    int32_t chain_base;        // first chain of the launch
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;
@@ -337,7 +339,9 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 }
 
 struct DownArgs {
-    const NodeDesc* desc;  // per level item
+    const NodeDesc* desc;  // per level item (chain kernels: all chains' descriptors)
+    const int32_t* chain_off;
+    int32_t chain_base;
     const TailDesc* tail;  // k_tail items
     int32_t count;
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
@@ -596,6 +600,66 @@ __device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* sta
     return true;
 }
 
+// The node's final codes F (code planes) and the sites where it is resolved (pres), from
+// its own set (Fitch: one-hot planes; Sankoff: Z0 / Z1) and its parent's final pc.
+template <Mode M>
+__device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, int64_t word, const uint32_t* own,
+                                              const uint32_t* z1, const uint32_t* pc, uint32_t* F, uint32_t& pres) {
+    if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
+        // One sweep over the 16 planes from code 15 down to 0: "parent code in own set"
+        // (hit), any code present, and the lowest present code in code-plane form.
+        const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
+        uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int v = 15; v >= 0; --v) {
+            const uint32_t o = own[v];
+            const uint32_t is_v = ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) & ((v & 4) ? pc[2] : np[2]) &
+                                  ((v & 8) ? pc[3] : np[3]);
+            hit |= is_v & o;
+            any |= o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
+        }
+        pres = any;   // state 0: subtree absent, skipped (:101-103, :136-138)
+        // root: lowest code of its set; otherwise (and always for blocks, :249-264)
+        // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:98-123)
+        const bool generic = !is_root || M == Mode::kBlockFitch;
+        if (!generic) hit = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
+        if (M == Mode::kBlockFitch && is_root && a.forced) {   // defaultValue (:249-250)
+            const uint4 f = a.forced[word];
+            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
+            pres = ~0u;
+        }
+    } else {
+        uint32_t P[16], fin[16];
+        onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
+        if (is_root) {
+            if (a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
+                const uint4 f = a.forced[word];
+                onehot_from_code(f.x, f.y, f.z, f.w, ~0u, fin);
+            } else {          // argmin, lowest index (:495-507); all-INF -> unresolved
+                lowest_code(own, fin);
+            }
+        } else {
+            uint32_t cand[16], low[16];
+            uint32_t hit = 0;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                hit |= P[v] & own[v];
+                cand[v] = own[v] | (P[v] & z1[v]);
+            }
+            lowest_code(cand, low);
+            const uint32_t live = any_plane(P);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) fin[v] = ((P[v] & hit) | (low[v] & ~hit)) & live;
+        }
+        pres = any_plane(fin);
+        code_from_onehot(fin, F[0], F[1], F[2], F[3]);
+    }
+}
+
 // Pre-order + assignment for one node and its leaf children.  Final state:
 //   Fitch   (src/fitchSankoff.cpp:96-129): root -> lowest code of its set; otherwise
 //           parent if parent & own, else lowest(own); own == 0 stays unresolved.
@@ -742,6 +806,77 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
     if (lane == 0) stage_cnt[wave] = 0;
     kid_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
+}
+
+// Pre-order + assignment along heavy-path chains: wave = (chain, tile), walking the
+// chain top-down with the parent's final carried in registers (only the chain top reads
+// its parent's final, written by an earlier launch).  Each step is k_down's body; the
+// records of successive steps share the wave's LDS stage, flushed with one global atomic
+// once it is half full (a step that overflows the stage is redone straight into global).
+template <Mode M, bool AP>
+__global__ __launch_bounds__(kBlock) void k_down_chain(DownArgs a) {
+    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    __shared__ uint32_t stage_cnt[kWavesPerBlock];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    if (item >= a.count) return;
+    if (lane == 0) stage_cnt[wave] = 0;
+    const int32_t chain = a.chain_base + item;
+    const int32_t s0 = a.chain_off[chain], s1 = a.chain_off[chain + 1];
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint32_t valid = valid_mask(a, word);
+    uint32_t pc[4];
+    {
+        const int32_t top_parent = a.desc[s0].parent;
+        const uint4 q = top_parent < 0 ? a.cons[word] : a.finals[(size_t)top_parent * a.wpad + word];
+        pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
+    }
+    uint32_t flushes = 0;
+    for (int32_t k = s0; k < s1; ++k) {
+        const NodeDesc& d = a.desc[k];
+        const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
+        const bool is_root = d.parent < 0;
+        Kid kids[2];
+        kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
+        if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
+        uint32_t own[16], z1[16], F[4], pres;
+        if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
+        else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
+        resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
+        a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
+        if (is_root) {
+            for (int b = 0; b < 32; ++b) {
+                const int64_t site = word * 32 + b;
+                if (site < a.sites)
+                    a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
+            }
+        }
+        const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+        const uint32_t before = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+        node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
+        uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+        if (cnt > kStage) {   // this step overflowed the stage: its records go straight to global
+            const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u + k) % kShards;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], cnt - before);
+            base = __shfl(base, 0, 64);
+            if (lane == 0) stage_cnt[wave] = 0;
+            node_records<M, AP>(a, GlobalSink{a.recs + (size_t)shard * a.shard_cap, (int64_t)base, a.shard_cap,
+                                              &stage_cnt[wave]},
+                                n, e0, e1, kids, word, valid, pc, F, self_diff);
+            if (lane == 0) stage_cnt[wave] = before;
+            cnt = before;
+        }
+        if (cnt > kStage / 2 || (k + 1 == s1 && cnt > 0)) {
+            const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u + 977u * flushes++) % kShards;
+            uint32_t base;
+            pm_mut* out;
+            flush_stage(a, stage[wave], cnt, shard, lane, item, tile, base, out);
+            if (lane == 0) stage_cnt[wave] = 0;
+        }
+        pc[0] = F[0]; pc[1] = F[1]; pc[2] = F[2]; pc[3] = F[3];
+    }
 }
 
 }  // namespace pm

@@ -57,12 +57,15 @@ def _random_columns(rng, leaves, sites, absent_frac=0.1, gap=0.2):
     return codes, present
 
 
-VARIANTS = ["virtual", "plain", "regions"]
+VARIANTS = ["virtual", "plain", "regions", "chains", "plain-chains"]
 
 
 def _variant(engine, variant):
+    """virtual / plain: per-level kernels with or without virtual leaf-parents; chains /
+    plain-chains: the same over heavy-path chains; regions: LDS subtree regions."""
     engine.set_fused(variant == "regions")
-    engine.set_virtual(variant == "virtual")
+    engine.set_virtual(variant in ("virtual", "chains"))
+    engine.set_chains(variant in ("chains", "plain-chains"))
 
 
 def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant="virtual"):
