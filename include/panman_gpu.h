@@ -99,6 +99,10 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
 #define PM_OPT_CHAINS 4
+/*   PM_OPT_BANDS   (default 0): Fitch passes in bands of 8 tree levels: one launch per
+ *                  band, a workgroup per (connected piece, tile) with workgroup barriers
+ *                  between the band's levels -- for deep trees (SARS-like ladders). */
+#define PM_OPT_BANDS 5
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

@@ -71,6 +71,10 @@ void free_tree(DevTree& t) {
         dev_free(t.down_chain_desc[v]);
         dev_free(t.up_chain_off[v]);
         dev_free(t.down_chain_off[v]);
+        dev_free(t.up_band_desc[v]);
+        dev_free(t.down_band_desc[v]);
+        dev_free(t.up_band_lvl[v]);
+        dev_free(t.down_band_lvl[v]);
     }
     dev_free(t.vleaf);
     dev_free(t.rg_node_off);
@@ -190,7 +194,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
-    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->chains,
+    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->chains, (uint64_t)c->bands,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
                               (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals,
@@ -514,6 +518,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->virtual_leaf_parents = value != 0;
         return PM_OK;
     }
+    if (option == PM_OPT_BANDS) {
+        c->bands = value != 0;
+        return PM_OK;
+    }
     if (option == PM_OPT_CHAINS) {
         c->chains = value != 0;
         return PM_OK;
@@ -800,6 +808,59 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
     }
 
+    // bands of kBand levels and their connected pieces (see DevTree)
+    std::vector<NodeDesc> up_band_desc[2], down_band_desc[2];
+    std::vector<int32_t> up_band_lvl[2], down_band_lvl[2];
+    for (int v = 0; v < 2; ++v) {
+        const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
+        auto live = [&](int32_t d) { return v ? !virt[d] : true; };
+        for (int dir = 0; dir < 2; ++dir) {   // 0: up (height), 1: down (depth)
+            auto level = [&](int32_t d) {
+                return dir == 0 ? height[ht.internal_id[d]] - 1 : depth[ht.internal_id[d]];
+            };
+            // piece root: parent absent or in another band; pieces gathered by BFS over
+            // same-band children, then their nodes bucketed by level inside the band
+            int32_t B = 0;
+            for (int32_t d = 0; d < I; ++d)
+                if (live(d)) B = std::max(B, level(d) / kBand + 1);
+            std::vector<std::vector<int32_t>> roots(B);
+            for (int32_t k = 0; k < N; ++k) {
+                const int32_t d = ht.dense_of[bfs[k]];
+                if (d < 0 || !live(d)) continue;
+                const int32_t p = parent_dense[d];
+                if (p < 0 || level(p) / kBand != level(d) / kBand) roots[level(d) / kBand].push_back(d);
+            }
+            std::vector<int32_t> nodes, lvl, boff{0}, stack, mine;
+            for (int32_t b = 0; b < B; ++b) {
+                const int32_t band = dir == 0 ? b : b;   // up: band 0 first (leaves); down: root band first
+                for (int32_t r : roots[band]) {
+                    mine.clear();
+                    stack.assign(1, r);
+                    while (!stack.empty()) {
+                        const int32_t d = stack.back();
+                        stack.pop_back();
+                        mine.push_back(d);
+                        for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                            const int32_t x = enc[e];
+                            if (x >= 0 && !(x & kVirtualBit) && level(x) / kBand == band) stack.push_back(x);
+                        }
+                    }
+                    std::stable_sort(mine.begin(), mine.end(), [&](int32_t x, int32_t y) { return level(x) < level(y); });
+                    size_t at = 0;
+                    for (int j = 0; j <= kBand; ++j) {
+                        while (at < mine.size() && level(mine[at]) - band * kBand < j) ++at;
+                        lvl.push_back((int32_t)(nodes.size() + at));
+                    }
+                    nodes.insert(nodes.end(), mine.begin(), mine.end());
+                }
+                boff.push_back((int32_t)(lvl.size() / (kBand + 1)));
+            }
+            (dir == 0 ? up_band_desc[v] : down_band_desc[v]) = make_desc(nodes, enc);
+            (dir == 0 ? up_band_lvl[v] : down_band_lvl[v]) = lvl;
+            (dir == 0 ? ht.up_band_off[v] : ht.down_band_off[v]) = boff;
+        }
+    }
+
     const std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
     const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
@@ -843,6 +904,14 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_chain_off[1], up_chain_off[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.down_chain_off[0], down_chain_off[0], c->stream)) != hipSuccess ||
         (e = upload(&dt.down_chain_off[1], down_chain_off[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_band_desc[0], up_band_desc[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_band_desc[1], up_band_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_band_desc[0], down_band_desc[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_band_desc[1], down_band_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_band_lvl[0], up_band_lvl[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_band_lvl[1], up_band_lvl[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_band_lvl[0], down_band_lvl[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_band_lvl[1], down_band_lvl[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||

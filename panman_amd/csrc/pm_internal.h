@@ -30,6 +30,8 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
 constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
+constexpr int kBand = 8;          // levels per band (PM_OPT_BANDS)
+constexpr int kBandWaves = 8;     // waves per band workgroup
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
@@ -85,6 +87,14 @@ struct DevTree {
     NodeDesc* down_chain_desc[2] = {nullptr, nullptr};
     int32_t* up_chain_off[2] = {nullptr, nullptr};
     int32_t* down_chain_off[2] = {nullptr, nullptr};
+    // height / depth bands of kBand levels: each band's connected pieces, one workgroup
+    // per (piece, tile) walking the piece's levels with workgroup barriers in between;
+    // descriptors piece by piece, level by level; piece p's level j at
+    // [lvl[p*(kBand+1)+j], lvl[p*(kBand+1)+j+1])
+    NodeDesc* up_band_desc[2] = {nullptr, nullptr};
+    NodeDesc* down_band_desc[2] = {nullptr, nullptr};
+    int32_t* up_band_lvl[2] = {nullptr, nullptr};
+    int32_t* down_band_lvl[2] = {nullptr, nullptr};
     // subtree regions for the fused Fitch kernels (pm_fused.hip)
     int32_t num_regions = 0;
     int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
@@ -125,6 +135,9 @@ struct HostTree {
     // chains per rank: up launches rank 0.. (chains of rank r hang only rank < r chains off
     // their nodes), down launches in the reverse order; [variant][rank + 1] chain offsets
     std::vector<int32_t> up_rank_off[2], down_rank_off[2];
+    // pieces per band: [variant][band + 1] piece offsets (up: bands by height from the
+    // leaves, down: by depth from the root)
+    std::vector<int32_t> up_band_off[2], down_band_off[2];
     std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
     std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
 };
@@ -150,6 +163,7 @@ struct pm_ctx {
     bool fused = false;               // Fitch: subtree-region kernels (PM_OPT_FUSED, experimental)
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
     bool chains = false;              // heavy-path chain kernels instead of per-level ones (PM_OPT_CHAINS)
+    bool bands = false;               // banded level kernels (PM_OPT_BANDS)
 
     // column shard
     int64_t num_sites = 0;

@@ -879,4 +879,82 @@ __global__ __launch_bounds__(kBlock) void k_down_chain(DownArgs a) {
     }
 }
 
+// Pre-order + assignment over a band of kBand depth levels: workgroup = (piece, tile),
+// its waves share each level's nodes and meet at a workgroup barrier before the next level
+// (finals written by one wave are read by another wave of the same workgroup, so the
+// barrier's workgroup-scope ordering suffices).  Each node is k_down's body; records go
+// through the wave's LDS stage as in k_down_chain.
+template <Mode M, bool AP>
+__global__ __launch_bounds__(kBandWaves * kWave) void k_down_band(DownArgs a) {
+    __shared__ pm_mut stage[kBandWaves][kStage];
+    __shared__ uint32_t stage_cnt[kBandWaves];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (lane == 0) stage_cnt[wave] = 0;
+    const int32_t piece = a.chain_base + blockIdx.x;
+    const int32_t* lv = a.chain_off + (size_t)piece * (kBand + 1);
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint32_t valid = valid_mask(a, word);
+    uint32_t flushes = 0;
+    for (int j = 0; j < kBand; ++j) {
+        const int32_t lb = lv[j], le = lv[j + 1];
+        for (int32_t k = lb + wave; k < le; k += kBandWaves) {
+            const NodeDesc& d = a.desc[k];
+            const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
+            const bool is_root = d.parent < 0;
+            uint32_t pc[4];
+            {
+                const uint4 q = is_root ? a.cons[word] : a.finals[(size_t)d.parent * a.wpad + word];
+                pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
+            }
+            Kid kids[2];
+            kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
+            if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
+            uint32_t own[16], z1[16], F[4], pres;
+            if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
+            else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
+            resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
+            a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
+            if (is_root) {
+                for (int b = 0; b < 32; ++b) {
+                    const int64_t site = word * 32 + b;
+                    if (site < a.sites)
+                        a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
+                }
+            }
+            const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+            const uint32_t before = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+            node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
+            uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+            if (cnt > kStage) {   // this node overflowed the stage: its records go straight to global
+                const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + k) % kShards;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], cnt - before);
+                base = __shfl(base, 0, 64);
+                if (lane == 0) stage_cnt[wave] = 0;
+                node_records<M, AP>(a, GlobalSink{a.recs + (size_t)shard * a.shard_cap, (int64_t)base, a.shard_cap,
+                                                  &stage_cnt[wave]},
+                                    n, e0, e1, kids, word, valid, pc, F, self_diff);
+                if (lane == 0) stage_cnt[wave] = before;
+                cnt = before;
+            }
+            if (cnt > kStage / 2) {
+                const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + wave * 131u + 977u * flushes++) % kShards;
+                uint32_t base;
+                pm_mut* out;
+                flush_stage(a, stage[wave], cnt, shard, lane, piece, tile, base, out);
+                if (lane == 0) stage_cnt[wave] = 0;
+            }
+        }
+        __syncthreads();
+    }
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+    if (cnt > 0) {
+        const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + wave * 131u + 977u * flushes) % kShards;
+        uint32_t base;
+        pm_mut* out;
+        flush_stage(a, stage[wave], cnt, shard, lane, piece, tile, base, out);
+    }
+}
+
 }  // namespace pm
