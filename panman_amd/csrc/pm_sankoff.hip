@@ -95,6 +95,135 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1);
 }
 
+// Z0 of one child (leaf, virtual leaf-parent or record), as k_sankoff_up reads it.
+template <class Args>
+__device__ __forceinline__ void child_z0(const Args& a, int32_t c, int32_t l0, int32_t l1, int tile, int lane,
+                                         int64_t word, uint32_t* z) {
+    if (c >= 0 && (c & kVirtualBit)) {
+        uint32_t x[16];
+        leaf_set16(a, l0, word, z);
+        if (l1 >= 0) {
+            leaf_set16(a, l1, word, x);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) z[v] |= x[v];
+        }
+    } else if (c >= 0) {
+        load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);
+    } else {
+        leaf_set16(a, -c - 1, word, z);
+    }
+}
+
+template <int B>
+__device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& finite, const uint32_t* z) {
+    finite |= any_plane(z);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t x = z[v];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint32_t t = cnt[v][b] & x;
+            cnt[v][b] ^= x;
+            x = t;
+        }
+    }
+}
+
+// Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
+// to its 4 waves (64 encodings per vector load, two children fetched before either is
+// counted); the waves' bit-sliced counters are summed through LDS (the sum of the
+// per-wave counts is the node's count: src/fitchSankoff.cpp:391-402 is a sum over
+// children), then Z0 / Z1 as in k_sankoff_up.
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
+    __shared__ uint32_t part[16 * B + 1][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const NodeDesc& d = a.desc[blockIdx.x];
+    const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
+    const int tile = blockIdx.y;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    uint32_t cnt[16][B];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+#pragma unroll
+        for (int b = 0; b < B; ++b) cnt[v][b] = 0;
+    uint32_t finite = 0;
+    for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
+        const int32_t my = base + kWavesPerBlock * lane;
+        const int32_t enc = my < e1 ? a.child_enc[my] : 0;
+        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+                                                                   : make_int4(-1, -1, -1, -1);
+        const int cntc = min(kWave, (e1 - base + kWavesPerBlock - 1) / kWavesPerBlock);
+        for (int k = 0; k < cntc; k += 2) {
+            uint32_t z0[16], z1[16];
+            const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
+            child_z0(a, c0, __builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), tile, lane, word, z0);
+            const bool two = k + 1 < cntc;
+            if (two) {
+                const int32_t c1 = __builtin_amdgcn_readlane(enc, k + 1);
+                child_z0(a, c1, __builtin_amdgcn_readlane(vl.x, k + 1), __builtin_amdgcn_readlane(vl.y, k + 1), tile,
+                         lane, word, z1);
+            }
+            count_child<B>(cnt, finite, z0);
+            if (two) count_child<B>(cnt, finite, z1);
+        }
+    }
+    // sum the waves' counters into wave 0, one wave at a time through one LDS buffer
+    for (int w = 1; w < kWavesPerBlock; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v)
+#pragma unroll
+                for (int b = 0; b < B; ++b) part[v * B + b][lane] = cnt[v][b];
+            part[16 * B][lane] = finite;
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                uint32_t carry = 0;
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    const uint32_t x = part[v * B + b][lane], y = cnt[v][b];
+                    cnt[v][b] = x ^ y ^ carry;
+                    carry = (x & y) | (carry & (x ^ y));
+                }
+            }
+            finite |= part[16 * B][lane];
+        }
+        __syncthreads();
+    }
+    if (wave != 0) return;
+    uint32_t cand[16], mx[B];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cand[v] = ~0u;
+#pragma unroll
+    for (int b = B - 1; b >= 0; --b) {
+        uint32_t hit = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) hit |= cand[v] & cnt[v][b];
+        mx[b] = hit;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) cand[v] &= cnt[v][b] | ~hit;
+    }
+    uint32_t mm1[B], borrow = ~0u;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        mm1[b] = mx[b] ^ borrow;
+        borrow &= ~mx[b];
+    }
+    uint32_t z0[16], z1[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t eq = finite;
+#pragma unroll
+        for (int b = 0; b < B; ++b) eq &= ~(cnt[v][b] ^ mm1[b]);
+        z0[v] = cand[v] & finite;
+        z1[v] = eq;
+    }
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1);
+}
+
 }  // namespace
 
 hipError_t launch_sankoff(pm_ctx* c, bool block) {
@@ -134,11 +263,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             if (e == b) continue;
             up.desc = up_desc + b;
             up.count = e - b;
-            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles), wide(up.count, tiles);
             timer_begin(c, 0);
             if (k == 0) hipLaunchKernelGGL(k_sankoff_up<2>, grid, dim3(kBlock), 0, c->stream, up);
-            else if (k == 1) hipLaunchKernelGGL(k_sankoff_up<4>, grid, dim3(kBlock), 0, c->stream, up);
-            else if (k == 2) hipLaunchKernelGGL(k_sankoff_up<8>, grid, dim3(kBlock), 0, c->stream, up);
+            else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
+            else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL(k_sankoff_up<12>, grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
