@@ -633,30 +633,32 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
             pres = ~0u;
         }
     } else {
-        uint32_t P[16], fin[16];
-        onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
-        if (is_root) {
-            if (a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
-                const uint4 f = a.forced[word];
-                onehot_from_code(f.x, f.y, f.z, f.w, ~0u, fin);
-            } else {          // argmin, lowest index (:495-507); all-INF -> unresolved
-                lowest_code(own, fin);
-            }
+        if (is_root && a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
+            const uint4 f = a.forced[word];
+            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
+            pres = ~0u;
         } else {
-            uint32_t cand[16], low[16];
-            uint32_t hit = 0;
+            // One sweep from code 15 down to 0 in code-plane form.  Root: argmin = lowest
+            // optimal code (:495-507).  Otherwise the parent's code if optimal, else the
+            // lowest of Z0 and (the parent's code if it is one above optimal, Z1)
+            // (:513-530); an all-INF subtree (Z0 = Z1 = 0) stays unresolved.
+            const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
+            uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                hit |= P[v] & own[v];
-                cand[v] = own[v] | (P[v] & z1[v]);
+            for (int v = 15; v >= 0; --v) {
+                const uint32_t is_v = is_root ? 0u
+                                              : ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) &
+                                                    ((v & 4) ? pc[2] : np[2]) & ((v & 8) ? pc[3] : np[3]);
+                const uint32_t o = own[v] | (is_v & z1[v]);
+                hit |= is_v & own[v];
+                any |= o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
             }
-            lowest_code(cand, low);
-            const uint32_t live = any_plane(P);
 #pragma unroll
-            for (int v = 0; v < 16; ++v) fin[v] = ((P[v] & hit) | (low[v] & ~hit)) & live;
+            for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
+            pres = any;
         }
-        pres = any_plane(fin);
-        code_from_onehot(fin, F[0], F[1], F[2], F[3]);
     }
 }
 
@@ -727,30 +729,32 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
             pres = ~0u;
         }
     } else {
-        uint32_t P[16], fin[16];
-        onehot_from_code(pc[0], pc[1], pc[2], pc[3], ~0u, P);
-        if (is_root) {
-            if (a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
-                const uint4 f = a.forced[word];
-                onehot_from_code(f.x, f.y, f.z, f.w, ~0u, fin);
-            } else {          // argmin, lowest index (:495-507); all-INF -> unresolved
-                lowest_code(own, fin);
-            }
+        if (is_root && a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
+            const uint4 f = a.forced[word];
+            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
+            pres = ~0u;
         } else {
-            uint32_t cand[16], low[16];
-            uint32_t hit = 0;
+            // One sweep from code 15 down to 0 in code-plane form.  Root: argmin = lowest
+            // optimal code (:495-507).  Otherwise the parent's code if optimal, else the
+            // lowest of Z0 and (the parent's code if it is one above optimal, Z1)
+            // (:513-530); an all-INF subtree (Z0 = Z1 = 0) stays unresolved.
+            const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
+            uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                hit |= P[v] & own[v];
-                cand[v] = own[v] | (P[v] & z1[v]);
+            for (int v = 15; v >= 0; --v) {
+                const uint32_t is_v = is_root ? 0u
+                                              : ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) &
+                                                    ((v & 4) ? pc[2] : np[2]) & ((v & 8) ? pc[3] : np[3]);
+                const uint32_t o = own[v] | (is_v & z1[v]);
+                hit |= is_v & own[v];
+                any |= o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
             }
-            lowest_code(cand, low);
-            const uint32_t live = any_plane(P);
 #pragma unroll
-            for (int v = 0; v < 16; ++v) fin[v] = ((P[v] & hit) | (low[v] & ~hit)) & live;
+            for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
+            pres = any;
         }
-        pres = any_plane(fin);
-        code_from_onehot(fin, F[0], F[1], F[2], F[3]);
     }
     a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
 
