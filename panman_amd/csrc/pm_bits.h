@@ -43,6 +43,39 @@ __device__ __forceinline__ void lowest_code(const uint32_t* s, uint32_t* out) {
     }
 }
 
+// bitwise select, bit by bit: t ? a : b (one v_bfi_b32)
+__device__ __forceinline__ uint32_t bsel(uint32_t t, uint32_t a, uint32_t b) { return (t & a) | (~t & b); }
+
+// Plane c of a 16-plane set, site by site (c in 4 code planes): a 16:1 multiplexer.
+__device__ __forceinline__ uint32_t plane_at(const uint32_t* s, const uint32_t* c) {
+    uint32_t m8[8], m4[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m8[k] = bsel(c[0], s[2 * k + 1], s[2 * k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m4[k] = bsel(c[1], m8[2 * k + 1], m8[2 * k]);
+    return bsel(c[3], bsel(c[2], m4[3], m4[2]), bsel(c[2], m4[1], m4[0]));
+}
+
+// Lowest code of each site's set in code-plane form (0 for an empty set) by a binary
+// search from the top code bit; returns the sites with a non-empty set.
+__device__ __forceinline__ uint32_t lowest_code_planes(const uint32_t* s, uint32_t* c) {
+    const uint32_t l8 = s[0] | s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7];
+    uint32_t h[8], q[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = bsel(l8, s[k], s[8 + k]);
+    const uint32_t l4 = h[0] | h[1] | h[2] | h[3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = bsel(l4, h[k], h[4 + k]);
+    const uint32_t l2 = q[0] | q[1];
+    const uint32_t r0 = bsel(l2, q[0], q[2]), r1 = bsel(l2, q[1], q[3]);
+    const uint32_t any = r0 | r1;
+    c[0] = ~r0 & any;
+    c[1] = ~l2 & any;
+    c[2] = ~l4 & any;
+    c[3] = ~l8 & any;
+    return any;
+}
+
 __device__ __forceinline__ uint32_t any_plane(const uint32_t* s) {
     uint32_t r = 0;
 #pragma unroll

@@ -24,25 +24,26 @@ namespace {
 // (src/fitchSankoff.cpp:39-55); the first two children's loads are independent and issued
 // back to back.
 template <bool AP>
-__global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
+__global__ __launch_bounds__(kBlock, AP ? 6 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
     const NodeDesc& d = a.desc[item];
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
-    uint32_t both[16], either[16];
+    uint32_t both[16], either[16], vd = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either);
+    fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
     if (e1 - e0 > 1)
-        fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either);
+        fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
     for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-        fold_child<AP>(a, c, vl, tile, lane, word, both, either);
+        fold_child<AP>(a, c, vl, tile, lane, word, both, either, vd);
     }
     // AND if non-empty, else OR (src/fitchSankoff.cpp:48-55)
     const uint32_t nz = any_plane(both);
@@ -53,7 +54,9 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up(UpArgs a) {
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
+    // dirty lanes: complex, or a leaf-parent child's leaves disagree; every lane when some
+    // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
+    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both, !AP || vd != 0u);
 #ifdef PM_EXP_COUNT_COMPLEX
     {
         uint32_t one = 0, two = 0;
@@ -113,7 +116,7 @@ __device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, in
     }
 }
 
-__device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* both, uint32_t* either) {
+__device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* both, uint32_t* either, uint32_t& vd) {
     uint32_t x[16];
     if (c >= 0 && !(c & kVirtualBit) && f.complex_lane) {
 #pragma unroll
@@ -124,6 +127,7 @@ __device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* b
 #pragma unroll
         for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
         if (c >= 0 && (c & kVirtualBit)) {
+            vd |= f.w[9] & ((f.w[0] ^ f.w[5]) | (f.w[1] ^ f.w[6]) | (f.w[2] ^ f.w[7]) | (f.w[3] ^ f.w[8]));
             const LoHi u = lohi_of(f.w[5], f.w[6], f.w[7], f.w[8], f.w[9]);
 #pragma unroll
             for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];
@@ -138,14 +142,16 @@ __device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* b
 
 template <bool AP>
 __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
-    __shared__ uint32_t part[kWavesPerBlock - 1][32][kWave];
+    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const NodeDesc& d = a.desc[blockIdx.x];
+    int32_t item;
+    int tile;
+    block_item(a.tiles, item, tile);
+    const NodeDesc& d = a.desc[item];
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
-    uint32_t both[16], either[16];
+    uint32_t both[16], either[16], vd = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
     for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
@@ -167,8 +173,8 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
                                           __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1);
                 up_fetch<AP>(a, c1, v1, tile, lane, word, f1);
             }
-            up_fold(c0, f0, both, either);
-            if (two) up_fold(c1, f1, both, either);
+            up_fold(c0, f0, both, either, vd);
+            if (two) up_fold(c1, f1, both, either, vd);
         }
     }
     if (wave > 0) {
@@ -177,16 +183,19 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
             part[wave - 1][v][lane] = both[v];
             part[wave - 1][16 + v][lane] = either[v];
         }
+        part[wave - 1][32][lane] = vd;
     }
     __syncthreads();
     if (wave > 0) return;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock - 1; ++w)
+    for (int w = 0; w < kWavesPerBlock - 1; ++w) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             both[v] &= part[w][v][lane];
             either[v] |= part[w][16 + v][lane];
         }
+        vd |= part[w][32][lane];
+    }
     const uint32_t nz = any_plane(both);
 #pragma unroll
     for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
+    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both, !AP || vd != 0u);
 }
 
 // Post-order along heavy-path chains: wave = (chain, tile), walking the chain bottom-up
@@ -214,17 +223,17 @@ __global__ __launch_bounds__(kBlock) void k_fitch_chain_up(UpArgs a) {
     for (int32_t k = s0; k < s1; ++k) {
         const NodeDesc& d = a.desc[k];
         const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-        uint32_t both[16], either[16];
+        uint32_t both[16], either[16], vd = 0;
         if (k > s0) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] = prev[v]; either[v] = prev[v]; }
         } else {
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either);
+            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
         }
         if (e1 - e0 > 1)
-            fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either);
+            fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
         for (int32_t e = e0 + 2; e < e1; e += 2) {   // polytomies: two children in flight
             const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
             const int4 v0 = c0 >= 0 && (c0 & kVirtualBit) ? a.vleaf[c0 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
@@ -240,8 +249,8 @@ __global__ __launch_bounds__(kBlock) void k_fitch_chain_up(UpArgs a) {
                              make_int4(__builtin_amdgcn_readfirstlane(v1.x), __builtin_amdgcn_readfirstlane(v1.y), -1, -1),
                              tile, lane, word, f1);
             }
-            up_fold(c0, f0, both, either);
-            if (two) up_fold(c1, f1, both, either);
+            up_fold(c0, f0, both, either, vd);
+            if (two) up_fold(c1, f1, both, either, vd);
         }
         const uint32_t nz = any_plane(both);
 #pragma unroll
@@ -271,12 +280,12 @@ __global__ __launch_bounds__(kBandWaves * kWave) void k_fitch_band_up(UpArgs a) 
         for (int32_t k = lb + wave; k < le; k += kBandWaves) {
             const NodeDesc& d = a.desc[k];
             const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-            uint32_t both[16], either[16];
+            uint32_t both[16], either[16], vd = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either);
+            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
             if (e1 - e0 > 1)
-                fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either);
+                fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
             for (int32_t e = e0 + 2; e < e1; e += 2) {
                 const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
                 const int4 v0 = c0 >= 0 && (c0 & kVirtualBit) ? a.vleaf[c0 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
@@ -294,8 +303,8 @@ __global__ __launch_bounds__(kBandWaves * kWave) void k_fitch_band_up(UpArgs a) 
                                            -1),
                                  tile, lane, word, f1);
                 }
-                up_fold(c0, f0, both, either);
-                if (two) up_fold(c1, f1, both, either);
+                up_fold(c0, f0, both, either, vd);
+                if (two) up_fold(c1, f1, both, either, vd);
             }
             const uint32_t nz = any_plane(both);
 #pragma unroll
@@ -368,6 +377,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.cons = c->cons;
     up.forced = (c->has_forced && !block) ? c->forced : nullptr;   // refState (M1); blocks force in backward
     up.absent_code0 = false;
+    up.all_present = c->leaves_all_present;
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
@@ -410,7 +420,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         if (m > b) {
             up.desc = up_desc + b;
             up.count = m - b;
-            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+            const dim3 grid = wave_grid(up.count, tiles);
             timer_begin(c, 0);
             if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up<true>, grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL(k_fitch_up<false>, grid, dim3(kBlock), 0, c->stream, up);
@@ -419,7 +429,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         if (e > m) {
             up.desc = up_desc + m;
             up.count = e - m;
-            dim3 grid(up.count, tiles);
+            const dim3 grid = block_grid(up.count, tiles);
             timer_begin(c, 0);
             if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL(k_fitch_up_wide<false>, grid, dim3(kBlock), 0, c->stream, up);
@@ -438,9 +448,9 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.leaf_flag = c->leaf_flag;
     dn.leaf_planes = c->leaf_planes;
     dn.leaf_present = c->leaf_present;
-    dn.sets = reinterpret_cast<const uint4*>(c->sets);
+    dn.sets = reinterpret_cast<uint4*>(c->sets);
     dn.cmask = c->cmask;
-    dn.finals = c->finals;
+    dn.root_final = c->root_final;
     dn.cons = c->cons;
     dn.root_dense = dt.root_dense;
     dn.tiles = tiles;
@@ -453,6 +463,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.root_code = c->root_code;
     dn.forced = (c->has_forced && block) ? c->forced : nullptr;
     dn.absent_code0 = false;
+    dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     if (c->bands) {
         dn.desc = dt.down_band_desc[cv];
@@ -494,7 +505,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
-        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
         const bool ap = c->leaves_all_present;
         if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
@@ -506,7 +517,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
     dn.count = virt ? ht.num_tail_v : ht.num_tail;
     if (dn.count > 0) {
-        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        const dim3 grid = wave_grid(dn.count, tiles);
         const bool ap = c->leaves_all_present;
         timer_begin(c, 1);
         if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);

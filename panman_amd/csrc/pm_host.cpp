@@ -105,6 +105,7 @@ void free_columns(pm_ctx* c) {
     dev_free(c->forced);
     dev_free(c->score);
     dev_free(c->root_code);
+    dev_free(c->root_final);
     c->has_leaves = c->has_sites = c->has_forced = false;
     c->ran = false;
 }
@@ -134,7 +135,8 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
         (e = dev_alloc(&c->cons, (size_t)wpad)) != hipSuccess ||
         (e = dev_alloc(&c->forced, (size_t)wpad)) != hipSuccess ||
         (e = dev_alloc(&c->score, (size_t)sites)) != hipSuccess ||
-        (e = dev_alloc(&c->root_code, (size_t)sites)) != hipSuccess) {
+        (e = dev_alloc(&c->root_code, (size_t)sites)) != hipSuccess ||
+        (e = dev_alloc(&c->root_final, (size_t)wpad)) != hipSuccess) {
         free_columns(c);
         return fail(c, PM_ERR_OOM, std::string("column buffers: ") + hipGetErrorString(e));
     }
@@ -149,7 +151,7 @@ int alloc_work(pm_ctx* c, int mode) {
     const bool fitch = mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH;
     const size_t planes = fitch ? 20 : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
-    const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * 2 * sizeof(uint64_t);
+    const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * kMaskWords * sizeof(uint64_t);
     const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
     hipError_t e;
     if (need_sets > c->sets_bytes) {
@@ -197,7 +199,7 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->chains, (uint64_t)c->bands,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
-                              (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals,
+                              (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals, (uint64_t)(uintptr_t)c->root_final,
                               (uint64_t)(uintptr_t)c->leaf_planes, (uint64_t)(uintptr_t)c->leaf_present,
                               (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
                               (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
@@ -587,7 +589,21 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.num_nodes = N;
     ht.root = t->root;
     ht.dense_of.assign(N, 0);
-    for (int32_t i = 0; i < N; ++i) {
+    // Dense internal indices and leaf ranks in DFS pre-order: a subtree's leaf rows and
+    // records are contiguous, and the nodes of one level (bucketed in dense order below)
+    // run in tree order, so neighbouring waves read neighbouring rows.
+    std::vector<int32_t> dfs;
+    dfs.reserve(N);
+    {
+        std::vector<int32_t> stack{t->root};
+        while (!stack.empty()) {
+            const int32_t u = stack.back();
+            stack.pop_back();
+            dfs.push_back(u);
+            for (int32_t e = off[u + 1] - 1; e >= off[u]; --e) stack.push_back(idx[e]);
+        }
+    }
+    for (const int32_t i : dfs) {
         if (off[i + 1] > off[i]) {
             ht.dense_of[i] = (int32_t)ht.internal_id.size();
             ht.internal_id.push_back(i);
@@ -1132,10 +1148,18 @@ int pm_leaf_codes_fetch(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* out) {
     hipError_t e = dev_alloc(&d, bytes);
     if (e != hipSuccess) return fail(c, PM_ERR_OOM, "fetch staging");
     e = launch_unpack_leaf_codes(c, s0, ns, d);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, c->stream);
+    std::vector<uint8_t> by_rank(bytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(by_rank.data(), d, bytes, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(d);
-    return e == hipSuccess ? PM_OK : hip_fail(c, e, "leaf fetch");
+    if (e != hipSuccess) return hip_fail(c, e, "leaf fetch");
+    // rows by leaf rank (tree order) -> rows in increasing node-id order
+    std::vector<int32_t> ranks(c->dt.num_leaves);
+    std::iota(ranks.begin(), ranks.end(), 0);
+    std::sort(ranks.begin(), ranks.end(), [&](int32_t x, int32_t y) { return c->ht.leaf_id[x] < c->ht.leaf_id[y]; });
+    for (size_t k = 0; k < ranks.size(); ++k)
+        std::memcpy(out + k * ns, by_rank.data() + (size_t)ranks[k] * ns, (size_t)ns);
+    return PM_OK;
 }
 
 int pm_consensus_fetch(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* out) {

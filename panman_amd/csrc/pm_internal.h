@@ -6,7 +6,8 @@
 //   Fitch sets    [I][tile] records: 4 code planes per word + dense 16-plane sets for the
 //                 words holding a multi-code or empty set (pm_kernels.h store_fitch_set)
 //   Sankoff sets  [I][W][32] u32   Z0 (optimal codes) + Z1 (one above optimal) planes
-//   finals        [I][W] uint4     4 code bit-planes of the internal node's final state
+//   finals        the root's in root_final [W] uint4; every other internal node's in its
+//                 record (complex lanes: quad 0 of the lane's slot; others: the record code)
 //   consensus     [W] uint4        root's parent state; forced [W] uint4 (optional)
 //   records       [shards][cap]    pm_mut, sharded write cursors (one atomic per wave)
 // Internal nodes are addressed by a dense index (0..I-1), leaves by their rank among
@@ -30,6 +31,7 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
 constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
+constexpr int kMaskWords = 4;     // record masks per (node, tile): complex, simple, dirty, pad
 constexpr int kBand = 8;          // levels per band (PM_OPT_BANDS)
 constexpr int kBandWaves = 8;     // waves per band workgroup
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
@@ -183,8 +185,9 @@ struct pm_ctx {
     size_t sets_bytes = 0;
     uint64_t* cmask = nullptr;        // Fitch: [I][tile] complex-lane masks
     size_t cmask_bytes = 0;
-    uint4* finals = nullptr;          // [I][W]
+    uint4* finals = nullptr;          // [I][W] synthetic generator scratch (internal sequences)
     size_t finals_bytes = 0;
+    uint4* root_final = nullptr;      // [W] the root's final codes (other finals live in the records)
     pm_mut* recs = nullptr;           // [kShards][shard_cap]
     int64_t shard_cap = 0;
     uint32_t* shard_cnt = nullptr;    // [kShards]

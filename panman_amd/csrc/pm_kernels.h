@@ -12,6 +12,51 @@ namespace pm {
 
 enum class Mode { kFitch, kSankoff, kBlockFitch };
 
+// Level launches number their (item, tile) waves tile-fastest: the tiles of one node run
+// side by side, so its leaf rows, records and parent's records -- contiguous per node --
+// stream as whole rows (DRAM pages, TLB entries) instead of 1-KiB pieces of thousands of
+// rows.  One-wave kernels: wave g = (item g / tiles, tile g % tiles); one-workgroup
+// kernels: workgroup b likewise.  (PM_TILE_FAST=0: the former 2-D grid, tile = blockIdx.y.)
+#ifndef PM_TILE_FAST
+#define PM_TILE_FAST 1
+#endif
+__device__ __forceinline__ void wave_item(int wave, int32_t tiles, int32_t& item, int& tile) {
+#if PM_TILE_FAST
+    const int32_t g = (int32_t)blockIdx.x * kWavesPerBlock + wave;
+    item = g / tiles;
+    tile = g - item * tiles;
+#else
+    item = (int32_t)blockIdx.x * kWavesPerBlock + wave;
+    tile = blockIdx.y;
+#endif
+}
+
+__device__ __forceinline__ void block_item(int32_t tiles, int32_t& item, int& tile) {
+#if PM_TILE_FAST
+    item = (int32_t)blockIdx.x / tiles;
+    tile = (int32_t)blockIdx.x - item * tiles;
+#else
+    item = blockIdx.x;
+    tile = blockIdx.y;
+#endif
+}
+
+// Grids of the level launches (count items x tiles; memory bounds count * tiles far below 2^31).
+inline dim3 wave_grid(int32_t count, int32_t tiles) {
+#if PM_TILE_FAST
+    return dim3((unsigned)(((int64_t)count * tiles + kWavesPerBlock - 1) / kWavesPerBlock));
+#else
+    return dim3((count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+#endif
+}
+inline dim3 block_grid(int32_t count, int32_t tiles) {
+#if PM_TILE_FAST
+    return dim3((unsigned)((int64_t)count * tiles));
+#else
+    return dim3(count, tiles);
+#endif
+}
+
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
     const NodeDesc* desc;  // Fitch: level items (chain kernels: all chains' descriptors)
@@ -32,6 +77,7 @@ struct UpArgs {
     int32_t tiles;
     int64_t wpad;
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
+    bool all_present;      // every leaf present at every site (dirty-lane rules)
 };
 
 // Load 16 planes (quads q0..q0+3) of a record of Q quads.
@@ -75,10 +121,13 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 }
 
 struct RecMask {
-    uint64_t x, s;   // complex lanes, simple (non-consensus) lanes
+    uint64_t x, s, d;   // complex lanes, simple (non-consensus) lanes, dirty lanes (below)
 };
 
-__device__ __forceinline__ RecMask rec_mask(const uint64_t* cm, size_t rec) { return RecMask{cm[2 * rec], cm[2 * rec + 1]}; }
+__device__ __forceinline__ RecMask rec_mask(const uint64_t* cm, size_t rec) {
+    const uint64_t* q = cm + kMaskWords * rec;
+    return RecMask{q[0], q[1], q[2]};
+}
 
 // Code planes of a non-complex lane: stored (simple) or the consensus word.
 __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
@@ -87,42 +136,97 @@ __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int 
 }
 
 // Classify a word from its single-code test and code planes, write code / masks.
+// Dirty lanes (d): the lanes whose leaf / leaf-parent children the pre-order pass must
+// read -- complex lanes plus every lane the caller flags (`dirty_extra`).  Elsewhere each
+// site's set is one code c reached by the AND of every child's set, so each leaf child
+// holds c, the node's final is c (src/fitchSankoff.cpp:115-123) and no child record exists.
 __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t rec, int lane, bool complex_word,
-                                               const uint32_t* code, const uint4* cons, int64_t word, uint64_t& mx) {
+                                               bool dirty_extra, const uint32_t* code, const uint4* cons,
+                                               int64_t word, uint64_t& mx) {
     const uint4 cw = cons[word];
     const bool same = !complex_word && code[0] == cw.x && code[1] == cw.y && code[2] == cw.z && code[3] == cw.w;
     mx = __ballot(complex_word);
     const uint64_t ms = __ballot(!complex_word && !same);
+    const uint64_t md = __ballot(complex_word || dirty_extra);
     if (!complex_word && !same) p[lanes_below(ms)] = make_uint4(code[0], code[1], code[2], code[3]);
     if (lane == 0) {
-        cm[2 * rec] = mx;
-        cm[2 * rec + 1] = ms;
+        cm[kMaskWords * rec] = mx;
+        cm[kMaskWords * rec + 1] = ms;
+        cm[kMaskWords * rec + 2] = md;
+    }
+}
+
+// Code planes of any lane of a record: the consensus word, overwritten by an exec-masked
+// load for simple lanes (see kid_fetch on why loads are not selected between branches).
+__device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, int lane, const uint4* cons,
+                                              int64_t word) {
+    uint4 c = cons[word];
+    if ((m.s >> lane) & 1ull) c = p[lanes_below(m.s)];
+    return c;
+}
+
+// A record lane in flight: its code planes and, for a complex lane, its 16 planes.
+struct SetFetch {
+    uint4 c, v[4];
+    bool cx;
+};
+
+__device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m, const uint4* cons, int lane,
+                                                int64_t word, SetFetch& f) {
+    f.cx = (m.x >> lane) & 1ull;
+    f.c = rec_code_all(p, m, lane, cons, word);
+    // every lane loads; lanes that are not complex read the first complex slot (one cache
+    // line, value unused) -- a branch here makes the compiler copy the results out of the
+    // load registers and wait for them
+    const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f.v[q] = p[kWave + q * kWave + k];
+}
+
+__device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s) {
+    onehot_from_code(f.c.x, f.c.y, f.c.z, f.c.w, ~0u, s);
+    if (f.cx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            s[4 * q + 0] = f.v[q].x;
+            s[4 * q + 1] = f.v[q].y;
+            s[4 * q + 2] = f.v[q].z;
+            s[4 * q + 3] = f.v[q].w;
+        }
+    }
+}
+
+__device__ __forceinline__ void load_fitch_set(const uint4* p, const RecMask& m, const uint4* cons, int lane,
+                                               int64_t word, uint32_t* s) {
+    const bool cx = (m.x >> lane) & 1ull;
+    const uint4 c = rec_code_all(p, m, lane, cons, word);
+    uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (cx) {
+        const uint32_t k = lanes_below(m.x);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = p[kWave + q * kWave + k];
+    }
+    onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
+    if (cx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            s[4 * q + 0] = v[q].x;
+            s[4 * q + 1] = v[q].y;
+            s[4 * q + 2] = v[q].z;
+            s[4 * q + 3] = v[q].w;
+        }
     }
 }
 
 __device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t* cmask, const uint4* cons, int64_t node,
                                                int32_t tiles, int tile, int lane, int64_t word, uint32_t* s) {
     const size_t rec = (size_t)node * tiles + tile;
-    const RecMask m = rec_mask(cmask, rec);
-    const uint4* p = sets + rec * kFitchRec;
-    if ((m.x >> lane) & 1ull) {
-        const uint32_t k = lanes_below(m.x);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 v = p[kWave + q * kWave + k];
-            s[4 * q + 0] = v.x;
-            s[4 * q + 1] = v.y;
-            s[4 * q + 2] = v.z;
-            s[4 * q + 3] = v.w;
-        }
-    } else {
-        const uint4 c = rec_code(p, m, lane, cons, word);
-        onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
-    }
+    load_fitch_set(sets + rec * kFitchRec, rec_mask(cmask, rec), cons, lane, word, s);
 }
 
 __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
-                                                int32_t tiles, int tile, int lane, int64_t word, const uint32_t* s) {
+                                                int32_t tiles, int tile, int lane, int64_t word, const uint32_t* s,
+                                                bool dirty_extra = true) {
     uint32_t one = 0, two = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -135,7 +239,7 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
     uint32_t code[4];
     code_from_onehot(s, code[0], code[1], code[2], code[3]);
     uint64_t mx;
-    rec_store_head(p, cmask, rec, lane, complex_word, code, cons, word, mx);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons, word, mx);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -145,12 +249,8 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
 
 // Sankoff: a word is single-code when every site has one optimal code (Z0) and no code
 // one above optimal (Z1 empty) -- for a binary node, "both children agree".
-__device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* cmask, const uint4* cons, int64_t node,
-                                             int32_t tiles, int tile, int lane, int64_t word, uint32_t* z0, uint32_t* z1,
-                                             bool want_z1) {
-    const size_t rec = (size_t)node * tiles + tile;
-    const RecMask m = rec_mask(cmask, rec);
-    const uint4* p = sets + rec * kSankoffRec;
+__device__ __forceinline__ void load_sankoff(const uint4* p, const RecMask& m, const uint4* cons, int lane, int64_t word,
+                                             uint32_t* z0, uint32_t* z1, bool want_z1) {
     if ((m.x >> lane) & 1ull) {
         const uint32_t k = lanes_below(m.x);
 #pragma unroll
@@ -175,9 +275,16 @@ __device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* 
     }
 }
 
+__device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* cmask, const uint4* cons, int64_t node,
+                                             int32_t tiles, int tile, int lane, int64_t word, uint32_t* z0, uint32_t* z1,
+                                             bool want_z1) {
+    const size_t rec = (size_t)node * tiles + tile;
+    load_sankoff(sets + rec * kSankoffRec, rec_mask(cmask, rec), cons, lane, word, z0, z1, want_z1);
+}
+
 __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
                                               int32_t tiles, int tile, int lane, int64_t word, const uint32_t* z0,
-                                              const uint32_t* z1) {
+                                              const uint32_t* z1, bool dirty_extra = true) {
     uint32_t one = 0, two = 0, any1 = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -191,7 +298,7 @@ __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, cons
     uint32_t code[4];
     code_from_onehot(z0, code[0], code[1], code[2], code[3]);
     uint64_t mx;
-    rec_store_head(p, cmask, rec, lane, complex_word, code, cons, word, mx);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons, word, mx);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -239,10 +346,11 @@ __device__ __forceinline__ void leaf_word(const Args& a, int32_t leaf, int64_t w
     m = ~0u;
 }
 
-// Fold child `c` (child_enc_v encoding; `vl` its leaves if virtual) into (both, either).
+// Fold child `c` (child_enc_v encoding; `vl` its leaves if virtual) into (both, either);
+// `vd` collects the sites where a leaf-parent's two leaves disagree (dirty lanes).
 template <bool AP>
 __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
-                                           uint32_t* both, uint32_t* either) {
+                                           uint32_t* both, uint32_t* either, uint32_t& vd) {
     if (c < 0) {   // leaf (src/fitchSankoff.cpp:32-38, absent -> 0)
         uint4 L;
         uint32_t m;
@@ -259,7 +367,10 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
         uint4 L0, L1 = make_uint4(0, 0, 0, 0);
         uint32_t m0, m1 = 0;
         leaf_word<AP>(a, l0, word, L0, m0);
-        if (l1 >= 0) leaf_word<AP>(a, l1, word, L1, m1);
+        if (l1 >= 0) {
+            leaf_word<AP>(a, l1, word, L1, m1);
+            vd |= (L0.x ^ L1.x) | (L0.y ^ L1.y) | (L0.z ^ L1.z) | (L0.w ^ L1.w);
+        }
         const LoHi t0 = lohi_of(L0.x, L0.y, L0.z, L0.w, m0), t1 = lohi_of(L1.x, L1.y, L1.z, L1.w, m1);
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
@@ -353,9 +464,9 @@ struct DownArgs {
     const uint8_t* leaf_flag;
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
-    const uint4* sets;
+    uint4* sets;           // records; after a node's step its complex lanes hold its final
     const uint64_t* cmask;
-    uint4* finals;
+    uint4* root_final;     // [W] the root's final codes (forced roots differ from its set)
     const uint4* cons;
     int32_t root_dense;
     int32_t tiles;
@@ -368,6 +479,7 @@ struct DownArgs {
     uint8_t* root_code;
     const uint4* forced;   // Sankoff / block defaultState per site (nullable)
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
+    bool all_present;      // every leaf present at every site
 };
 
 template <class Args>
@@ -426,12 +538,11 @@ struct GlobalSink {
 };
 
 // One record per changed site (src/fitchSankoff.cpp:140-166): parent gap -> NI,
-// child gap -> ND (char '-', code 0), else NS; NI/NS carry the child's code.
+// child gap -> ND (char '-', code 0), else NS; NI/NS carry the child's code.  Written at
+// positions p, p+1, ... of the sink (p advanced).
 template <class Sink>
-__device__ __forceinline__ void emit(const Sink& sink, uint32_t node, uint32_t diff, int64_t word, const uint32_t* pc,
-                                     uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    if (!diff) return;
-    uint32_t p = sink.reserve((uint32_t)__builtin_popcount(diff));
+__device__ __forceinline__ void put_records(const Sink& sink, uint32_t& p, uint32_t node, uint32_t diff, int64_t word,
+                                            const uint32_t* pc, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     while (diff) {
         const int b = __builtin_ctz(diff);
         diff &= diff - 1;
@@ -502,16 +613,37 @@ struct Kid {
     uint32_t m0 = 0, m1 = 0;
 };
 
+// A clean lane of the parent (not `dirty`, RecMask::d) fetches nothing: its children hold
+// the parent's code there, so their masks stay 0 and they emit no records.
+// Loads are written as "initialise, then exec-masked load" with the leaf choice made on
+// uniform values first: zero-filling a load's registers on a sibling branch instead makes
+// the compiler drain every outstanding load (s_waitcnt vmcnt(0)) between the fetches.
 template <Mode M, bool AP>
-__device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 vl, int64_t word, Kid& k) {
+__device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 vl, int64_t word, bool dirty, Kid& k) {
     k.enc = enc;
+    int32_t l0 = -1, l1 = -1;
     if (enc < 0) {
-        leaf_fetch<AP>(a, -enc - 1, word, k.L0, k.m0);
+        l0 = -enc - 1;
     } else if (M != Mode::kBlockFitch && (enc & kVirtualBit)) {
         k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                          __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
-        leaf_fetch<AP>(a, k.vl.x, word, k.L0, k.m0);
-        if (k.vl.y >= 0) leaf_fetch<AP>(a, k.vl.y, word, k.L1, k.m1);
+        l0 = k.vl.x;
+        l1 = k.vl.y;
+    }
+    k.L0 = k.L1 = make_uint4(0, 0, 0, 0);
+    k.m0 = k.m1 = 0;
+    if (AP) {
+        if (l0 >= 0 && dirty) {
+            k.L0 = a.leaf_planes[(size_t)l0 * a.wpad + word];
+            k.m0 = ~0u;
+        }
+        if (l1 >= 0 && dirty) {
+            k.L1 = a.leaf_planes[(size_t)l1 * a.wpad + word];
+            k.m1 = ~0u;
+        }
+    } else {
+        if (l0 >= 0 && dirty) leaf_fetch<AP>(a, l0, word, k.L0, k.m0);
+        if (l1 >= 0 && dirty) leaf_fetch<AP>(a, l1, word, k.L1, k.m1);
     }
 }
 
@@ -526,18 +658,28 @@ __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint
     have |= m;
 }
 
-// A virtual child (one or two leaves, prefetched) of a node with final codes Fn: its
-// final, its mutation and its leaves'.
+// What a child of a node with final codes Fn records: a leaf its changed sites (d0); a
+// virtual child (one or two leaves, prefetched) its final F, its own changed sites
+// (self, against Fn) and its leaves' (d0, d1, against F).  A virtual child's final:
 //   Fitch   (src/fitchSankoff.cpp:115-123 on the union set): Fn if among the leaves'
 //           codes, else the lowest of them.
 //   Sankoff (:513-530): the optimal codes are the present leaves' codes; every other code
 //           is one above optimal unless both leaves are present with one code (then two
 //           above).  So Fn wins if among the leaves' codes, otherwise the lowest of them
 //           and -- when Fn is one above optimal -- Fn (ties go to the lowest index).
-template <Mode M, bool AP, class Sink>
-__device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
-                                            uint32_t valid, const uint32_t* Fn) {
-    const int32_t v = k.enc & ~kVirtualBit;
+struct KidOut {
+    uint32_t F[4];
+    uint32_t self, d0, d1;
+};
+
+template <Mode M>
+__device__ __forceinline__ void kid_prepare(const Kid& k, uint32_t valid, const uint32_t* Fn, KidOut& o) {
+    o.self = o.d0 = o.d1 = 0;
+    if (k.enc < 0) {
+        o.d0 = valid & k.m0 & diff4(k.L0, Fn);
+        return;
+    }
+    if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
     virt_fold(k.L0, k.m0, Fn, low, have, hit);
     virt_fold(k.L1, k.m1, Fn, low, have, hit);
@@ -548,37 +690,62 @@ __device__ __forceinline__ void virtual_kid(const DownArgs& a, const Sink& sink,
             (k.m0 & k.m1 & ((k.L0.x ^ k.L1.x) | (k.L0.y ^ k.L1.y) | (k.L0.z ^ k.L1.z) | (k.L0.w ^ k.L1.w)));
         const uint32_t take = z1_has_fn & code_less(Fn, low);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) low[j] = (Fn[j] & take) | (low[j] & ~take);
+        for (int j = 0; j < 4; ++j) low[j] = bsel(take, Fn[j], low[j]);
     }
-    uint32_t F[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) F[j] = (Fn[j] & hit) | (low[j] & ~hit);
-    const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
-    emit(sink, (uint32_t)a.internal_id[v], self, word, Fn, F[0], F[1], F[2], F[3]);
-    emit(sink, (uint32_t)a.leaf_id[k.vl.x], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
-    if (k.vl.y >= 0)
-        emit(sink, (uint32_t)a.leaf_id[k.vl.y], valid & k.m1 & diff4(k.L1, F), word, F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
+    for (int j = 0; j < 4; ++j) o.F[j] = bsel(hit, Fn[j], low[j]);
+    o.self = have & valid & ((o.F[0] ^ Fn[0]) | (o.F[1] ^ Fn[1]) | (o.F[2] ^ Fn[2]) | (o.F[3] ^ Fn[3]));
+    o.d0 = valid & k.m0 & diff4(k.L0, o.F);
+    o.d1 = valid & k.m1 & diff4(k.L1, o.F);
 }
 
+__device__ __forceinline__ uint32_t kid_count(const KidOut& o) {
+    return (uint32_t)(__builtin_popcount(o.self) + __builtin_popcount(o.d0) + __builtin_popcount(o.d1));
+}
+
+template <Mode M, class Sink>
+__device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
+                                        int64_t word, const uint32_t* Fn) {
+    if (k.enc < 0) {
+        put_records(sink, p, (uint32_t)a.leaf_id[-k.enc - 1], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
+        return;
+    }
+    if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
+    put_records(sink, p, (uint32_t)a.internal_id[k.enc & ~kVirtualBit], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
+    put_records(sink, p, (uint32_t)a.leaf_id[k.vl.x], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
+    if (k.vl.y >= 0) put_records(sink, p, (uint32_t)a.leaf_id[k.vl.y], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
+}
+
+// Records of one child (k_tail items): one sink reservation per lane.
 template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
                                             uint32_t valid, const uint32_t* F) {
-    if (k.enc < 0)
-        emit(sink, (uint32_t)a.leaf_id[-k.enc - 1], valid & k.m0 & diff4(k.L0, F), word, F, k.L0.x, k.L0.y, k.L0.z,
-             k.L0.w);
-    else if (M != Mode::kBlockFitch && (k.enc & kVirtualBit))
-        virtual_kid<M, AP>(a, sink, k, word, valid, F);
+    KidOut o;
+    kid_prepare<M>(k, valid, F, o);
+    const uint32_t n = kid_count(o);
+    if (n == 0) return;
+    uint32_t p = sink.reserve(n);
+    kid_put<M>(a, sink, p, k, o, word, F);
 }
 
 // Every record of node n's wave: the node itself and its first two children (prefetched
-// in registers).  Leaf / virtual children beyond the second are k_tail's items.
+// in registers), all counted first so each lane reserves its sink range once.  Leaf /
+// virtual children beyond the second are k_tail's items.
 template <Mode M, bool AP, class Sink>
 __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int32_t e0, int32_t e1,
                                              const Kid* kids, int64_t word, uint32_t valid, const uint32_t* pc,
                                              const uint32_t* F, uint32_t self_diff) {
-    emit(sink, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_records<M, AP>(a, sink, kids[0], word, valid, F);
-    if (e1 - e0 > 1) kid_records<M, AP>(a, sink, kids[1], word, valid, F);
+    KidOut o0, o1;
+    kid_prepare<M>(kids[0], valid, F, o0);
+    const bool two = e1 - e0 > 1;
+    if (two) kid_prepare<M>(kids[1], valid, F, o1);
+    else o1.self = o1.d0 = o1.d1 = 0;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count(o0) + kid_count(o1);
+    if (cnt == 0) return;
+    uint32_t p = sink.reserve(cnt);
+    put_records(sink, p, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    kid_put<M>(a, sink, p, kids[0], o0, word, F);
+    if (two) kid_put<M>(a, sink, p, kids[1], o1, word, F);
 }
 
 // Move a wave's staged records to one of the kShards record shards (one global atomic);
@@ -600,33 +767,48 @@ __device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* sta
     return true;
 }
 
+// Compact finals.  After an internal node's pre-order step its final codes are: the
+// root's in root_final; a complex lane's in quad 0 of that lane's record slot (the set is
+// not read again); every other lane's its record code -- a single-code set resolves to
+// its code whatever the parent holds (src/fitchSankoff.cpp:115-123 and :513-530 with
+// Z0 = {c}, Z1 = {}).  Only complex lanes are written, and children read 16 B per lane
+// only for the parent's non-consensus lanes.
+__device__ __forceinline__ uint4 rec_final(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
+    uint4 q = rec_code_all(p, m, lane, cons, word);
+    if ((m.x >> lane) & 1ull) q = p[kWave + lanes_below(m.x)];
+    return q;
+}
+
+template <int REC>
+__device__ __forceinline__ uint4 node_final(const DownArgs& a, int32_t node, int tile, int lane, int64_t word) {
+    if (node == a.root_dense) return a.root_final[word];
+    const size_t rec = (size_t)node * a.tiles + tile;
+    return rec_final(a.sets + rec * REC, rec_mask(a.cmask, rec), lane, a.cons, word);
+}
+
+__device__ __forceinline__ void store_final(const DownArgs& a, bool is_root, uint4* p, const RecMask& m, int lane,
+                                            int64_t word, const uint32_t* F) {
+    if (is_root) a.root_final[word] = make_uint4(F[0], F[1], F[2], F[3]);
+    else if ((m.x >> lane) & 1ull) p[kWave + lanes_below(m.x)] = make_uint4(F[0], F[1], F[2], F[3]);
+}
+
 // The node's final codes F (code planes) and the sites where it is resolved (pres), from
 // its own set (Fitch: one-hot planes; Sankoff: Z0 / Z1) and its parent's final pc.
 template <Mode M>
 __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, int64_t word, const uint32_t* own,
                                               const uint32_t* z1, const uint32_t* pc, uint32_t* F, uint32_t& pres) {
     if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
-        // One sweep over the 16 planes from code 15 down to 0: "parent code in own set"
-        // (hit), any code present, and the lowest present code in code-plane form.
-        const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
-        uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int v = 15; v >= 0; --v) {
-            const uint32_t o = own[v];
-            const uint32_t is_v = ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) & ((v & 4) ? pc[2] : np[2]) &
-                                  ((v & 8) ? pc[3] : np[3]);
-            hit |= is_v & o;
-            any |= o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
-        }
-        pres = any;   // state 0: subtree absent, skipped (:101-103, :136-138)
+        // "parent code in own set" (hit) by a multiplexer on the parent's code bits, the
+        // lowest code of the set by a binary search; state 0: subtree absent, skipped
+        // (:101-103, :136-138)
+        uint32_t c[4];
+        pres = lowest_code_planes(own, c);
         // root: lowest code of its set; otherwise (and always for blocks, :249-264)
         // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:98-123)
         const bool generic = !is_root || M == Mode::kBlockFitch;
-        if (!generic) hit = 0;
+        const uint32_t hit = generic ? plane_at(own, pc) : 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
+        for (int j = 0; j < 4; ++j) F[j] = bsel(hit, pc[j], c[j]);
         if (M == Mode::kBlockFitch && is_root && a.forced) {   // defaultValue (:249-250)
             const uint4 f = a.forced[word];
             F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
@@ -638,26 +820,23 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
             F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
             pres = ~0u;
         } else {
-            // One sweep from code 15 down to 0 in code-plane form.  Root: argmin = lowest
-            // optimal code (:495-507).  Otherwise the parent's code if optimal, else the
-            // lowest of Z0 and (the parent's code if it is one above optimal, Z1)
-            // (:513-530); an all-INF subtree (Z0 = Z1 = 0) stays unresolved.
-            const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
-            uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
+            // Root: argmin = lowest optimal code (:495-507).  Otherwise the parent's code if
+            // optimal (Z0), else the lowest of Z0 and -- if it is one above optimal (Z1) --
+            // the parent's code (:513-530, ties to the lowest index); an all-INF subtree
+            // (Z0 = Z1 = 0) stays unresolved.
+            uint32_t c[4];
+            const uint32_t any0 = lowest_code_planes(own, c);
+            uint32_t hit = 0, z1hit = 0;
+            if (!is_root) {
+                hit = plane_at(own, pc);
+                z1hit = plane_at(z1, pc);
+                const uint32_t take = z1hit & (~any0 | code_less(pc, c));
 #pragma unroll
-            for (int v = 15; v >= 0; --v) {
-                const uint32_t is_v = is_root ? 0u
-                                              : ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) &
-                                                    ((v & 4) ? pc[2] : np[2]) & ((v & 8) ? pc[3] : np[3]);
-                const uint32_t o = own[v] | (is_v & z1[v]);
-                hit |= is_v & own[v];
-                any |= o;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
+                for (int j = 0; j < 4; ++j) c[j] = bsel(take, pc[j], c[j]);
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
-            pres = any;
+            for (int j = 0; j < 4; ++j) F[j] = bsel(hit, pc[j], c[j]);
+            pres = any0 | z1hit;
         }
     }
 }
@@ -670,93 +849,49 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 //           one above optimal, Z1); an all-INF subtree (Z0 == 0) stays unresolved (-1).
 // Leaf children keep their own code in both modes.  Mutations (:131-171, :676-703):
 // parent code 0 -> NI, child code 0 -> ND, else NS.
-// Every load that does not depend on the parent's final (own set, parent final, the
-// first two children's words) is issued before any of them is consumed.
-// Fitch with all leaves present sits 2 VGPRs over the 8-wave budget; capping it there
-// (3 spilled VGPRs) measured 2 % faster at N*.  The other modes keep their natural size.
+// Every load that does not depend on the parent's final (own set, parent final, the first
+// two children's words) is issued before any of them is consumed.
 template <Mode M, bool AP>
 __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;   // whole wave leaves together
     if (lane == 0) stage_cnt[wave] = 0;
     const NodeDesc& d = a.desc[item];
     const int32_t n = d.node, parent = d.parent, e0 = d.e0, e1 = d.e1;
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
     const bool is_root = parent < 0;
 
+    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    const size_t rec = (size_t)n * a.tiles + tile;
+    const RecMask m = rec_mask(a.cmask, rec);
+    uint4* const p = a.sets + rec * REC;
     uint32_t own[16], pc[4], F[4];
     {
-        const uint4 q = is_root ? a.cons[word] : a.finals[(size_t)parent * a.wpad + word];
+        const uint4 q = is_root ? a.cons[word] : node_final<REC>(a, parent, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
+    const bool dirty = is_root || ((m.d >> lane) & 1ull);
     Kid kids[2];
-    kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
+    kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
     uint32_t z1[16];
-    if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
-    else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
-    uint32_t pres;
-    if constexpr (M == Mode::kFitch || M == Mode::kBlockFitch) {
-        // One sweep over the 16 planes from code 15 down to 0: "parent code in own set"
-        // (hit), any code present, and the lowest present code in code-plane form.
-        const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
-        uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int v = 15; v >= 0; --v) {
-            const uint32_t o = own[v];
-            const uint32_t is_v = ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) & ((v & 4) ? pc[2] : np[2]) &
-                                  ((v & 8) ? pc[3] : np[3]);
-            hit |= is_v & o;
-            any |= o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
-        }
-        pres = any;   // state 0: subtree absent, skipped (:101-103, :136-138)
-        // root: lowest code of its set; otherwise (and always for blocks, :249-264)
-        // parent & own ? parent : lowest(own)   (src/fitchSankoff.cpp:98-123)
-        const bool generic = !is_root || M == Mode::kBlockFitch;
-        if (!generic) hit = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
-        if (M == Mode::kBlockFitch && is_root && a.forced) {   // defaultValue (:249-250)
-            const uint4 f = a.forced[word];
-            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
-            pres = ~0u;
-        }
+    if constexpr (M == Mode::kSankoff) {
+        load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
     } else {
-        if (is_root && a.forced) {   // defaultState (src/fitchSankoff.cpp:492-493)
-            const uint4 f = a.forced[word];
-            F[0] = f.x; F[1] = f.y; F[2] = f.z; F[3] = f.w;
-            pres = ~0u;
-        } else {
-            // One sweep from code 15 down to 0 in code-plane form.  Root: argmin = lowest
-            // optimal code (:495-507).  Otherwise the parent's code if optimal, else the
-            // lowest of Z0 and (the parent's code if it is one above optimal, Z1)
-            // (:513-530); an all-INF subtree (Z0 = Z1 = 0) stays unresolved.
-            const uint32_t np[4] = {~pc[0], ~pc[1], ~pc[2], ~pc[3]};
-            uint32_t hit = 0, any = 0, c[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int v = 15; v >= 0; --v) {
-                const uint32_t is_v = is_root ? 0u
-                                              : ((v & 1) ? pc[0] : np[0]) & ((v & 2) ? pc[1] : np[1]) &
-                                                    ((v & 4) ? pc[2] : np[2]) & ((v & 8) ? pc[3] : np[3]);
-                const uint32_t o = own[v] | (is_v & z1[v]);
-                hit |= is_v & own[v];
-                any |= o;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) c[j] = ((v >> j) & 1) ? (c[j] | o) : (c[j] & ~o);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) F[j] = (pc[j] & hit) | (c[j] & ~hit);
-            pres = any;
-        }
+        SetFetch f;
+        fetch_fitch_set(p, m, a.cons, lane, word, f);
+        __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any is consumed
+        expand_fitch_set(f, own);
     }
-    a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
+    uint32_t pres;
+    resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
+    store_final(a, is_root, p, m, lane, word, F);
 
     if (is_root) {
         for (int b = 0; b < 32; ++b) {
@@ -769,12 +904,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
     node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-#ifdef PM_EXP_NOEMIT
-    if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
-    return;
-#endif
     if (total == 0) return;
-    const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
+    const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
     uint32_t base;
     pm_mut* out;
     if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
@@ -784,27 +915,31 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
 }
 
 // Records of the leaf / virtual children beyond a node's second (polytomies), after the
-// pre-order levels: wave = (tail item, tile), parent final read back from `finals`.
+// pre-order levels: wave = (tail item, tile), parent final read back (node_final).
 template <Mode M, bool AP>
 __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
     if (lane == 0) stage_cnt[wave] = 0;
     const TailDesc& t = a.tail[item];
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
+    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    const bool proot = t.parent == a.root_dense;
+    const RecMask pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
     Kid k;
-    kid_fetch<M, AP>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, k);
-    const uint4 q = a.finals[(size_t)t.parent * a.wpad + word];
+    kid_fetch<M, AP>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
+    const uint4 q = node_final<REC>(a, t.parent, tile, lane, word);
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
     kid_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
     if (total == 0) return;
-    const uint32_t shard = (uint32_t)(blockIdx.x * kWavesPerBlock + wave + blockIdx.y * 7919u) % kShards;
+    const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
     uint32_t base;
     pm_mut* out;
     if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
@@ -833,7 +968,9 @@ __global__ __launch_bounds__(kBlock) void k_down_chain(DownArgs a) {
     uint32_t pc[4];
     {
         const int32_t top_parent = a.desc[s0].parent;
-        const uint4 q = top_parent < 0 ? a.cons[word] : a.finals[(size_t)top_parent * a.wpad + word];
+        const uint4 q = top_parent < 0 ? a.cons[word]
+                                       : node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, top_parent, tile,
+                                                                                                  lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
     uint32_t flushes = 0;
@@ -841,14 +978,19 @@ __global__ __launch_bounds__(kBlock) void k_down_chain(DownArgs a) {
         const NodeDesc& d = a.desc[k];
         const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
         const bool is_root = d.parent < 0;
+        constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+        const size_t rec = (size_t)n * a.tiles + tile;
+        const RecMask m = rec_mask(a.cmask, rec);
+        uint4* const p = a.sets + rec * REC;
+        const bool dirty = is_root || ((m.d >> lane) & 1ull);
         Kid kids[2];
-        kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
-        if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
+        kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
+        if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
         uint32_t own[16], z1[16], F[4], pres;
-        if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
-        else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
+        if constexpr (M == Mode::kSankoff) load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
+        else load_fitch_set(p, m, a.cons, lane, word, own);
         resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
-        a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
+        store_final(a, is_root, p, m, lane, word, F);
         if (is_root) {
             for (int b = 0; b < 32; ++b) {
                 const int64_t site = word * 32 + b;
@@ -908,17 +1050,24 @@ __global__ __launch_bounds__(kBandWaves * kWave) void k_down_band(DownArgs a) {
             const bool is_root = d.parent < 0;
             uint32_t pc[4];
             {
-                const uint4 q = is_root ? a.cons[word] : a.finals[(size_t)d.parent * a.wpad + word];
+                const uint4 q = is_root ? a.cons[word]
+                                        : node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, d.parent, tile,
+                                                                                                   lane, word);
                 pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
             }
+            constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+            const size_t rec = (size_t)n * a.tiles + tile;
+            const RecMask m = rec_mask(a.cmask, rec);
+            uint4* const p = a.sets + rec * REC;
+            const bool dirty = is_root || ((m.d >> lane) & 1ull);
             Kid kids[2];
-            kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, kids[0]);
-            if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, kids[1]);
+            kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
+            if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
             uint32_t own[16], z1[16], F[4], pres;
-            if constexpr (M == Mode::kSankoff) load_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own, z1, !is_root);
-            else load_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, own);
+            if constexpr (M == Mode::kSankoff) load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
+            else load_fitch_set(p, m, a.cons, lane, word, own);
             resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
-            a.finals[(size_t)n * a.wpad + word] = make_uint4(F[0], F[1], F[2], F[3]);
+            store_final(a, is_root, p, m, lane, word, F);
             if (is_root) {
                 for (int b = 0; b < 32; ++b) {
                     const int64_t site = word * 32 + b;

@@ -19,11 +19,12 @@ namespace {
 template <int B>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
     const NodeDesc& d = a.desc[item];
     const int32_t n = d.node;
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
 
     uint32_t cnt[16][B];
@@ -92,7 +93,10 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
         z0[v] = cand[v] & finite;
         z1[v] = eq;
     }
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1);
+    // dirty lanes: complex ones, and all when a child's code can differ from a single
+    // optimal code (three or more children: Z0 = {c}, Z1 = {} still admits a child at
+    // count 1 <= max - 2) or a leaf can be absent
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, !a.all_present || e1 - e0 > 2);
 }
 
 // Z0 of one child (leaf, virtual leaf-parent or record), as k_sankoff_up reads it.
@@ -138,9 +142,11 @@ template <int B>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
     __shared__ uint32_t part[16 * B + 1][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const NodeDesc& d = a.desc[blockIdx.x];
+    int32_t item;
+    int tile;
+    block_item(a.tiles, item, tile);
+    const NodeDesc& d = a.desc[item];
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-    const int tile = blockIdx.y;
     const int64_t word = (int64_t)tile * kWave + lane;
     uint32_t cnt[16][B];
 #pragma unroll
@@ -253,6 +259,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.cons = c->cons;
     up.forced = nullptr;   // Sankoff forces the root in the backward pass only
     up.absent_code0 = block;
+    up.all_present = c->leaves_all_present;
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
@@ -263,7 +270,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             if (e == b) continue;
             up.desc = up_desc + b;
             up.count = e - b;
-            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles), wide(up.count, tiles);
+            const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
             if (k == 0) hipLaunchKernelGGL(k_sankoff_up<2>, grid, dim3(kBlock), 0, c->stream, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
@@ -284,9 +291,9 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.leaf_flag = c->leaf_flag;
     dn.leaf_planes = c->leaf_planes;
     dn.leaf_present = c->leaf_present;
-    dn.sets = reinterpret_cast<const uint4*>(c->sets);
+    dn.sets = reinterpret_cast<uint4*>(c->sets);
     dn.cmask = c->cmask;
-    dn.finals = c->finals;
+    dn.root_final = c->root_final;
     dn.cons = c->cons;
     dn.root_dense = dt.root_dense;
     dn.tiles = tiles;
@@ -299,13 +306,14 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.root_code = c->root_code;
     dn.forced = c->has_forced ? c->forced : nullptr;
     dn.absent_code0 = block;
+    dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
-        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
         if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else hipLaunchKernelGGL((k_down<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
@@ -314,7 +322,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
     dn.count = virt ? ht.num_tail_v : ht.num_tail;
     if (dn.count > 0) {
-        dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
+        const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
         if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
