@@ -540,18 +540,53 @@ struct GlobalSink {
 // One record per changed site (src/fitchSankoff.cpp:140-166): parent gap -> NI,
 // child gap -> ND (char '-', code 0), else NS; NI/NS carry the child's code.  Written at
 // positions p, p+1, ... of the sink (p advanced).
+// The record's low byte, (type << 4) | code, comes from six bit-planes computed for all 32
+// sites at once: the child's code planes (an ND child has code 0, the '-' record code),
+// ND = parent not gap & child gap, NI = parent gap (PM_MUT_ND = 1, PM_MUT_NI = 2).
+static_assert(PM_MUT_NS == 0 && PM_MUT_ND == 1 && PM_MUT_NI == 2, "record type bits");
+__device__ __forceinline__ uint32_t bit_at(uint32_t plane, int b) { return __builtin_amdgcn_ubfe(plane, b, 1); }
+
+// A lane whose word holds more than kHeavyBits records (an N run at a leaf, a gap) is
+// expanded by 32 lanes at once; the others write theirs one per loop iteration, so the
+// wave's trip count is at most kHeavyBits plus one per heavy lane instead of the largest
+// per-lane count (up to 32).  Positions p .. p + popc(diff) - 1 were reserved by the lane.
+// Called with every lane of the wave active (lanes 0-31 write a heavy lane's records).
+constexpr int kHeavyBits = 4;
+
 template <class Sink>
 __device__ __forceinline__ void put_records(const Sink& sink, uint32_t& p, uint32_t node, uint32_t diff, int64_t word,
                                             const uint32_t* pc, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    while (diff) {
-        const int b = __builtin_ctz(diff);
-        diff &= diff - 1;
-        const uint32_t pcode = code_at(pc[0], pc[1], pc[2], pc[3], b);
-        const uint32_t c = code_at(c0, c1, c2, c3, b);
-        const uint32_t type = pcode == 0 ? PM_MUT_NI : (c == 0 ? PM_MUT_ND : PM_MUT_NS);
-        const uint32_t site = (uint32_t)(word * 32 + b);
-        sink.put(p++, pm_mut{node, (site << 8) | (type << 4) | (type == PM_MUT_ND ? 0u : c)});
+    if (__ballot(diff != 0) == 0) return;
+    const uint32_t pz = ~(pc[0] | pc[1] | pc[2] | pc[3]);
+    const uint32_t nd = ~pz & ~(c0 | c1 | c2 | c3);
+    const uint32_t site0 = (uint32_t)(word * 32);
+    const uint32_t nbits = (uint32_t)__builtin_popcount(diff);
+    const bool heavy = nbits > (uint32_t)kHeavyBits;
+    uint32_t d = heavy ? 0u : diff, q = p;
+    while (d) {
+        const int b = __builtin_ctz(d);
+        d &= d - 1;
+        const uint32_t low = bit_at(c0, b) | (bit_at(c1, b) << 1) | (bit_at(c2, b) << 2) | (bit_at(c3, b) << 3) |
+                             (bit_at(nd, b) << 4) | (bit_at(pz, b) << 5);
+        sink.put(q++, pm_mut{node, ((site0 + (uint32_t)b) << 8) | low});
     }
+    uint64_t hv = __ballot(heavy);
+    const int lane = threadIdx.x & 63, j = lane & 31;
+    while (hv) {
+        const int l = __builtin_ctzll(hv);
+        hv &= hv - 1;
+        const uint32_t w = __builtin_amdgcn_readlane(diff, l);
+        const uint32_t h0 = __builtin_amdgcn_readlane(c0, l), h1 = __builtin_amdgcn_readlane(c1, l),
+                       h2 = __builtin_amdgcn_readlane(c2, l), h3 = __builtin_amdgcn_readlane(c3, l),
+                       hn = __builtin_amdgcn_readlane(nd, l), hz = __builtin_amdgcn_readlane(pz, l),
+                       hs = __builtin_amdgcn_readlane(site0, l), hp = __builtin_amdgcn_readlane(p, l);
+        if (lane < 32 && ((w >> j) & 1u)) {
+            const uint32_t low = bit_at(h0, j) | (bit_at(h1, j) << 1) | (bit_at(h2, j) << 2) | (bit_at(h3, j) << 3) |
+                                 (bit_at(hn, j) << 4) | (bit_at(hz, j) << 5);
+            sink.put(hp + __builtin_amdgcn_mbcnt_lo(w, 0u), pm_mut{node, ((hs + (uint32_t)j) << 8) | low});
+        }
+    }
+    p += nbits;
 }
 
 // Same records written at out[pos...] (count returned): the region kernels' two-pass form.
@@ -723,8 +758,7 @@ __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink,
     KidOut o;
     kid_prepare<M>(k, valid, F, o);
     const uint32_t n = kid_count(o);
-    if (n == 0) return;
-    uint32_t p = sink.reserve(n);
+    uint32_t p = n ? sink.reserve(n) : 0u;   // every lane stays active (put_records expands cooperatively)
     kid_put<M>(a, sink, p, k, o, word, F);
 }
 
@@ -741,8 +775,7 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
     if (two) kid_prepare<M>(kids[1], valid, F, o1);
     else o1.self = o1.d0 = o1.d1 = 0;
     const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count(o0) + kid_count(o1);
-    if (cnt == 0) return;
-    uint32_t p = sink.reserve(cnt);
+    uint32_t p = cnt ? sink.reserve(cnt) : 0u;   // every lane stays active (put_records expands cooperatively)
     put_records(sink, p, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
     kid_put<M>(a, sink, p, kids[0], o0, word, F);
     if (two) kid_put<M>(a, sink, p, kids[1], o1, word, F);
@@ -902,8 +935,20 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     }
 
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+#ifdef PM_EXP_NORECORDS   // timing experiment: loads and finals only, no records
+    {
+        uint32_t x = self_diff;
+        for (int k = 0; k < 2; ++k) x ^= kids[k].L0.x ^ kids[k].L0.y ^ kids[k].L0.z ^ kids[k].L0.w ^ kids[k].L1.x ^ kids[k].L1.y ^ kids[k].L1.z ^ kids[k].L1.w;
+        if (x == 0x9E3779B9u) a.shard_cnt[0] = x;
+        return;
+    }
+#endif
     node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+#ifdef PM_EXP_NOFLUSH     // timing experiment: records staged in LDS, not written out
+    if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
+    return;
+#endif
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
     uint32_t base;
