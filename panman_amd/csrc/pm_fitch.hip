@@ -24,7 +24,7 @@ namespace {
 // (src/fitchSankoff.cpp:39-55); the first two children's loads are independent and issued
 // back to back.
 template <bool AP>
-__global__ __launch_bounds__(kBlock, AP ? 6 : 1) void k_fitch_up(UpArgs a) {
+__global__ __launch_bounds__(kBlock, AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
@@ -34,12 +34,26 @@ __global__ __launch_bounds__(kBlock, AP ? 6 : 1) void k_fitch_up(UpArgs a) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
 
+    uint4 cw;   // consensus word for the store; loaded after the children's loads (see below)
     uint32_t both[16], either[16], vd = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
-    if (e1 - e0 > 1)
-        fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
+    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
+    if constexpr (AP) {   // both children's loads in flight together
+        ChildFetch f0, f1;
+        fetch_child_ap(a, d.c0, vl0, tile, lane, word, f0);
+        if (e1 - e0 > 1) fetch_child_ap(a, d.c1, vl1, tile, lane, word, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        // after the children's consensus loads: loaded before them, the compiler reuses it
+        // for them through register copies that wait on every outstanding load
+        cw = a.cons[word];
+        fold_child_ap(d.c0, vl0, f0, both, either, vd);
+        if (e1 - e0 > 1) fold_child_ap(d.c1, vl1, f1, both, either, vd);
+    } else {
+        fold_child<AP>(a, d.c0, vl0, tile, lane, word, both, either, vd);
+        if (e1 - e0 > 1) fold_child<AP>(a, d.c1, vl1, tile, lane, word, both, either, vd);
+        cw = a.cons[word];
+    }
     for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
@@ -56,7 +70,9 @@ __global__ __launch_bounds__(kBlock, AP ? 6 : 1) void k_fitch_up(UpArgs a) {
     }
     // dirty lanes: complex, or a leaf-parent child's leaves disagree; every lane when some
     // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
-    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both, !AP || vd != 0u);
+    uint64_t mx, ms;
+    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
 #ifdef PM_EXP_COUNT_COMPLEX
     {
         uint32_t one = 0, two = 0;
@@ -203,7 +219,9 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both, !AP || vd != 0u);
+    uint64_t mx, ms;
+    store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
 }
 
 // Post-order along heavy-path chains: wave = (chain, tile), walking the chain bottom-up
@@ -259,7 +277,8 @@ __global__ __launch_bounds__(kBlock) void k_fitch_chain_up(UpArgs a) {
             const uint4 F = a.forced[word];
             onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
         }
-        store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
+        uint64_t mx, ms;   // chain / band pre-order kernels read parents' masks themselves (node_final)
+        store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, true, mx, ms);
 #pragma unroll
         for (int v = 0; v < 16; ++v) prev[v] = both[v];
     }
@@ -313,7 +332,8 @@ __global__ __launch_bounds__(kBandWaves * kWave) void k_fitch_band_up(UpArgs a) 
                 const uint4 F = a.forced[word];
                 onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
             }
-            store_fitch_set(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, both);
+            uint64_t mx, ms;
+            store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, true, mx, ms);
         }
         __syncthreads();
     }
@@ -451,6 +471,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.sets = reinterpret_cast<uint4*>(c->sets);
     dn.cmask = c->cmask;
     dn.root_final = c->root_final;
+    dn.dense_base = -1;
     dn.cons = c->cons;
     dn.root_dense = dt.root_dense;
     dn.tiles = tiles;
@@ -508,10 +529,13 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
         const bool ap = c->leaves_all_present;
-        if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else if (block) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
-        else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else hipLaunchKernelGGL((k_down<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        const bool dense = virt && ht.down_dense_v;   // level d = dense indices [down_off[d], down_off[d+1])
+        dn.dense_base = dense ? down_off[d] : -1;
+        if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (block) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
     dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;

@@ -135,7 +135,10 @@ __device__ __forceinline__ void region_sets(const FusedArgs& a, int32_t r, int t
             const uint4 F = a.forced[word];
             onehot_from_code(F.x, F.y, F.z, F.w, ~0u, x);
         }
-        if (e == n1 - 1 && root_to_hbm) store_fitch_set(a.sets, a.cmask, a.cons, dense, a.tiles, tile, lane, word, x);
+        if (e == n1 - 1 && root_to_hbm) {
+            uint64_t mx, ms;   // the region kernels keep full finals, no mask push needed
+            store_fitch_set(a.sets, a.cmask, a.cons[word], dense, a.tiles, tile, lane, x, true, mx, ms);
+        }
         else slot_store(e - n0, lane, x);
     }
 }

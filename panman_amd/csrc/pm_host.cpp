@@ -603,13 +603,34 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             for (int32_t e = off[u + 1] - 1; e >= off[u]; --e) stack.push_back(idx[e]);
         }
     }
-    for (const int32_t i : dfs) {
-        if (off[i + 1] > off[i]) {
+    // Internal nodes: the materialised ones (every internal node but the virtual
+    // leaf-parents, see below) by depth, then the virtual ones; DFS order within a depth.
+    // A pre-order level of the virtual-leaf-parent form is then a contiguous range of
+    // dense indices, so its waves know their node -- and its record masks -- without
+    // reading the level descriptor first (DevTree::down_dense).
+    auto virtual_id = [&](int32_t u) {
+        if (u == t->root || off[u + 1] == off[u] || off[u + 1] - off[u] > 2) return false;
+        for (int32_t e = off[u]; e < off[u + 1]; ++e)
+            if (off[idx[e] + 1] > off[idx[e]]) return false;
+        return true;
+    };
+    {
+        std::vector<int32_t> inner;
+        for (const int32_t i : dfs) {
+            if (off[i + 1] > off[i]) {
+                inner.push_back(i);
+            } else {
+                ht.dense_of[i] = -(int32_t)ht.leaf_id.size() - 1;
+                ht.leaf_id.push_back(i);
+            }
+        }
+        std::stable_sort(inner.begin(), inner.end(), [&](int32_t x, int32_t y) {
+            const bool vx = virtual_id(x), vy = virtual_id(y);
+            return vx != vy ? vy : depth[x] < depth[y];
+        });
+        for (const int32_t i : inner) {
             ht.dense_of[i] = (int32_t)ht.internal_id.size();
             ht.internal_id.push_back(i);
-        } else {
-            ht.dense_of[i] = -(int32_t)ht.leaf_id.size() - 1;
-            ht.leaf_id.push_back(i);
         }
     }
     const int32_t I = (int32_t)ht.internal_id.size();
@@ -726,6 +747,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         for (int32_t h = 0; h <= H; ++h) ht.up_level_off_v[h] = ht.up_class_off_v[h * kDegreeClasses];
         bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
         drop(down_order_v, ht.down_level_off_v);
+        ht.down_dense_v = true;   // pre-order item k of the virtual form is dense index k
+        for (size_t k = 0; k < down_order_v.size(); ++k) ht.down_dense_v &= down_order_v[k] == (int32_t)k;
     }
 
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {

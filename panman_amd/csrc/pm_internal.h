@@ -31,7 +31,8 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = 1024;
 constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
-constexpr int kMaskWords = 4;     // record masks per (node, tile): complex, simple, dirty, pad
+constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
+                                  // complex, parent's simple, 3 pad (one 64-B scalar load)
 constexpr int kBand = 8;          // levels per band (PM_OPT_BANDS)
 constexpr int kBandWaves = 8;     // waves per band workgroup
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
@@ -133,6 +134,7 @@ struct HostTree {
     std::vector<int32_t> up_class_off_v;    // [4H+1] (level, degree class) buckets of up_order_v
     std::vector<int32_t> down_level_off_v;
     int64_t num_virtual = 0;
+    bool down_dense_v = false;            // down_order_v[k] == k (dense order = pre-order levels)
     int32_t num_tail = 0, num_tail_v = 0;
     // chains per rank: up launches rank 0.. (chains of rank r hang only rank < r chains off
     // their nodes), down launches in the reverse order; [variant][rank + 1] chain offsets

@@ -122,11 +122,38 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 
 struct RecMask {
     uint64_t x, s, d;   // complex lanes, simple (non-consensus) lanes, dirty lanes (below)
+    uint64_t px, ps;    // the parent's x and s, pushed by the parent's post-order wave
 };
 
 __device__ __forceinline__ RecMask rec_mask(const uint64_t* cm, size_t rec) {
     const uint64_t* q = cm + kMaskWords * rec;
-    return RecMask{q[0], q[1], q[2]};
+    return RecMask{q[0], q[1], q[2], q[3], q[4]};
+}
+
+// A node's post-order wave copies its x / s masks into each materialised child's mask
+// record (words 3, 4), so the child's pre-order wave finds its parent's final (compact
+// finals, see node_final) from its own masks -- loaded with its descriptor -- instead of
+// loading the parent's masks after the descriptor.
+__device__ __forceinline__ void push_masks(uint64_t* cm, int32_t tiles, int tile, int32_t child, uint64_t mx, uint64_t ms) {
+    uint64_t* q = cm + kMaskWords * ((size_t)child * tiles + tile);
+    q[3] = mx;
+    q[4] = ms;
+}
+
+// push_masks for every materialised child of the node with children [e0, e1) (child
+// encodings as in UpArgs::child_enc; the first two also in c0, c1); lanes share the list.
+__device__ __forceinline__ bool materialised(int32_t c) { return c >= 0 && !(c & kVirtualBit); }
+
+__device__ __forceinline__ void push_children(const UpArgs& a, int tile, int lane, int32_t e0, int32_t e1, int32_t c0,
+                                              int32_t c1, uint64_t mx, uint64_t ms) {
+    if (lane == 0) {
+        if (materialised(c0)) push_masks(a.cmask, a.tiles, tile, c0, mx, ms);
+        if (e1 - e0 > 1 && materialised(c1)) push_masks(a.cmask, a.tiles, tile, c1, mx, ms);
+    }
+    for (int32_t e = e0 + 2 + lane; e < e1; e += kWave) {
+        const int32_t c = a.child_enc[e];
+        if (materialised(c)) push_masks(a.cmask, a.tiles, tile, c, mx, ms);
+    }
 }
 
 // Code planes of a non-complex lane: stored (simple) or the consensus word.
@@ -141,12 +168,11 @@ __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int 
 // site's set is one code c reached by the AND of every child's set, so each leaf child
 // holds c, the node's final is c (src/fitchSankoff.cpp:115-123) and no child record exists.
 __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t rec, int lane, bool complex_word,
-                                               bool dirty_extra, const uint32_t* code, const uint4* cons,
-                                               int64_t word, uint64_t& mx) {
-    const uint4 cw = cons[word];
+                                               bool dirty_extra, const uint32_t* code, const uint4& cw, uint64_t& mx,
+                                               uint64_t& ms) {
     const bool same = !complex_word && code[0] == cw.x && code[1] == cw.y && code[2] == cw.z && code[3] == cw.w;
     mx = __ballot(complex_word);
-    const uint64_t ms = __ballot(!complex_word && !same);
+    ms = __ballot(!complex_word && !same);
     const uint64_t md = __ballot(complex_word || dirty_extra);
     if (!complex_word && !same) p[lanes_below(ms)] = make_uint4(code[0], code[1], code[2], code[3]);
     if (lane == 0) {
@@ -156,13 +182,13 @@ __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t re
     }
 }
 
-// Code planes of any lane of a record: the consensus word, overwritten by an exec-masked
-// load for simple lanes (see kid_fetch on why loads are not selected between branches).
+// Code planes of any lane of a record (complex lanes: unused), one load from a per-lane
+// address: the stored word of a simple lane or the consensus word (see kid_fetch on why
+// loads are not selected between branches).
 __device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, int lane, const uint4* cons,
                                               int64_t word) {
-    uint4 c = cons[word];
-    if ((m.s >> lane) & 1ull) c = p[lanes_below(m.s)];
-    return c;
+    const uint4* src = ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
+    return *src;
 }
 
 // A record lane in flight: its code planes and, for a complex lane, its 16 planes.
@@ -224,9 +250,10 @@ __device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t
     load_fitch_set(sets + rec * kFitchRec, rec_mask(cmask, rec), cons, lane, word, s);
 }
 
-__device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
-                                                int32_t tiles, int tile, int lane, int64_t word, const uint32_t* s,
-                                                bool dirty_extra = true) {
+// Returns the record's (x, s) masks through mx / ms (for push_masks).
+__device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, const uint4& cw, int64_t node,
+                                                int32_t tiles, int tile, int lane, const uint32_t* s,
+                                                bool dirty_extra, uint64_t& mx, uint64_t& ms) {
     uint32_t one = 0, two = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -238,8 +265,7 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
     uint4* p = sets + rec * kFitchRec;
     uint32_t code[4];
     code_from_onehot(s, code[0], code[1], code[2], code[3]);
-    uint64_t mx;
-    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons, word, mx);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cw, mx, ms);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -284,7 +310,7 @@ __device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* 
 
 __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
                                               int32_t tiles, int tile, int lane, int64_t word, const uint32_t* z0,
-                                              const uint32_t* z1, bool dirty_extra = true) {
+                                              const uint32_t* z1, bool dirty_extra, uint64_t& mx, uint64_t& ms) {
     uint32_t one = 0, two = 0, any1 = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -297,8 +323,7 @@ __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, cons
     uint4* p = sets + rec * kSankoffRec;
     uint32_t code[4];
     code_from_onehot(z0, code[0], code[1], code[2], code[3]);
-    uint64_t mx;
-    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons, word, mx);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons[word], mx, ms);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -407,6 +432,64 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
     }
 }
 
+// All-present post-order children in two phases, so that both children's loads are in
+// flight together: a fetch into `code` (leaf codes, or the record's code planes) and `v`
+// (a leaf-parent's second leaf in v[0], or a complex lane's 16 planes), written only by
+// loads -- zero-filling them on a sibling branch makes the compiler drain all outstanding
+// loads -- then the fold into (both, either).
+struct ChildFetch {
+    uint4 code, v[4];
+    bool cx;
+};
+
+__device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
+                                               ChildFetch& f) {
+    f.cx = false;
+    if (c < 0) {
+        f.code = a.leaf_planes[(size_t)(-c - 1) * a.wpad + word];
+    } else if (c & kVirtualBit) {
+        const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
+        f.code = a.leaf_planes[(size_t)l0 * a.wpad + word];
+        if (l1 >= 0) f.v[0] = a.leaf_planes[(size_t)l1 * a.wpad + word];
+    } else {
+        const size_t rec = (size_t)c * a.tiles + tile;
+        const RecMask m = rec_mask(a.cmask, rec);
+        const uint4* p = a.sets + rec * kFitchRec;
+        f.cx = (m.x >> lane) & 1ull;
+        f.code = rec_code_all(p, m, lane, a.cons, word);
+        const uint32_t k = f.cx ? lanes_below(m.x) : 0u;   // other lanes: one shared line, unused
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f.v[q] = p[kWave + q * kWave + k];
+    }
+}
+
+__device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
+                                              uint32_t& vd) {
+    uint32_t x[16];
+    const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
+    if (c >= 0 && (c & kVirtualBit)) {
+        if (__builtin_amdgcn_readfirstlane(vl.y) >= 0) {
+            const uint4 L1 = f.v[0];
+            vd |= (f.code.x ^ L1.x) | (f.code.y ^ L1.y) | (f.code.z ^ L1.z) | (f.code.w ^ L1.w);
+            const LoHi u = lohi_of(L1.x, L1.y, L1.z, L1.w, ~0u);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];
+        }
+    } else if (c >= 0 && f.cx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            x[4 * q] = f.v[q].x; x[4 * q + 1] = f.v[q].y; x[4 * q + 2] = f.v[q].z; x[4 * q + 3] = f.v[q].w;
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        both[v] &= x[v];
+        either[v] |= x[v];
+    }
+}
+
 // Leaf child as a one-hot set: src/fitchSankoff.cpp:32-38 (absent leaf -> 0).
 template <class Args>
 __device__ __forceinline__ void leaf_set16(const Args& a, int32_t leaf, int64_t word, uint32_t* s) {
@@ -466,7 +549,8 @@ struct DownArgs {
     const uint32_t* leaf_present;
     uint4* sets;           // records; after a node's step its complex lanes hold its final
     const uint64_t* cmask;
-    uint4* root_final;     // [W] the root's final codes (forced roots differ from its set)
+    uint4* root_final;     // [W] the root's final codes (a forced root's differ from its set)
+    int32_t dense_base;    // k_down<.., DENSE>: the level's first dense index (item k = dense base + k)
     const uint4* cons;
     int32_t root_dense;
     int32_t tiles;
@@ -804,14 +888,25 @@ __device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* sta
 // root's in root_final; a complex lane's in quad 0 of that lane's record slot (the set is
 // not read again); every other lane's its record code -- a single-code set resolves to
 // its code whatever the parent holds (src/fitchSankoff.cpp:115-123 and :513-530 with
-// Z0 = {c}, Z1 = {}).  Only complex lanes are written, and children read 16 B per lane
-// only for the parent's non-consensus lanes.
+// Z0 = {c}, Z1 = {}).  Only complex lanes are written; a child reads 16 B per lane only
+// for its parent's non-consensus lanes, locating them with the parent's x / s masks
+// (pushed into its own mask record by the post-order pass, RecMask::px / ps).
 __device__ __forceinline__ uint4 rec_final(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
-    uint4 q = rec_code_all(p, m, lane, cons, word);
-    if ((m.x >> lane) & 1ull) q = p[kWave + lanes_below(m.x)];
-    return q;
+    const uint4* src = ((m.x >> lane) & 1ull) ? p + kWave + lanes_below(m.x)
+                                              : ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
+    return *src;
 }
 
+// The parent's final for a node whose own masks (with the pushed parent masks) are `m`.
+template <int REC>
+__device__ __forceinline__ uint4 parent_final(const DownArgs& a, int32_t parent, const RecMask& m, int tile, int lane,
+                                              int64_t word) {
+    if (parent == a.root_dense) return a.root_final[word];
+    const RecMask pm{m.px, m.ps, 0, 0, 0};
+    return rec_final(a.sets + ((size_t)parent * a.tiles + tile) * REC, pm, lane, a.cons, word);
+}
+
+// Any internal node's final, its own masks loaded here (tail, chain and band kernels).
 template <int REC>
 __device__ __forceinline__ uint4 node_final(const DownArgs& a, int32_t node, int tile, int lane, int64_t word) {
     if (node == a.root_dense) return a.root_final[word];
@@ -884,7 +979,9 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 // parent code 0 -> NI, child code 0 -> ND, else NS.
 // Every load that does not depend on the parent's final (own set, parent final, the first
 // two children's words) is issued before any of them is consumed.
-template <Mode M, bool AP>
+// DENSE: the level's nodes are the dense indices dense_base + item (DevTree down order),
+// so the record masks are fetched alongside the descriptor, not after it.
+template <Mode M, bool AP, bool DENSE>
 __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
@@ -895,7 +992,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     if (item >= a.count) return;   // whole wave leaves together
     if (lane == 0) stage_cnt[wave] = 0;
     const NodeDesc& d = a.desc[item];
-    const int32_t n = d.node, parent = d.parent, e0 = d.e0, e1 = d.e1;
+    const int32_t n = DENSE ? a.dense_base + item : d.node;
+    const int32_t parent = d.parent, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
     const bool is_root = parent < 0;
@@ -906,7 +1004,7 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_d
     uint4* const p = a.sets + rec * REC;
     uint32_t own[16], pc[4], F[4];
     {
-        const uint4 q = is_root ? a.cons[word] : node_final<REC>(a, parent, tile, lane, word);
+        const uint4 q = is_root ? a.cons[word] : parent_final<REC>(a, parent, m, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
     const bool dirty = is_root || ((m.d >> lane) & 1ull);
@@ -974,12 +1072,11 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     const TailDesc& t = a.tail[item];
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
-    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
     const bool proot = t.parent == a.root_dense;
     const RecMask pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
     Kid k;
     kid_fetch<M, AP>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
-    const uint4 q = node_final<REC>(a, t.parent, tile, lane, word);
+    const uint4 q = node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, t.parent, tile, lane, word);
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
     kid_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);

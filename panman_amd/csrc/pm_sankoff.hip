@@ -96,7 +96,9 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     // dirty lanes: complex ones, and all when a child's code can differ from a single
     // optimal code (three or more children: Z0 = {c}, Z1 = {} still admits a child at
     // count 1 <= max - 2) or a leaf can be absent
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, !a.all_present || e1 - e0 > 2);
+    uint64_t rx, rs;
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, !a.all_present || e1 - e0 > 2, rx, rs);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
 // Z0 of one child (leaf, virtual leaf-parent or record), as k_sankoff_up reads it.
@@ -227,7 +229,9 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
         z0[v] = cand[v] & finite;
         z1[v] = eq;
     }
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1);
+    uint64_t rx, rs;
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
 }  // namespace
@@ -294,6 +298,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.sets = reinterpret_cast<uint4*>(c->sets);
     dn.cmask = c->cmask;
     dn.root_final = c->root_final;
+    dn.dense_base = -1;
     dn.cons = c->cons;
     dn.root_dense = dt.root_dense;
     dn.tiles = tiles;
@@ -315,8 +320,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         if (dn.count == 0) continue;
         const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
-        if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else hipLaunchKernelGGL((k_down<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        const bool dense = virt && ht.down_dense_v;   // level d = dense indices [down_off[d], down_off[d+1])
+        dn.dense_base = dense ? down_off[d] : -1;
+        if (c->leaves_all_present && dense) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else hipLaunchKernelGGL((k_down<Mode::kSankoff, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
     dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
