@@ -442,6 +442,7 @@ struct ChildFetch {
     bool cx;
 };
 
+template <int REC = kFitchRec>
 __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
                                                ChildFetch& f) {
     f.cx = false;
@@ -454,7 +455,7 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
     } else {
         const size_t rec = (size_t)c * a.tiles + tile;
         const RecMask m = rec_mask(a.cmask, rec);
-        const uint4* p = a.sets + rec * kFitchRec;
+        const uint4* p = a.sets + rec * REC;   // Sankoff: the Z0 planes
         f.cx = (m.x >> lane) & 1ull;
         f.code = rec_code_all(p, m, lane, a.cons, word);
         const uint32_t k = f.cx ? lanes_below(m.x) : 0u;   // other lanes: one shared line, unused
@@ -463,9 +464,8 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
     }
 }
 
-__device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
-                                              uint32_t& vd) {
-    uint32_t x[16];
+// A fetched child's 16-plane set (Fitch) / optimal set Z0 (Sankoff); vd as fold_child's.
+__device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
     const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u);
 #pragma unroll
     for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
@@ -483,6 +483,12 @@ __device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFet
             x[4 * q] = f.v[q].x; x[4 * q + 1] = f.v[q].y; x[4 * q + 2] = f.v[q].z; x[4 * q + 3] = f.v[q].w;
         }
     }
+}
+
+__device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
+                                              uint32_t& vd) {
+    uint32_t x[16];
+    child_set_ap(c, vl, f, x, vd);
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         both[v] &= x[v];
@@ -982,7 +988,7 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 // DENSE: the level's nodes are the dense indices dense_base + item (DevTree down order),
 // so the record masks are fetched alongside the descriptor, not after it.
 template <Mode M, bool AP, bool DENSE>
-__global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : 1) void k_down(DownArgs a) {
+__global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;

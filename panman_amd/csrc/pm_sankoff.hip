@@ -16,7 +16,43 @@
 namespace pm {
 namespace {
 
+// Z0 of one child (leaf, virtual leaf-parent or record), as k_sankoff_up reads it.
+template <class Args>
+__device__ __forceinline__ void child_z0(const Args& a, int32_t c, int32_t l0, int32_t l1, int tile, int lane,
+                                         int64_t word, uint32_t* z) {
+    if (c >= 0 && (c & kVirtualBit)) {
+        uint32_t x[16];
+        leaf_set16(a, l0, word, z);
+        if (l1 >= 0) {
+            leaf_set16(a, l1, word, x);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) z[v] |= x[v];
+        }
+    } else if (c >= 0) {
+        load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);
+    } else {
+        leaf_set16(a, -c - 1, word, z);
+    }
+}
+
 template <int B>
+__device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& finite, const uint32_t* z) {
+    finite |= any_plane(z);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t x = z[v];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint32_t t = cnt[v][b] & x;
+            cnt[v][b] ^= x;
+            x = t;
+        }
+    }
+}
+
+// AP: every leaf present -- the first two children's loads are issued together (see
+// fetch_child_ap), the third (if any) after.
+template <int B, bool AP>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
@@ -34,35 +70,30 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
         for (int b = 0; b < B; ++b) cnt[v][b] = 0;
     uint32_t finite = 0, z[16];
     const int32_t e0 = d.e0, e1 = d.e1;
-    for (int32_t e = e0; e < e1; ++e) {
+    int32_t first = e0;
+    if constexpr (AP) {
+        const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], -1, -1), vl1 = make_int4(d.vl1[0], d.vl1[1], -1, -1);
+        ChildFetch f0, f1;
+        fetch_child_ap<kSankoffRec>(a, d.c0, vl0, tile, lane, word, f0);
+        if (e1 - e0 > 1) fetch_child_ap<kSankoffRec>(a, d.c1, vl1, tile, lane, word, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t vd = 0;
+        child_set_ap(d.c0, vl0, f0, z, vd);
+        count_child<B>(cnt, finite, z);
+        if (e1 - e0 > 1) {
+            child_set_ap(d.c1, vl1, f1, z, vd);
+            count_child<B>(cnt, finite, z);
+        }
+        first = e0 + 2;
+    }
+    for (int32_t e = first; e < e1; ++e) {   // one or two leaves: Z0 = their codes (:376-402)
         const int32_t c = e == e0 ? d.c0 : (e == e0 + 1 ? d.c1 : __builtin_amdgcn_readfirstlane(a.child_enc[e]));
-        if (c >= 0 && (c & kVirtualBit)) {   // one or two leaves: Z0 = their codes (:376-402)
-            const int4 vl = e == e0 ? make_int4(d.vl0[0], d.vl0[1], -1, -1)
-                                    : (e == e0 + 1 ? make_int4(d.vl1[0], d.vl1[1], -1, -1) : a.vleaf[c & ~kVirtualBit]);
-            const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
-            uint32_t x[16];
-            leaf_set16(a, l0, word, z);
-            if (l1 >= 0) {
-                leaf_set16(a, l1, word, x);
-#pragma unroll
-                for (int v = 0; v < 16; ++v) z[v] |= x[v];
-            }
-        } else if (c >= 0) {
-            load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);   // child's Z0
-        } else {
-            leaf_set16(a, -c - 1, word, z);   // leaf: {code}, absent: INF
-        }
-        finite |= any_plane(z);   // an all-INF child adds nothing (:398-400)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            uint32_t x = z[v];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const uint32_t t = cnt[v][b] & x;
-                cnt[v][b] ^= x;
-                x = t;
-            }
-        }
+        const int4 vl = !(c >= 0 && (c & kVirtualBit)) ? make_int4(-1, -1, -1, -1)
+                        : e == e0                       ? make_int4(d.vl0[0], d.vl0[1], -1, -1)
+                        : e == e0 + 1                   ? make_int4(d.vl1[0], d.vl1[1], -1, -1)
+                                                        : a.vleaf[c & ~kVirtualBit];
+        child_z0(a, c, __builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y), tile, lane, word, z);
+        count_child<B>(cnt, finite, z);   // an all-INF child adds nothing (:398-400)
     }
     // maximum count per site, most significant bit first
     uint32_t cand[16], mx[B];
@@ -99,40 +130,6 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     uint64_t rx, rs;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, !a.all_present || e1 - e0 > 2, rx, rs);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
-}
-
-// Z0 of one child (leaf, virtual leaf-parent or record), as k_sankoff_up reads it.
-template <class Args>
-__device__ __forceinline__ void child_z0(const Args& a, int32_t c, int32_t l0, int32_t l1, int tile, int lane,
-                                         int64_t word, uint32_t* z) {
-    if (c >= 0 && (c & kVirtualBit)) {
-        uint32_t x[16];
-        leaf_set16(a, l0, word, z);
-        if (l1 >= 0) {
-            leaf_set16(a, l1, word, x);
-#pragma unroll
-            for (int v = 0; v < 16; ++v) z[v] |= x[v];
-        }
-    } else if (c >= 0) {
-        load_sankoff(a.sets, a.cmask, a.cons, c, a.tiles, tile, lane, word, z, nullptr, false);
-    } else {
-        leaf_set16(a, -c - 1, word, z);
-    }
-}
-
-template <int B>
-__device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& finite, const uint32_t* z) {
-    finite |= any_plane(z);
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        uint32_t x = z[v];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const uint32_t t = cnt[v][b] & x;
-            cnt[v][b] ^= x;
-            x = t;
-        }
-    }
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
@@ -276,10 +273,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             up.count = e - b;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (k == 0) hipLaunchKernelGGL(k_sankoff_up<2>, grid, dim3(kBlock), 0, c->stream, up);
+            if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, c->stream, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
             else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_sankoff_up<12>, grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL((k_sankoff_up<12, false>), grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
     }
