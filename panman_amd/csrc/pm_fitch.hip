@@ -340,10 +340,13 @@ __global__ __launch_bounds__(kBandWaves * kWave) void k_fitch_band_up(UpArgs a) 
 }
 
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
-// LDS (sites fit) or straight into global counters.
-__global__ __launch_bounds__(kBlock) void k_site_score(const pm_mut* recs, const uint32_t* shard_cnt,
-                                                       int64_t shard_cap, uint32_t root_id, int32_t* score,
-                                                       int64_t sites, int shards_per_block, bool use_lds) {
+// LDS (sites fit) or straight into global counters.  1024-thread workgroups: the LDS
+// histogram (4 B per site) admits one workgroup per CU, so the workgroup brings the waves.
+constexpr int kScoreBlock = 1024;
+
+__global__ __launch_bounds__(kScoreBlock) void k_site_score(const pm_mut* recs, const uint32_t* shard_cnt,
+                                                            int64_t shard_cap, uint32_t root_id, int32_t* score,
+                                                            int64_t sites, int shards_per_block, bool use_lds) {
     extern __shared__ uint32_t hist[];
     if (use_lds) {
         for (int64_t s = threadIdx.x; s < sites; s += blockDim.x) hist[s] = 0;
@@ -354,12 +357,21 @@ __global__ __launch_bounds__(kBlock) void k_site_score(const pm_mut* recs, const
         if (shard >= kShards) break;
         const int64_t n = min((int64_t)shard_cnt[shard], shard_cap);
         const pm_mut* r = recs + (size_t)shard * shard_cap;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const pm_mut m = r[i];
-            if (m.node == root_id) continue;
-            const uint32_t site = m.site_info >> 8;
-            if (use_lds) atomicAdd(&hist[site], 1u);
-            else atomicAdd(&score[site], 1);
+        constexpr int U = 4;   // records in flight per thread
+        for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)U * blockDim.x) {
+            pm_mut m[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + (int64_t)u * blockDim.x;
+                m[u] = i < n ? r[i] : pm_mut{root_id, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (m[u].node == root_id) continue;
+                const uint32_t site = m[u].site_info >> 8;
+                if (use_lds) atomicAdd(&hist[site], 1u);
+                else atomicAdd(&score[site], 1);
+            }
         }
     }
     if (use_lds) {
@@ -561,7 +573,7 @@ hipError_t launch_score(pm_ctx* c) {
     const int blocks = kShards / spb;
     const size_t lds = use_lds ? (size_t)c->num_sites * 4 : 0;
     timer_begin(c, 2);
-    hipLaunchKernelGGL(k_site_score, dim3(blocks), dim3(kBlock), lds, c->stream, c->recs, c->shard_cnt,
+    hipLaunchKernelGGL(k_site_score, dim3(blocks), dim3(kScoreBlock), lds, c->stream, c->recs, c->shard_cnt,
                        c->shard_cap, (uint32_t)c->ht.root, c->score, c->num_sites, spb, use_lds);
     timer_end(c, 2);
     return hipGetLastError();
