@@ -49,9 +49,11 @@ def parse():
                    help="Fitch passes in bands of 8 levels (PM_OPT_BANDS=1)")
     p.add_argument("--chains", action="store_true",
                    help="heavy-path chain kernels instead of one launch per tree level (PM_OPT_CHAINS=1)")
-    p.add_argument("--graph", action="store_true",
-                   help="replay each step's launch sequence from a hipGraph (PM_OPT_GRAPH); "
-                        "per-kernel times then come from an extra untimed eager pass")
+    p.add_argument("--eager", action="store_true",
+                   help="launch each step's kernels one by one instead of replaying the step's launch "
+                        "sequence from a hipGraph (PM_OPT_GRAPH, the default; per-kernel times then come "
+                        "from an extra untimed eager pass)")
+    p.add_argument("--graph", action="store_true", help="(default) hipGraph replay")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -61,7 +63,9 @@ def parse():
     p.add_argument("--cpu-leaves", type=int, default=16, help="leaves replayed on the CPU baseline")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
-    return p.parse_args()
+    a = p.parse_args()
+    a.graph = not a.eager
+    return a
 
 
 def log(rank, *a):
