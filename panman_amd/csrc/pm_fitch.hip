@@ -23,8 +23,13 @@ namespace {
 // One wave = (node, tile).  Children are folded straight into the AND / OR accumulators
 // (src/fitchSankoff.cpp:39-55); the first two children's loads are independent and issued
 // back to back.
-template <bool AP>
-__global__ __launch_bounds__(kBlock, AP ? 5 : 1) void k_fitch_up(UpArgs a) {
+// LEAFY: every child of the level's nodes is a leaf or a virtual leaf-parent (the lowest
+// post-order level): no record loads, fewer registers, more waves per SIMD.
+#ifndef PM_LEAFY_WAVES
+#define PM_LEAFY_WAVES 6
+#endif
+template <bool AP, bool LEAFY>
+__global__ __launch_bounds__(kBlock, LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
@@ -41,8 +46,8 @@ __global__ __launch_bounds__(kBlock, AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;
-        fetch_child_ap(a, d.c0, vl0, tile, lane, word, f0);
-        if (e1 - e0 > 1) fetch_child_ap(a, d.c1, vl1, tile, lane, word, f1);
+        fetch_child_ap<kFitchRec, LEAFY>(a, d.c0, vl0, tile, lane, word, f0);
+        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY>(a, d.c1, vl1, tile, lane, word, f1);
         __builtin_amdgcn_sched_barrier(0);
         // after the children's consensus loads: loaded before them, the compiler reuses it
         // for them through register copies that wait on every outstanding load
@@ -57,7 +62,13 @@ __global__ __launch_bounds__(kBlock, AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-        fold_child<AP>(a, c, vl, tile, lane, word, both, either, vd);
+        if constexpr (LEAFY) {
+            ChildFetch f;
+            fetch_child_ap<kFitchRec, true>(a, c, vl, tile, lane, word, f);
+            fold_child_ap(c, vl, f, both, either, vd);
+        } else {
+            fold_child<AP>(a, c, vl, tile, lane, word, both, either, vd);
+        }
     }
     // AND if non-empty, else OR (src/fitchSankoff.cpp:48-55)
     const uint32_t nz = any_plane(both);
@@ -453,9 +464,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             up.desc = up_desc + b;
             up.count = m - b;
             const dim3 grid = wave_grid(up.count, tiles);
+            const bool leafy = virt && ht.up_leafy_v[h];
             timer_begin(c, 0);
-            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up<true>, grid, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_fitch_up<false>, grid, dim3(kBlock), 0, c->stream, up);
+            if (c->leaves_all_present && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (c->leaves_all_present) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
+            else hipLaunchKernelGGL((k_fitch_up<false, false>), grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
         if (e > m) {

@@ -132,7 +132,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
     hipError_t e;
     if ((e = dev_alloc(&c->leaf_planes, (size_t)c->dt.num_leaves * wpad)) != hipSuccess ||
         (e = dev_alloc(&c->leaf_flag, (size_t)c->dt.num_leaves)) != hipSuccess ||
-        (e = dev_alloc(&c->cons, (size_t)wpad)) != hipSuccess ||
+        (e = dev_alloc(&c->cons, (size_t)std::max<int64_t>(wpad, 4 * kWave))) != hipSuccess ||   // cx_base reads 4 tiles
         (e = dev_alloc(&c->forced, (size_t)wpad)) != hipSuccess ||
         (e = dev_alloc(&c->score, (size_t)sites)) != hipSuccess ||
         (e = dev_alloc(&c->root_code, (size_t)sites)) != hipSuccess ||
@@ -140,7 +140,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
         free_columns(c);
         return fail(c, PM_ERR_OOM, std::string("column buffers: ") + hipGetErrorString(e));
     }
-    (void)hipMemsetAsync(c->cons, 0, sizeof(uint4) * wpad, c->stream);
+    (void)hipMemsetAsync(c->cons, 0, sizeof(uint4) * std::max<int64_t>(wpad, 4 * kWave), c->stream);
     return PM_OK;
 }
 
@@ -745,6 +745,15 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         drop(up_order_v, ht.up_class_off_v);
         ht.up_level_off_v.assign(H + 1, 0);
         for (int32_t h = 0; h <= H; ++h) ht.up_level_off_v[h] = ht.up_class_off_v[h * kDegreeClasses];
+        // levels whose nodes of out-degree <= 3 have only leaf / virtual children
+        ht.up_leafy_v.assign(H, 0);
+        for (int32_t h = 0; h < H; ++h) {
+            bool leafy = true;
+            for (int32_t i = ht.up_class_off_v[h * kDegreeClasses]; i < ht.up_class_off_v[h * kDegreeClasses + 1] && leafy; ++i)
+                for (int32_t e = ht.child_off[up_order_v[i]]; e < ht.child_off[up_order_v[i] + 1]; ++e)
+                    leafy &= child_enc_v[e] < 0 || (child_enc_v[e] & kVirtualBit) != 0;
+            ht.up_leafy_v[h] = leafy;
+        }
         bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off_v, down_order_v);
         drop(down_order_v, ht.down_level_off_v);
         ht.down_dense_v = true;   // pre-order item k of the virtual form is dense index k

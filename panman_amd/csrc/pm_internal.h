@@ -132,6 +132,7 @@ struct HostTree {
     std::vector<int32_t> child_enc;
     std::vector<int32_t> up_level_off_v;    // levels of up_order_v / down_order_v
     std::vector<int32_t> up_class_off_v;    // [4H+1] (level, degree class) buckets of up_order_v
+    std::vector<uint8_t> up_leafy_v;        // [H] level's out-degree <= 3 nodes have leaf / virtual children only
     std::vector<int32_t> down_level_off_v;
     int64_t num_virtual = 0;
     bool down_dense_v = false;            // down_order_v[k] == k (dense order = pre-order levels)

@@ -191,6 +191,13 @@ __device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, 
     return *src;
 }
 
+// Where a wave's complex-slot loads point: the record's complex area, or -- when the record
+// has no complex lane (uniform) -- the consensus words, which every wave reads anyway (L2
+// resident), instead of four DRAM lines of unused record memory.
+__device__ __forceinline__ const uint4* cx_base(const uint4* p, const RecMask& m, const uint4* cons) {
+    return m.x ? p + kWave : cons;
+}
+
 // A record lane in flight: its code planes and, for a complex lane, its 16 planes.
 struct SetFetch {
     uint4 c, v[4];
@@ -201,12 +208,13 @@ __device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m
                                                 int64_t word, SetFetch& f) {
     f.cx = (m.x >> lane) & 1ull;
     f.c = rec_code_all(p, m, lane, cons, word);
-    // every lane loads; lanes that are not complex read the first complex slot (one cache
-    // line, value unused) -- a branch here makes the compiler copy the results out of the
-    // load registers and wait for them
+    // every lane loads (a branch here makes the compiler copy the results out of the load
+    // registers and wait for them): lanes that are not complex read the first complex slot
+    // (value unused), or -- no complex lane at all -- the cache-resident consensus
+    const uint4* base = cx_base(p, m, cons);
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f.v[q] = p[kWave + q * kWave + k];
+    for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
 }
 
 __device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s) {
@@ -442,7 +450,8 @@ struct ChildFetch {
     bool cx;
 };
 
-template <int REC = kFitchRec>
+// LEAFY: the caller knows c is a leaf or a virtual leaf-parent (no record, fewer registers).
+template <int REC = kFitchRec, bool LEAFY = false>
 __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
                                                ChildFetch& f) {
     f.cx = false;
@@ -452,15 +461,16 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
         f.code = a.leaf_planes[(size_t)l0 * a.wpad + word];
         if (l1 >= 0) f.v[0] = a.leaf_planes[(size_t)l1 * a.wpad + word];
-    } else {
+    } else if (!LEAFY) {
         const size_t rec = (size_t)c * a.tiles + tile;
         const RecMask m = rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * REC;   // Sankoff: the Z0 planes
         f.cx = (m.x >> lane) & 1ull;
         f.code = rec_code_all(p, m, lane, a.cons, word);
-        const uint32_t k = f.cx ? lanes_below(m.x) : 0u;   // other lanes: one shared line, unused
+        const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
+        const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) f.v[q] = p[kWave + q * kWave + k];
+        for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
     }
 }
 
