@@ -254,14 +254,23 @@ struct ReplayDev {
     const int64_t* edit_off = nullptr;    // [N+1]
     const uint32_t* edit_col = nullptr;
     const uint8_t* edit_chr = nullptr;
-    const int32_t* edit_blk = nullptr;
+    // blocks' column ranges [blk_lo, blk_hi) (id order = column order) and, per column tile,
+    // the first block ending inside or after it: an absent block's columns are restored to
+    // the consensus after the edits, so edits need no per-edit presence test
+    int32_t blocks = 0;
+    const int64_t* blk_lo = nullptr;
+    const int64_t* blk_hi = nullptr;
+    const int32_t* tile_blk = nullptr;   // [tiles + 1]
     // column tiles of kReplayTile bytes: per node, the first edit of each tile
     int32_t tiles = 0;
     const int64_t* tile_edit = nullptr;   // [N][tiles + 1]
     const int64_t* path_off = nullptr;    // [leaves + 1] root-to-leaf node lists
     const int32_t* path = nullptr;
 };
-constexpr int64_t kReplayTile = 32768;   // leaf-row bytes assembled in LDS per workgroup
+#ifndef PM_REPLAY_TILE
+#define PM_REPLAY_TILE 16384
+#endif
+constexpr int64_t kReplayTile = PM_REPLAY_TILE;   // leaf-row bytes assembled in LDS per workgroup
 
 // FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
 // segment per (leaf, print position) -- a block read forward or reverse-complemented from

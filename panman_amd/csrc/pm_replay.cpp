@@ -258,6 +258,17 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
             tile_edit[(size_t)v * (tiles + 1) + t] = e;
         }
     }
+    std::vector<int64_t> blk_lo(M), blk_hi(M);
+    for (int32_t id = 0; id < M; ++id) {
+        blk_lo[id] = r.col_start[id];
+        blk_hi[id] = r.col_start[id] + r.width[id];
+    }
+    std::vector<int32_t> tile_blk(tiles + 1);
+    for (int32_t t = 0, id = 0; t <= tiles; ++t) {
+        const int64_t c0 = (int64_t)t * kReplayTile;
+        while (id < M && blk_hi[id] <= c0) ++id;
+        tile_blk[t] = id;
+    }
 
     // ---- device
     std::vector<char> cons_row(stride, '-');
@@ -268,7 +279,8 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     if ((e = dput(&r.d_cons, cons_row, c->stream)) != hipSuccess || (e = dput(&r.d_parent, r.parent, c->stream)) != hipSuccess ||
         (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, presence, c->stream)) != hipSuccess ||
         (e = dput(&r.d_eoff, eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, ecol, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_echr, echr, c->stream)) != hipSuccess || (e = dput(&r.d_eblk, eblk, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_echr, echr, c->stream)) != hipSuccess || (e = dput(&r.d_blk_lo, blk_lo, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_blk_hi, blk_hi, c->stream)) != hipSuccess || (e = dput(&r.d_tile_blk, tile_blk, c->stream)) != hipSuccess ||
         (e = dput(&r.d_tile_edit, tile_edit, c->stream)) != hipSuccess ||
         (e = dput(&r.d_path_off, path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, path_all, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
@@ -287,7 +299,10 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     d.edit_off = r.d_eoff;
     d.edit_col = r.d_ecol;
     d.edit_chr = r.d_echr;
-    d.edit_blk = r.d_eblk;
+    d.blocks = M;
+    d.blk_lo = r.d_blk_lo;
+    d.blk_hi = r.d_blk_hi;
+    d.tile_blk = r.d_tile_blk;
     d.tiles = tiles;
     d.tile_edit = r.d_tile_edit;
     d.path_off = r.d_path_off;
@@ -310,7 +325,9 @@ void free_replay(pm_ctx* c) {
     dfree(r->d_eoff);
     dfree(r->d_ecol);
     dfree(r->d_echr);
-    dfree(r->d_eblk);
+    dfree(r->d_blk_lo);
+    dfree(r->d_blk_hi);
+    dfree(r->d_tile_blk);
     dfree(r->d_tile_edit);
     dfree(r->d_path_off);
     dfree(r->d_path);

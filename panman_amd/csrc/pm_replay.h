@@ -42,7 +42,9 @@ struct ReplayState {
     int64_t* d_eoff = nullptr;
     uint32_t* d_ecol = nullptr;
     uint8_t* d_echr = nullptr;
-    int32_t* d_eblk = nullptr;
+    int64_t* d_blk_lo = nullptr;
+    int64_t* d_blk_hi = nullptr;
+    int32_t* d_tile_blk = nullptr;
     int64_t* d_tile_edit = nullptr;
     int64_t* d_path_off = nullptr;
     int32_t* d_path = nullptr;

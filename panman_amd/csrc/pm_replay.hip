@@ -68,14 +68,18 @@ __global__ __launch_bounds__(256) void k_replay_tile(ReplayDev d) {
                     else hi_k = mid - 1;
                 }
                 const int64_t e = lo[lo_k] + (g - pre[lo_k]);
-                const int32_t b = d.edit_blk[e];
-                if ((pres[b >> 5] >> (b & 31)) & 1u) {
-                    node[j] = lo_k;
-                    col[j] = d.edit_col[e];
-                    chr[j] = (char)d.edit_chr[e];
-                }
+                node[j] = lo_k;
+                col[j] = d.edit_col[e];
+                chr[j] = (char)d.edit_chr[e];
             }
             const int64_t hi_g = min(total, base + (int64_t)kPer * blockDim.x);
+#ifdef PM_EXP_NOBARRIERS   // timing experiment: edits written in one pass (conflicts unordered)
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+                if (node[j] >= 0) buf[col[j] - c0] = chr[j];
+            __syncthreads();
+            if (hi_g >= 0) continue;
+#endif
             for (int k = 0; k < cnt; ++k) {   // root first
                 if (pre[k + 1] <= base || pre[k] >= hi_g) continue;   // uniform: no edits this round
 #pragma unroll
@@ -86,6 +90,15 @@ __global__ __launch_bounds__(256) void k_replay_tile(ReplayDev d) {
         }
         __syncthreads();   // lo / pre are reused by the next chunk
     }
+    // blocks absent at the leaf keep the consensus (their edits are not applied: :1842)
+    for (int32_t id = d.tile_blk[t]; id < d.blocks; ++id) {
+        const int64_t b_lo = d.blk_lo[id];
+        if (b_lo >= c0 + n) break;
+        if ((pres[id >> 5] >> (id & 31)) & 1u) continue;
+        const int64_t a = max(b_lo, c0), b = min(d.blk_hi[id], c0 + n);
+        for (int64_t k = a + threadIdx.x; k < b; k += blockDim.x) buf[k - c0] = d.cons_row[k];
+    }
+    __syncthreads();
     uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
     for (int64_t k = threadIdx.x; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
 }
