@@ -190,18 +190,24 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
         for (int k = 0; k < cnt; k += 2) {
             const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
             const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
-            UpFetch f0, f1;
-            up_fetch<AP>(a, c0, v0, tile, lane, word, f0);
             const bool two = k + 1 < cnt;
-            int32_t c1 = 0;
-            if (two) {
-                c1 = __builtin_amdgcn_readlane(enc, k + 1);
-                const int4 v1 = make_int4(__builtin_amdgcn_readlane(vl.x, k + 1),
-                                          __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1);
-                up_fetch<AP>(a, c1, v1, tile, lane, word, f1);
+            const int32_t c1 = two ? __builtin_amdgcn_readlane(enc, k + 1) : 0;
+            const int4 v1 = two ? make_int4(__builtin_amdgcn_readlane(vl.x, k + 1), __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1)
+                                : make_int4(-1, -1, -1, -1);
+            if constexpr (AP) {   // both children's loads in flight together (see k_fitch_up)
+                ChildFetch f0, f1;
+                fetch_child_ap(a, c0, v0, tile, lane, word, f0);
+                if (two) fetch_child_ap(a, c1, v1, tile, lane, word, f1);
+                __builtin_amdgcn_sched_barrier(0);
+                fold_child_ap(c0, v0, f0, both, either, vd);
+                if (two) fold_child_ap(c1, v1, f1, both, either, vd);
+            } else {
+                UpFetch f0, f1;
+                up_fetch<AP>(a, c0, v0, tile, lane, word, f0);
+                if (two) up_fetch<AP>(a, c1, v1, tile, lane, word, f1);
+                up_fold(c0, f0, both, either, vd);
+                if (two) up_fold(c1, f1, both, either, vd);
             }
-            up_fold(c0, f0, both, either, vd);
-            if (two) up_fold(c1, f1, both, either, vd);
         }
     }
     if (wave > 0) {
