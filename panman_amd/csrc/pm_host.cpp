@@ -5,6 +5,9 @@
 // flattened once (pm_tree_upload): dense internal indices, height levels for the
 // post-order and depth levels for the pre-order, children encoded for the kernels.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <cstring>
 #include <numeric>
@@ -510,11 +513,28 @@ int pm_set_stream(pm_ctx* c, void* s) {
     return PM_OK;
 }
 
+namespace pm {
+int tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns);
+}
+
+// An experimental schedule switched on after pm_tree_upload: its structures are built by
+// uploading the same tree again, keeping the columns.
+int rebuild_tree(pm_ctx* c) {
+    if (!c->has_tree) return PM_OK;
+    const std::vector<int32_t> off = c->tree_off, idx = c->tree_idx;
+    pm_tree t{};
+    t.num_nodes = (int32_t)off.size() - 1;
+    t.child_offsets = off.data();
+    t.child_index = idx.data();
+    t.root = c->tree_root;
+    return pm::tree_upload(c, &t, true);
+}
+
 int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (!c) return PM_ERR_ARG;
     if (option == PM_OPT_FUSED) {
         c->fused = value != 0;
-        return PM_OK;
+        return c->fused && !c->built_regions ? rebuild_tree(c) : PM_OK;
     }
     if (option == PM_OPT_VIRTUAL) {
         c->virtual_leaf_parents = value != 0;
@@ -522,11 +542,11 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     }
     if (option == PM_OPT_BANDS) {
         c->bands = value != 0;
-        return PM_OK;
+        return c->bands && !c->built_bands ? rebuild_tree(c) : PM_OK;
     }
     if (option == PM_OPT_CHAINS) {
         c->chains = value != 0;
-        return PM_OK;
+        return c->chains && !c->built_chains ? rebuild_tree(c) : PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
         c->use_graph = value != 0;
@@ -543,7 +563,20 @@ int pm_set_profiling(pm_ctx* c, int enable) {
     return PM_OK;
 }
 
-int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
+int pm_tree_upload(pm_ctx* c, const pm_tree* t) { return pm::tree_upload(c, t, false); }
+
+// keep_columns: the same tree again (its leaf ranks and dense indices are the same), so the
+// uploaded columns and work buffers stay valid.
+int pm::tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns) {
+    // PM_UPLOAD_TIMING=1: host phase durations on stderr
+    const bool timing = std::getenv("PM_UPLOAD_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto upload_phase = [&](const char* what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[pm_tree_upload] %-16s %8.2f s\n", what, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
     if (!c || !t || !t->child_offsets || t->num_nodes < 2) return fail(c, PM_ERR_ARG, "bad tree");
     (void)hipSetDevice(c->device);
     const int32_t N = t->num_nodes;
@@ -624,14 +657,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 ht.leaf_id.push_back(i);
             }
         }
-        std::stable_sort(inner.begin(), inner.end(), [&](int32_t x, int32_t y) {
-            const bool vx = virtual_id(x), vy = virtual_id(y);
-            return vx != vy ? vy : depth[x] < depth[y];
-        });
-        for (const int32_t i : inner) {
-            ht.dense_of[i] = (int32_t)ht.internal_id.size();
-            ht.internal_id.push_back(i);
+        // stable counting sort by (virtual, depth): DFS order kept within a key
+        int32_t maxd = 0;
+        for (const int32_t i : inner) maxd = std::max(maxd, depth[i]);
+        const int32_t nk = 2 * (maxd + 1);
+        std::vector<int32_t> key(inner.size()), start(nk + 1, 0);
+        for (size_t k = 0; k < inner.size(); ++k) {
+            key[k] = (virtual_id(inner[k]) ? maxd + 1 : 0) + depth[inner[k]];
+            ++start[key[k] + 1];
         }
+        for (int32_t k = 0; k < nk; ++k) start[k + 1] += start[k];
+        ht.internal_id.assign(inner.size(), 0);
+        for (size_t k = 0; k < inner.size(); ++k) ht.internal_id[start[key[k]]++] = inner[k];
+        for (size_t k = 0; k < ht.internal_id.size(); ++k) ht.dense_of[ht.internal_id[k]] = (int32_t)k;
     }
     const int32_t I = (int32_t)ht.internal_id.size();
     const int32_t L = (int32_t)ht.leaf_id.size();
@@ -676,6 +714,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     bucket(D + 1, I, [&](int32_t d) { return depth[ht.internal_id[d]]; }, ht.down_level_off, down_order);
     bucket(DL + 1, L, [&](int32_t l) { return depth[ht.leaf_id[l]]; }, ht.leaf_level_off, leaf_down);
 
+    upload_phase("topology+levels");
     // heavy child first: the internal child with the largest subtree (a materialised one
     // on ties) leads its parent's child list, so it is the next node down the parent's
     // chain in both the plain and the virtual-leaf-parent form (children order is free:
@@ -707,6 +746,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
     }
 
+    upload_phase("heavy child");
     // virtual leaf-parents (Fitch level kernels)
     std::vector<int32_t> child_enc_v(ht.child_enc), up_order_v, down_order_v, vleaf((size_t)I * 4, -1);
     std::vector<uint8_t> virt(I, 0);
@@ -760,6 +800,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         for (size_t k = 0; k < down_order_v.size(); ++k) ht.down_dense_v &= down_order_v[k] == (int32_t)k;
     }
 
+    upload_phase("virtual form");
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<NodeDesc> desc(order.size());
         for (size_t k = 0; k < order.size(); ++k) {
@@ -798,10 +839,12 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             }
         return tail;
     };
-    // heavy-path chains over the materialised nodes of each form
+    upload_phase("descriptors");
+    // heavy-path chains over the materialised nodes of each form (PM_OPT_CHAINS only: the
+    // experimental schedules' structures cost seconds of host time on 10^7-node trees)
     std::vector<NodeDesc> up_chain_desc[2], down_chain_desc[2];
     std::vector<int32_t> up_chain_off[2], down_chain_off[2];
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < (c->chains ? 2 : 0); ++v) {
         const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
         auto mat = [&](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
         std::vector<int32_t> first(I, -1);   // next node down the chain
@@ -856,10 +899,11 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
     }
 
+    upload_phase("chains");
     // bands of kBand levels and their connected pieces (see DevTree)
     std::vector<NodeDesc> up_band_desc[2], down_band_desc[2];
     std::vector<int32_t> up_band_lvl[2], down_band_lvl[2];
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < (c->bands ? 2 : 0); ++v) {   // (PM_OPT_BANDS only)
         const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
         auto live = [&](int32_t d) { return v ? !virt[d] : true; };
         for (int dir = 0; dir < 2; ++dir) {   // 0: up (height), 1: down (depth)
@@ -915,12 +959,18 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.num_tail_v = (int32_t)tail_desc_v.size();
 
     Regions rg;
-    build_regions(bfs, off, idx, t->root, ht, rg);
+    upload_phase("bands");
+    if (c->fused) build_regions(bfs, off, idx, t->root, ht, rg);   // (PM_OPT_FUSED only)
+    upload_phase("regions");
     ht.rg_up_level_off = rg.up_level_off;
     ht.rg_down_level_off = rg.down_level_off;
 
-    free_work(c);
-    free_columns(c);
+    if (keep_columns) {
+        drop_graph(c);
+    } else {
+        free_work(c);
+        free_columns(c);
+    }
     free_tree(c->dt);
     DevTree dt;
     dt.num_internal = I;
@@ -981,6 +1031,13 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     c->max_degree = 0;
     for (int32_t d = 0; d < I; ++d) c->max_degree = std::max(c->max_degree, c->ht.child_off[d + 1] - c->ht.child_off[d]);
     c->has_tree = true;
+    c->built_chains = c->chains;
+    c->built_bands = c->bands;
+    c->built_regions = c->fused;
+    c->tree_off.assign(off, off + N + 1);
+    c->tree_idx.assign(idx, idx + E);
+    c->tree_root = t->root;
+    upload_phase("device upload");
     return PM_OK;
 }
 

@@ -169,6 +169,9 @@ struct pm_ctx {
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
     bool chains = false;              // heavy-path chain kernels instead of per-level ones (PM_OPT_CHAINS)
     bool bands = false;               // banded level kernels (PM_OPT_BANDS)
+    bool built_chains = false, built_bands = false, built_regions = false;   // their tree structures exist
+    std::vector<int32_t> tree_off, tree_idx;   // the uploaded tree (rebuilt when an option above is enabled)
+    int32_t tree_root = -1;
 
     // column shard
     int64_t num_sites = 0;
