@@ -1,0 +1,81 @@
+"""Parity at the benchmark's full sizes (BASELINE.json north_star N*: 1M leaves x 30k sites,
+random-join tree T1; C3: 100k leaves x 30k sites, SARS-like tree T2; one rank's shard of C4,
+8M leaves x 3 750 sites -- SURVEY.md §8d).
+
+The oracle cannot walk every column of these in seconds, so each run is checked by
+  * bit-exact oracle columns at the first word, across the first tile boundary
+    (sites 2040-2055: words 63/64 = tiles 0/1) and at the ragged last word, for every
+    node of the tree (src/fitchSankoff.cpp:30-171, :359-531 via oracle/pm_oracle.cpp);
+  * size-independent properties over ALL columns: records sorted by (node, site) and unique,
+    types/codes in range, and (Fitch) the per-site score equal to the number of non-root
+    mutation records at that site (the parsimony score, src/fitchSankoff.cpp:131-171).
+"""
+import numpy as np
+import pytest
+
+import panman_amd
+from _trees import names_for
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    "nstar": (panman_amd.random_join_tree, 1_000_000, 30_000),
+    "c3": (panman_amd.sars_like_tree, 100_000, 30_000),
+    # C4 (8M leaves x 30k sites over 8 GPUs): one rank's column shard of 3 750 sites
+    "c4shard": (panman_amd.random_join_tree, 8_000_000, 3_750),
+}
+
+
+def _samples(config, sites):
+    """(first site, count) runs: first word, the tile 0/1 boundary, the ragged last word."""
+    if config == "c4shard":   # 16M nodes: the faithful oracle walks ~1 column per thread-minute
+        return [(0, 1), (2047, 2), (sites - 1, 1)]
+    return [(0, 8), (2044, 8), (sites - 8, 8)]
+
+
+@pytest.fixture(scope="module")
+def trees():
+    return {}
+
+
+@pytest.mark.parametrize("config,mode", [(c, m) for c in CONFIGS for m in ("fitch", "sankoff")
+                                         if c != "c4shard" or m == "fitch"])
+def test_full_size_run(oracle, trees, config, mode):
+    make, leaves, sites = CONFIGS[config]
+    if config not in trees:
+        off, idx, root = make(leaves, seed=1)
+        trees[config] = (off, idx, root, names_for(off))
+    off, idx, root, names = trees[config]
+    n = off.shape[0] - 1
+    e = panman_amd.Engine(0)
+    try:
+        e.tree_upload(off, idx, root)
+        e.synth_columns(0, sites, seed=2)
+        e.run(panman_amd.MODE_FITCH if mode == "fitch" else panman_amd.MODE_SANKOFF)
+        got = e.mutations()
+        score, rootc = e.site_results()
+        runs = _samples(config, sites)
+        codes = np.hstack([e.leaf_codes(s0, ns, leaves) for s0, ns in runs])
+        cons = np.concatenate([e.consensus(s0, ns) for s0, ns in runs])
+    finally:
+        e.close()
+
+    # all columns: order, uniqueness, ranges
+    assert got.shape[0] > n // 10
+    key = got[:, 0].astype(np.int64) * sites + got[:, 1]
+    assert (np.diff(key) > 0).all()
+    assert (got[:, 0] < n).all() and (got[:, 1] < sites).all()
+    assert (got[:, 2] <= 2).all() and (got[:, 3] < 16).all()
+    if mode == "fitch":
+        assert (score == np.bincount(got[got[:, 0] != root][:, 1], minlength=sites)).all()
+
+    # sampled columns (one oracle call over all of them): every node, bit-exact
+    cols = np.concatenate([np.arange(s0, s0 + ns) for s0, ns in runs]).astype(np.uint32)
+    node_row = np.full(n, -1, np.int32)
+    node_row[:leaves] = np.arange(leaves)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names, codes, node_row, cons, None,
+                                            algo=0 if mode == "fitch" else 1, threads=8, with_root=True)
+    want[:, 1] = cols[want[:, 1]]
+    sel = got[np.isin(got[:, 1], cols)]
+    assert sel.shape == want.shape and (sel == want).all(), (sel.shape, want.shape)
+    assert (rootc[cols] == want_root).all()
