@@ -274,6 +274,7 @@ struct ReplayDev {
 #define PM_REPLAY_TILE 16384
 #endif
 constexpr int64_t kReplayTile = PM_REPLAY_TILE;   // leaf-row bytes assembled in LDS per workgroup
+constexpr uint8_t kEditOverrides = 0x80;   // edit_chr flag: an ancestor edits the same column
 
 // FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
 // segment per (leaf, print position) -- a block read forward or reverse-complemented from

@@ -195,6 +195,28 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     }
     r.edits = (int64_t)ecol.size();
 
+    // ---- edits that overwrite an ancestor's edit of the same column get kEditOverrides in
+    // their character byte: the replay kernel writes the others in any order and only these
+    // in path order (k_replay_tile).  Depth-first walk with a count of the ancestors'
+    // edits per column.
+    {
+        std::vector<int32_t> active(r.columns + 1, 0);
+        std::vector<std::pair<int32_t, bool>> stack{{p->root, false}};
+        while (!stack.empty()) {
+            const auto [v, leaving] = stack.back();
+            stack.pop_back();
+            if (leaving) {
+                for (int64_t e = eoff[v]; e < eoff[v + 1]; ++e) --active[ecol[e]];
+                continue;
+            }
+            for (int64_t e = eoff[v]; e < eoff[v + 1]; ++e)
+                if (active[ecol[e]]++ > 0) echr[e] |= kEditOverrides;
+            stack.push_back({v, true});
+            for (int32_t e = p->child_offsets[v]; e < p->child_offsets[v + 1]; ++e)
+                stack.push_back({p->child_index[e], false});
+        }
+    }
+
     // ---- per-leaf block state (getBlockSequence + the block-mutation pass of the helper)
     const int32_t L = (int32_t)r.leaves.size();
     const int32_t words = (M + 31) / 32;

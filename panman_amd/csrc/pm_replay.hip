@@ -6,101 +6,288 @@
 // nucleotide mutations of each node on its root->leaf path in order, only for blocks that
 // are present at the leaf (blockSequence, :1766-1787, :1842).
 //
-//   k_replay_tile   one workgroup per (leaf, 32 KiB column tile): consensus tile -> LDS,
-//                   the path nodes' edits inside the tile applied root first (edits of one
-//                   node are unique per column and sorted by column on the host, so a
-//                   per-(node, tile) offset table bounds each node's slice), one coalesced
-//                   write of the tile: 1 B per leaf-column to HBM, the replay roofline of
-//                   SURVEY.md §8d.
+//   k_replay_tile   one workgroup per (leaf, 16 KiB column tile): consensus tile -> LDS,
+//                   the path nodes' edits inside the tile applied root first by one wave
+//                   (edits of one node are unique per column and sorted by column on the
+//                   host, so a per-(node, tile) offset table bounds each node's slice),
+//                   absent blocks restored, one coalesced write of the tile: 1 B per
+//                   leaf-column to HBM, the replay roofline of SURVEY.md §8d.
 #include "pm_internal.h"
 
 namespace pm {
 namespace {
 
-// One workgroup = (leaf, tile of kReplayTile columns): the tile of the leaf's row is
-// assembled in LDS -- consensus copy, then each path node's edits that fall in the tile,
-// root first, one barrier per node with edits (a descendant's write wins) -- and leaves as
-// one coalesced write.  Each row byte is written to HBM once.
-__global__ __launch_bounds__(256) void k_replay_tile(ReplayDev d) {
-    __shared__ uint4 tile_buf[kReplayTile / 16];
-    char* buf = reinterpret_cast<char*>(tile_buf);
-    const int32_t leaf = blockIdx.x;
-    const int32_t t = blockIdx.y;
-    const int64_t c0 = (int64_t)t * kReplayTile;
-    const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
-    const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
-    for (int64_t k = threadIdx.x; k < n / 16; k += blockDim.x) tile_buf[k] = src[k];
-    __syncthreads();
-    const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
-    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
-    // The path's edit slices for this tile, 256 nodes at a time: slice bounds and their
-    // prefix sums in LDS, then every thread loads its share of ALL the chunk's edits at
-    // once (one round of memory latency instead of one per node), then the edits are
-    // written node by node, root first, with a barrier between nodes.
-    constexpr int kPer = 8;   // edits per thread per round
-    __shared__ int64_t lo[256], pre[257];
-    for (int64_t q = p0; q < p1; q += 256) {
-        const int cnt = (int)min((int64_t)256, p1 - q);
-        if ((int)threadIdx.x < cnt) {
-            const int64_t* te = d.tile_edit + (size_t)d.path[q + threadIdx.x] * (d.tiles + 1) + t;
-            lo[threadIdx.x] = te[0];
-            pre[threadIdx.x + 1] = te[1] - te[0];
-        }
-        if (threadIdx.x == 0) pre[0] = 0;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (int k = 1; k <= cnt; ++k) pre[k] += pre[k - 1];
-        __syncthreads();
-        const int64_t total = pre[cnt];
-        for (int64_t base = 0; base < total; base += (int64_t)kPer * blockDim.x) {
-            int node[kPer];
-            uint32_t col[kPer];
-            char chr[kPer];
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-                node[j] = -1;
-                const int64_t g = base + threadIdx.x + (int64_t)j * blockDim.x;
-                if (g >= total) continue;
-                int lo_k = 0, hi_k = cnt - 1;   // last node with pre[k] <= g
-                while (lo_k < hi_k) {
-                    const int mid = (lo_k + hi_k + 1) >> 1;
-                    if (pre[mid] <= g) lo_k = mid;
-                    else hi_k = mid - 1;
-                }
-                const int64_t e = lo[lo_k] + (g - pre[lo_k]);
-                node[j] = lo_k;
-                col[j] = d.edit_col[e];
-                chr[j] = (char)d.edit_chr[e];
-            }
-            const int64_t hi_g = min(total, base + (int64_t)kPer * blockDim.x);
-#ifdef PM_EXP_NOBARRIERS   // timing experiment: edits written in one pass (conflicts unordered)
-#pragma unroll
-            for (int j = 0; j < kPer; ++j)
-                if (node[j] >= 0) buf[col[j] - c0] = chr[j];
-            __syncthreads();
-            if (hi_g >= 0) continue;
+// The path's edits that fall in column tile t, applied to the LDS tile by ONE wave.  Only
+// an edit that overwrites an ancestor's edit of the same column (kEditOverrides, marked on
+// the host) needs ordering: the others touch distinct columns along any one path and are
+// written in any order, the overriding ones after them node by node, root first -- the
+// LDS writes of a wave take effect in issue order, so a descendant's edit wins without a
+// barrier.  A chunk is up to 64 path nodes: their slice bounds (one load per lane) and a
+// wave prefix sum of the slice lengths; a round gathers up to kEditsPerLane x 64 of the
+// chunk's edits at once (one memory round trip).
+#ifndef PM_REPLAY_EPL
+#define PM_REPLAY_EPL 4
 #endif
-            for (int k = 0; k < cnt; ++k) {   // root first
-                if (pre[k + 1] <= base || pre[k] >= hi_g) continue;   // uniform: no edits this round
-#pragma unroll
-                for (int j = 0; j < kPer; ++j)
-                    if (node[j] == k) buf[col[j] - c0] = chr[j];
-                __syncthreads();
-            }
-        }
-        __syncthreads();   // lo / pre are reused by the next chunk
+constexpr int kEditsPerLane = PM_REPLAY_EPL;
+
+struct EditChunk {
+    int cnt;
+    int64_t lo;       // this lane's node: first edit of its slice
+    int32_t len;      // this lane's node: slice length
+    int32_t excl;     // exclusive prefix of the lengths
+    int32_t total;    // edits in the chunk
+};
+
+struct EditRound {
+    uint32_t col[kEditsPerLane];
+    uint32_t nc[kEditsPerLane];   // path position << 8 | character byte; kNoEdit: none
+};
+constexpr uint32_t kNoEdit = ~0u;
+
+__device__ __forceinline__ EditChunk edit_chunk(const ReplayDev& d, int64_t q, int64_t p1, int32_t t, int lane) {
+    EditChunk c;
+    c.cnt = (int)min((int64_t)kWave, p1 - q);
+    c.lo = 0;
+    c.len = 0;
+    if (lane < c.cnt) {
+        const int64_t* te = d.tile_edit + (size_t)d.path[q + lane] * (d.tiles + 1) + t;
+        c.lo = te[0];
+        c.len = (int32_t)(te[1] - c.lo);
     }
-    // blocks absent at the leaf keep the consensus (their edits are not applied: :1842)
+    int32_t incl = c.len;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    c.excl = incl - c.len;
+    return c;
+}
+
+__device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& c, int32_t base, int64_t c0, int lane,
+                                           EditRound& r) {
+    int64_t e[kEditsPerLane];
+    int32_t node[kEditsPerLane];
+    const uint32_t lo_lo = (uint32_t)c.lo, lo_hi = (uint32_t)(c.lo >> 32);
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        // edit g of the chunk belongs to the last path node whose slice starts at or
+        // before g: a binary search over the lanes' prefix sums (64 nodes: 6 steps)
+        const int32_t g = base + lane + j * kWave;
+        int k_lo = 0, k_hi = c.cnt - 1;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            const int mid = (k_lo + k_hi + 1) >> 1;
+            if (__shfl(c.excl, mid) <= g) k_lo = mid;
+            else k_hi = mid - 1;
+        }
+        const int32_t ek = __shfl(c.excl, k_lo);
+        const int64_t lok = (int64_t)(((uint64_t)(uint32_t)__shfl((int)lo_hi, k_lo) << 32) |
+                                      (uint32_t)__shfl((int)lo_lo, k_lo));
+        node[j] = g < c.total ? k_lo : -1;
+        e[j] = lok + (g - ek);
+    }
+    uint8_t chr[kEditsPerLane];
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        r.col[j] = (uint32_t)c0;
+        chr[j] = 0;
+        if (node[j] >= 0) {
+            r.col[j] = d.edit_col[e[j]];
+            chr[j] = d.edit_chr[e[j]];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) r.nc[j] = node[j] >= 0 ? ((uint32_t)node[j] << 8 | chr[j]) : kNoEdit;
+}
+
+__device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_t c0) {
+    const int lane = (int)threadIdx.x & (kWave - 1);
+    uint64_t pend[kEditsPerLane];
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        const bool ok = r.nc[j] != kNoEdit;
+        const bool ovr = ok && (r.nc[j] & kEditOverrides);
+        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.nc[j] & 0x7fu);
+        pend[j] = __ballot(ovr);
+        any |= pend[j] != 0;
+    }
+    // the overriding edits after them, node by node in path order: the first pending edit
+    // (edits are in path order) names the next node
+    while (any) {
+        uint32_t k = 0;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < kEditsPerLane; ++j)
+            if (!found && pend[j]) {
+                k = __builtin_amdgcn_readlane(r.nc[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                found = true;
+            }
+        any = false;
+#pragma unroll
+        for (int j = 0; j < kEditsPerLane; ++j) {
+            const bool mine = ((pend[j] >> lane) & 1ull) && (r.nc[j] >> 8) == k;
+            if (mine) buf[r.col[j] - c0] = (char)(r.nc[j] & 0x7fu);
+            pend[j] &= ~__ballot(mine);
+            any |= pend[j] != 0;
+        }
+    }
+}
+
+// Any path (deep ones too): the edits of tile t, chunk by chunk, each round loaded then
+// written (no prefetch).
+__device__ __forceinline__ void apply_path_edits(const ReplayDev& d, char* buf, int32_t leaf, int32_t t, int64_t c0) {
+    const int lane = (int)threadIdx.x;
+    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
+    for (int64_t q = p0; q < p1; q += kWave) {
+        const EditChunk ch = edit_chunk(d, q, p1, t, lane);
+        for (int32_t base = 0; base < ch.total; base += kEditsPerLane * kWave) {
+            EditRound r;
+            edit_round(d, ch, base, c0, lane, r);
+            edit_write(r, buf, c0);
+        }
+    }
+}
+
+// A chunk from slice bounds already in registers (the short-path pipeline below).
+__device__ __forceinline__ EditChunk edit_chunk_from(int cnt, int64_t lo, int64_t hi, int lane) {
+    EditChunk c;
+    c.cnt = cnt;
+    c.lo = lo;
+    c.len = lane < cnt ? (int32_t)(hi - lo) : 0;
+    int32_t incl = c.len;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    c.excl = incl - c.len;
+    return c;
+}
+
+// Blocks absent at the leaf that overlap tile t, as tile-relative column ranges in LDS
+// (rng[0] = count, -1 = more than kRestoreRanges: the restore walks the blocks itself).
+constexpr int kRestoreRanges = 6;
+
+__device__ __forceinline__ void absent_ranges(const ReplayDev& d, int32_t leaf, int32_t t, int32_t* rng) {
+    const int64_t c0 = (int64_t)t * kReplayTile, c1 = min(c0 + kReplayTile, d.row_stride);
+    const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
+    int nr = 0;
     for (int32_t id = d.tile_blk[t]; id < d.blocks; ++id) {
         const int64_t b_lo = d.blk_lo[id];
-        if (b_lo >= c0 + n) break;
+        if (b_lo >= c1) break;
         if ((pres[id >> 5] >> (id & 31)) & 1u) continue;
-        const int64_t a = max(b_lo, c0), b = min(d.blk_hi[id], c0 + n);
-        for (int64_t k = a + threadIdx.x; k < b; k += blockDim.x) buf[k - c0] = d.cons_row[k];
+        if (nr == kRestoreRanges) {
+            nr = -1;
+            break;
+        }
+        rng[1 + 2 * nr] = (int32_t)(max(b_lo, c0) - c0);
+        rng[2 + 2 * nr] = (int32_t)(min(d.blk_hi[id], c1) - c0);
+        ++nr;
     }
-    __syncthreads();
-    uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
-    for (int64_t k = threadIdx.x; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
+    rng[0] = nr;
+}
+
+// blocks absent at the leaf keep the consensus (their edits are not applied: :1842)
+__device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf, int32_t t, const int32_t* rng,
+                                               char* buf, int first, int stride) {
+    const int64_t c0 = (int64_t)t * kReplayTile, c1 = min(c0 + kReplayTile, d.row_stride);
+    const int nr = rng[0];
+    if (nr >= 0) {
+        for (int i = 0; i < nr; ++i)
+            for (int32_t k = rng[1 + 2 * i] + first; k < rng[2 + 2 * i]; k += stride) buf[k] = d.cons_row[c0 + k];
+        return;
+    }
+    const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
+    for (int32_t id = d.tile_blk[t]; id < d.blocks; ++id) {
+        const int64_t b_lo = d.blk_lo[id];
+        if (b_lo >= c1) break;
+        if ((pres[id >> 5] >> (id & 31)) & 1u) continue;
+        const int64_t a = max(b_lo, c0), b = min(d.blk_hi[id], c1);
+        for (int64_t k = a + first; k < b; k += stride) buf[k - c0] = d.cons_row[k];
+    }
+}
+
+// One workgroup = (leaf, group of kReplayGroup column tiles), tile after tile: the tile of
+// the leaf's row is assembled in LDS -- consensus copy (all waves), the path nodes' edits
+// (wave 0, apply order above), blocks absent at the leaf restored (waves 1-3) -- and
+// leaves as one coalesced write; each row byte is written to HBM once.  For a path of at
+// most 64 nodes (each lane holds one), wave 0 loads the slice bounds of the whole group at
+// the start and the NEXT tile's edits while the other waves restore, write out and copy in,
+// and waves 1-3 look up the next tile's absent blocks the same way, so only the
+// consensus copy's latency stays on each tile's critical path.
+#ifndef PM_REPLAY_GROUP
+#define PM_REPLAY_GROUP 8
+#endif
+constexpr int kReplayGroup = PM_REPLAY_GROUP;   // column tiles per workgroup
+
+// PIPED: every path has at most 64 nodes (launch_replay checks max_depth).
+#ifndef PM_REPLAY_WAVES
+#define PM_REPLAY_WAVES 8
+#endif
+template <bool PIPED>
+__global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev d) {
+    __shared__ uint4 tile_buf[kReplayTile / 16];
+    __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
+    char* buf = reinterpret_cast<char*>(tile_buf);
+    const int32_t leaf = blockIdx.x;
+    const int32_t t_begin = (int32_t)blockIdx.y * kReplayGroup;
+    const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
+    const int tid = (int)threadIdx.x;
+    const bool editor = tid < kWave;
+    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
+    constexpr bool piped = PIPED;
+    const int cnt = (int)min((int64_t)kWave, p1 - p0);
+    // wave 0, piped: this lane's path node's slice bounds for the current tile and ahead
+    const int64_t* te = nullptr;
+    int64_t te_cur = 0, te_next = 0;
+    EditChunk ch{};
+    EditRound r{};
+    if (editor && piped && cnt > 0) {
+        const int32_t node = tid < cnt ? d.path[p0 + tid] : d.path[p0];
+        te = d.tile_edit + (size_t)node * (d.tiles + 1);
+        te_cur = te[t_begin];
+        te_next = te[t_begin + 1];
+        ch = edit_chunk_from(cnt, te_cur, te_next, tid);
+        if (ch.total > 0) edit_round(d, ch, 0, (int64_t)t_begin * kReplayTile, tid, r);
+    }
+    if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
+    for (int32_t t = t_begin; t < t_end; ++t) {
+        const int64_t c0 = (int64_t)t * kReplayTile;
+        const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
+        const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
+        for (int64_t k = tid; k < n / 16; k += blockDim.x) tile_buf[k] = src[k];
+        __syncthreads();
+        if (editor) {
+            if (!piped) {
+                apply_path_edits(d, buf, leaf, t, c0);
+            } else if (cnt > 0) {
+                // this tile: the prefetched round, then any further rounds (long slices)
+                if (ch.total > 0) edit_write(r, buf, c0);
+                for (int32_t base = kEditsPerLane * kWave; base < ch.total; base += kEditsPerLane * kWave) {
+                    edit_round(d, ch, base, c0, tid, r);
+                    edit_write(r, buf, c0);
+                }
+                // the next tile's first round, in flight through the restore / write / copy
+                if (t + 1 < t_end) {
+                    te_cur = te_next;
+                    te_next = te[t + 2];
+                    ch = edit_chunk_from(cnt, te_cur, te_next, tid);
+                    if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
+                }
+            }
+        }
+        __syncthreads();
+        if (!editor) restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
+        __syncthreads();
+        if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
+        uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
+        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
+        __syncthreads();   // the tile buffer is refilled next
+    }
 }
 
 // getCodeFromNucleotide (src/panman.cpp:78-113) for the replayed characters; the reroot
@@ -251,7 +438,11 @@ hipError_t launch_fmt_write(pm_ctx* c, const FmtArgs& f, int32_t leaves) {
 hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;
     timer_begin(c, 3);
-    hipLaunchKernelGGL(k_replay_tile, dim3((unsigned)d.leaves, (unsigned)d.tiles), dim3(256), 0, c->stream, d);
+    const unsigned groups = (unsigned)((d.tiles + kReplayGroup - 1) / kReplayGroup);
+    if (d.max_depth <= kWave)
+        hipLaunchKernelGGL(k_replay_tile<true>, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
+    else
+        hipLaunchKernelGGL(k_replay_tile<false>, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
     timer_end(c, 3);
     return hipGetLastError();
 }
