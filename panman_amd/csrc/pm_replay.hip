@@ -197,8 +197,16 @@ __device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf,
     const int64_t c0 = (int64_t)t * kReplayTile, c1 = min(c0 + kReplayTile, d.row_stride);
     const int nr = rng[0];
     if (nr >= 0) {
-        for (int i = 0; i < nr; ++i)
-            for (int32_t k = rng[1 + 2 * i] + first; k < rng[2 + 2 * i]; k += stride) buf[k] = d.cons_row[c0 + k];
+        const uint4* cons16 = reinterpret_cast<const uint4*>(d.cons_row + c0);
+        uint4* buf16 = reinterpret_cast<uint4*>(buf);
+        for (int i = 0; i < nr; ++i) {
+            const int32_t a = rng[1 + 2 * i], b = rng[2 + 2 * i];
+            const int32_t a16 = min((a + 15) & ~15, b), b16 = max(b & ~15, a16);
+            // ragged ends byte by byte, the aligned middle 16 B per thread
+            if (first < a16 - a) buf[a + first] = d.cons_row[c0 + a + first];
+            if (first < b - b16) buf[b16 + first] = d.cons_row[c0 + b16 + first];
+            for (int32_t k = a16 / 16 + first; k < b16 / 16; k += stride) buf16[k] = cons16[k];
+        }
         return;
     }
     const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
@@ -271,17 +279,18 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
                     edit_round(d, ch, base, c0, tid, r);
                     edit_write(r, buf, c0);
                 }
-                // the next tile's first round, in flight through the restore / write / copy
-                if (t + 1 < t_end) {
-                    te_cur = te_next;
-                    te_next = te[t + 2];
-                    ch = edit_chunk_from(cnt, te_cur, te_next, tid);
-                    if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
-                }
             }
         }
         __syncthreads();
-        if (!editor) restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
+        if (!editor) {
+            restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
+        } else if (piped && cnt > 0 && t + 1 < t_end) {
+            // the next tile's first round, in flight through the restore / write / copy
+            te_cur = te_next;
+            te_next = te[t + 2];
+            ch = edit_chunk_from(cnt, te_cur, te_next, tid);
+            if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
+        }
         __syncthreads();
         if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
         uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
