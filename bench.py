@@ -460,6 +460,13 @@ def replay_main(args):
         cpu = {"value": k * cols / secs, "unit": "leaf*column/s", "cores": 1, "kind": "port",
                "sample": f"first {k} leaves by name, aligned FASTA, oracle printFASTAUltraFast restatement "
                          f"({secs:.1f}s, 1 thread; the reference's tbb::parallel_for_each body)"}
+    # PMC-measured HBM bytes per k_replay_tile launch (tools/pmc_traffic.py, key replay:LxC)
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            traffic = json.load(open(args.traffic)).get("k_replay_tile", {}).get(f"replay:{leaves}x{cols}")
+        except (OSError, ValueError):
+            traffic = None
     out = {
         "metric": "FASTA replay leaf*column/s (aligned, GPU replay kernels)",
         "value": value, "unit": "leaf*column/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -473,7 +480,8 @@ def replay_main(args):
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
         "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "algorithmic_bytes_per_launch": alg_bytes,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
+                     "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,
                      "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},
         "host_format_s": round(fmt_s, 3),
         "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
