@@ -38,9 +38,13 @@ struct EditChunk {
     int32_t total;    // edits in the chunk
 };
 
+// A round in flight: col / chr straight from their loads (not combined with anything
+// until edit_write, so a prefetched round does not wait for its loads), node8 = path
+// position << 8, kNoEdit: none.
 struct EditRound {
     uint32_t col[kEditsPerLane];
-    uint32_t nc[kEditsPerLane];   // path position << 8 | character byte; kNoEdit: none
+    uint32_t chr[kEditsPerLane];
+    uint32_t node8[kEditsPerLane];
 };
 constexpr uint32_t kNoEdit = ~0u;
 
@@ -88,29 +92,33 @@ __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& 
         node[j] = g < c.total ? k_lo : -1;
         e[j] = lok + (g - ek);
     }
-    uint8_t chr[kEditsPerLane];
 #pragma unroll
     for (int j = 0; j < kEditsPerLane; ++j) {
         r.col[j] = (uint32_t)c0;
-        chr[j] = 0;
+        r.chr[j] = 0;
         if (node[j] >= 0) {
             r.col[j] = d.edit_col[e[j]];
-            chr[j] = d.edit_chr[e[j]];
+            r.chr[j] = d.edit_chr[e[j]];
         }
+        r.node8[j] = node[j] >= 0 ? (uint32_t)node[j] << 8 : kNoEdit;
     }
-#pragma unroll
-    for (int j = 0; j < kEditsPerLane; ++j) r.nc[j] = node[j] >= 0 ? ((uint32_t)node[j] << 8 | chr[j]) : kNoEdit;
 }
 
 __device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_t c0) {
+#ifdef PM_EXP_NOWRITE   // timing experiment: edits loaded, not written
+    uint32_t x = 0;
+    for (int j = 0; j < kEditsPerLane; ++j) x ^= r.col[j] ^ r.chr[j] ^ r.node8[j];
+    if (x == 0x9E3779B9u) buf[0] = 1;
+    return;
+#endif
     const int lane = (int)threadIdx.x & (kWave - 1);
     uint64_t pend[kEditsPerLane];
     bool any = false;
 #pragma unroll
     for (int j = 0; j < kEditsPerLane; ++j) {
-        const bool ok = r.nc[j] != kNoEdit;
-        const bool ovr = ok && (r.nc[j] & kEditOverrides);
-        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.nc[j] & 0x7fu);
+        const bool ok = r.node8[j] != kNoEdit;
+        const bool ovr = ok && (r.chr[j] & kEditOverrides);
+        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
         pend[j] = __ballot(ovr);
         any |= pend[j] != 0;
     }
@@ -122,14 +130,14 @@ __device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j)
             if (!found && pend[j]) {
-                k = __builtin_amdgcn_readlane(r.nc[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                k = __builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
                 found = true;
             }
         any = false;
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j) {
-            const bool mine = ((pend[j] >> lane) & 1ull) && (r.nc[j] >> 8) == k;
-            if (mine) buf[r.col[j] - c0] = (char)(r.nc[j] & 0x7fu);
+            const bool mine = ((pend[j] >> lane) & 1ull) && (r.node8[j] >> 8) == k;
+            if (mine) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
             pend[j] &= ~__ballot(mine);
             any |= pend[j] != 0;
         }
@@ -234,7 +242,7 @@ constexpr int kReplayGroup = PM_REPLAY_GROUP;   // column tiles per workgroup
 
 // PIPED: every path has at most 64 nodes (launch_replay checks max_depth).
 #ifndef PM_REPLAY_WAVES
-#define PM_REPLAY_WAVES 8
+#define PM_REPLAY_WAVES 7
 #endif
 template <bool PIPED>
 __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev d) {
@@ -248,17 +256,22 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
     const bool editor = tid < kWave;
     const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
     constexpr bool piped = PIPED;
+#ifdef PM_EXP_NOEDITS   // timing experiment: no edits
+    const int cnt = 0;
+#else
     const int cnt = (int)min((int64_t)kWave, p1 - p0);
+#endif
     // wave 0, piped: this lane's path node's slice bounds for the current tile and ahead
     const int64_t* te = nullptr;
-    int64_t te_cur = 0, te_next = 0;
+    int64_t te_next = 0, te_next2 = 0;   // this lane's node: slice starts of tiles t+1, t+2
     EditChunk ch{};
     EditRound r{};
     if (editor && piped && cnt > 0) {
         const int32_t node = tid < cnt ? d.path[p0 + tid] : d.path[p0];
         te = d.tile_edit + (size_t)node * (d.tiles + 1);
-        te_cur = te[t_begin];
+        const int64_t te_cur = te[t_begin];
         te_next = te[t_begin + 1];
+        if (t_begin + 2 <= d.tiles) te_next2 = te[t_begin + 2];
         ch = edit_chunk_from(cnt, te_cur, te_next, tid);
         if (ch.total > 0) edit_round(d, ch, 0, (int64_t)t_begin * kReplayTile, tid, r);
     }
@@ -267,7 +280,23 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
         const int64_t c0 = (int64_t)t * kReplayTile;
         const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
         const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
-        for (int64_t k = tid; k < n / 16; k += blockDim.x) tile_buf[k] = src[k];
+        {
+            // LDS-DMA copy-in (1 KiB per wave-instruction, every one in flight at once); in
+            // the group's first tile waves 0 and 1 are walking their lookup chains, so
+            // waves 2-3 copy the whole tile
+            const int wv = tid >> 6;
+            const bool first = t == t_begin;
+            if (!first || wv >= 2) {
+                const int w0 = first ? 2 : 0, nw = first ? 2 : 4;
+                for (int64_t b = (int64_t)(wv - w0) * kWave; b < n / 16; b += (int64_t)nw * kWave) {
+                    const int64_t k = b + (tid & (kWave - 1));
+                    if (k < n / 16)
+                        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                                         (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0,
+                                                         0);
+                }
+            }
+        }
         __syncthreads();
         if (editor) {
             if (!piped) {
@@ -286,9 +315,13 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
             restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
         } else if (piped && cnt > 0 && t + 1 < t_end) {
             // the next tile's first round, in flight through the restore / write / copy
-            te_cur = te_next;
-            te_next = te[t + 2];
-            ch = edit_chunk_from(cnt, te_cur, te_next, tid);
+            // slice bounds loaded a tile ago; the next ones' load goes out now
+            ch = edit_chunk_from(cnt, te_next, te_next2, tid);
+            te_next = te_next2;
+            if (t + 3 <= d.tiles) te_next2 = te[t + 3];
+#ifdef PM_EXP_NOROUND   // timing experiment: slice bounds and scan only, no edit gather
+            if (ch.total == 0x7fffffff)
+#endif
             if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
         }
         __syncthreads();
