@@ -15,6 +15,7 @@ e.tree_upload(off, idx, root)
 e.synth_columns(0, S, seed=2)
 e.run(panman_amd.MODE_FITCH)
 print("mutations", e.mutation_count())
-out = (C.c_ulonglong * 2)()
+out = (C.c_ulonglong * 4)()
 e.lib.pm_exp_counters(out)
 print(f"complex words {out[0]} of {out[1]} = {out[0] / max(1, out[1]):.4f}")
+print(f"simple words {out[2]} = {out[2] / max(1, out[1]):.4f}; of them ACGT-only {out[3]} = {out[3] / max(1, out[2]):.4f}")
