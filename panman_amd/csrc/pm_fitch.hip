@@ -16,7 +16,7 @@
 
 namespace pm {
 #ifdef PM_EXP_COUNT_COMPLEX
-__device__ unsigned long long g_exp_words[2];
+__device__ unsigned long long g_exp_words[4];
 #endif
 namespace {
 
@@ -91,9 +91,13 @@ __global__ __launch_bounds__(kBlock, LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k
         for (int v = 0; v < 16; ++v) { two |= one & both[v]; one |= both[v]; }
         const bool complex_word = (one != ~0u) || two;
         const unsigned long long m = __ballot(complex_word);
+        const bool acgt = ((ms >> lane) & 1ull) && (both[1] | both[2] | both[4] | both[8]) == ~0u;
+        const unsigned long long ma = __ballot(acgt);
         if (lane == 0) {
             atomicAdd(&g_exp_words[0], (unsigned long long)__popcll(m));
             atomicAdd(&g_exp_words[1], 64ull);
+            atomicAdd(&g_exp_words[2], (unsigned long long)__popcll(ms));
+            atomicAdd(&g_exp_words[3], (unsigned long long)__popcll(ma));
         }
     }
 #endif
@@ -602,6 +606,6 @@ hipError_t launch_score(pm_ctx* c) {
 
 #ifdef PM_EXP_COUNT_COMPLEX
 extern "C" int pm_exp_counters(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_words), 16) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_words), 32) == hipSuccess ? 0 : -1;
 }
 #endif
