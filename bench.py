@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--replay-leaves", type=int, default=1000)
     p.add_argument("--replay-blocks", type=int, default=500)
     p.add_argument("--replay-block-len", type=int, default=10_000)
-    p.add_argument("--cpu-leaves", type=int, default=16, help="leaves replayed on the CPU baseline")
+    p.add_argument("--cpu-leaves", type=int, default=128, help="leaves replayed on the CPU baseline (~10 s)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     a = p.parse_args()
@@ -443,7 +443,7 @@ def replay_main(args):
     ptr, n = C.c_void_p(), C.c_int64(0)
     eng._check(eng.lib.pm_replay_format(eng.ctx, 1, C.byref(ptr), C.byref(n)), "pm_replay_format")
     fmt_s = time.perf_counter() - tf
-    text = C.string_at(ptr, n.value)
+    text = panman_amd.engine.bytes_at(ptr, n.value)   # (ctypes.string_at truncates past 2 GiB)
     eng.lib.pm_free(ptr)
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:

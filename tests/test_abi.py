@@ -90,3 +90,17 @@ def test_pack_codes_roundtrip():
     assert p.shape == (3, 4)
     back = np.stack([p & 15, p >> 4], axis=2).reshape(3, 8)[:, :7]
     assert (back == codes).all()
+
+
+def test_bytes_at_past_2gib():
+    """Texts of 2 GiB and more (a full C5 FASTA is 5 GB) come back whole: ctypes.string_at
+    takes its size as a C int and truncates them."""
+    import ctypes as C
+
+    from panman_amd.engine import bytes_at
+    n = (1 << 31) + 37
+    buf = C.create_string_buffer(n)
+    C.memset(C.addressof(buf) + n - 4, ord("x"), 4)
+    out = bytes_at(C.c_void_p(C.addressof(buf)), n)
+    assert len(out) == n and out[-4:] == b"xxxx" and out[:4] == b"\0\0\0\0"
+    del out, buf

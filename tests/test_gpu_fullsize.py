@@ -79,3 +79,31 @@ def test_full_size_run(oracle, trees, config, mode):
     sel = got[np.isin(got[:, 1], cols)]
     assert sel.shape == want.shape and (sel == want).all(), (sel.shape, want.shape)
     assert (rootc[cols] == want_root).all()
+
+
+def test_c5_full_fasta(oracle):
+    """C5 (BASELINE.json config 5): the aligned FASTA of all 1000 leaves x 5.03 M columns of
+    the synthetic C5 PanMAT (5.1 GB of text: offsets past 4 GiB) -- every record present and
+    of the aligned length, the first 32 leaves by name bit-exact against the oracle's
+    printFASTAUltraFast restatement (src/fasta.cpp:1981-2099)."""
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=1000)
+    e = panman_amd.Engine(0)
+    try:
+        got = e.fasta(pm, True)
+    finally:
+        e.close()
+    recs = {}
+    for rec in got.split(">")[1:]:
+        name, _, body = rec.partition("\n")
+        recs[name] = body
+    del got
+    assert len(recs) == 1000
+    assert len({len(b) for b in recs.values()}) == 1   # aligned: one length for every leaf
+    want = oracle.fasta(pm, True, leaf_limit=32)
+    n = 0
+    for rec in want.split(">")[1:]:
+        name, _, body = rec.partition("\n")
+        assert recs[name] == body, name
+        n += 1
+    assert n == 32
