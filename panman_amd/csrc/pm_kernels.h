@@ -1057,20 +1057,51 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode:
         return;
     }
 #endif
-    node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
-    const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
 #ifdef PM_EXP_NOFLUSH     // timing experiment: records staged in LDS, not written out
-    if (total == 0xFFFFFFFFu) a.shard_cnt[0] = total;
+    node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
+    if (__builtin_amdgcn_readfirstlane(stage_cnt[wave]) == 0xFFFFFFFFu) a.shard_cnt[0] = 0;
     return;
 #endif
+    // Records: every lane's count first, positions by a wave prefix sum (no LDS counter),
+    // and the shard reservation's global atomic issued before the records are built, so
+    // its round trip overlaps the staging.
+    KidOut o0, o1;
+    kid_prepare<M>(kids[0], valid, F, o0);
+    const bool two = e1 - e0 > 1;
+    if (two) kid_prepare<M>(kids[1], valid, F, o1);
+    else o1.self = o1.d0 = o1.d1 = 0;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count(o0) + kid_count(o1);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
     if (total == 0) return;
+    const uint32_t p0 = incl - cnt;
     const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
-    uint32_t base;
-    pm_mut* out;
-    if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
-    if (lane == 0) stage_cnt[wave] = 0;   // overflowed the stage: redo straight into global
-    node_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc,
-                    F, self_diff);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
+    const uint32_t node_id = (uint32_t)a.internal_id[n];
+    uint32_t rp = p0;
+    const LdsSink ls{stage[wave], nullptr};
+    put_records(ls, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    kid_put<M>(a, ls, rp, kids[0], o0, word, F);
+    if (two) kid_put<M>(a, ls, rp, kids[1], o1, word, F);
+    base = __shfl(base, 0, 64);
+    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
+    if (total <= kStage) {
+        for (uint32_t i = lane; i < total; i += kWave)
+            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
+        return;
+    }
+    // overflowed the stage: the same records at the same positions, straight into global
+    const GlobalSink gs{out, (int64_t)base, a.shard_cap, nullptr};
+    rp = p0;
+    put_records(gs, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
+    kid_put<M>(a, gs, rp, kids[0], o0, word, F);
+    if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
 }
 
 // Records of the leaf / virtual children beyond a node's second (polytomies), after the
