@@ -45,10 +45,6 @@ def parse():
                    help="also time the end-to-end path (H2D of the packed leaf matrix, the run, D2H of "
                         "every mutation record) on the same workload (SURVEY.md §8d), N=1 only")
     p.add_argument("--cpu-sites-1t", type=int, default=4, help="columns timed on the 1-thread CPU baseline")
-    p.add_argument("--bands", action="store_true",
-                   help="Fitch passes in bands of 8 levels (PM_OPT_BANDS=1)")
-    p.add_argument("--chains", action="store_true",
-                   help="heavy-path chain kernels instead of one launch per tree level (PM_OPT_CHAINS=1)")
     p.add_argument("--eager", action="store_true",
                    help="launch each step's kernels one by one instead of replaying the step's launch "
                         "sequence from a hipGraph (PM_OPT_GRAPH, the default; per-kernel times then come "
@@ -103,8 +99,6 @@ def main():
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
     eng.tree_upload(off, idx, root)
-    eng.set_chains(args.chains)
-    eng.set_bands(args.bands)
     eng.synth_columns(lo, s_local, seed=2)
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
@@ -252,9 +246,7 @@ def main():
                 "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
                 "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
                 "mutations_total": muts_total,
-                "launch": ("hipGraph replay" if args.graph else "eager") + (
-                    ", heavy-path chain kernels" if args.chains else ", 8-level band kernels" if args.bands
-                    else ", per-level kernels"),
+                "launch": ("hipGraph replay" if args.graph else "eager") + ", per-level kernels",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -83,26 +83,16 @@ const char* pm_last_error(const pm_ctx* ctx);
 /* Queue all work on `hip_stream` (a hipStream_t; NULL = the ctx's own stream). */
 int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 /* Options (results are identical either way):
- *   PM_OPT_FUSED   (default 0): Fitch on subtree regions with intermediate sets in LDS
- *                  (experimental; slower than the level kernels on MI355X so far).
  *   PM_OPT_VIRTUAL (default 1): the level kernels evaluate internal nodes whose children
  *                  are one or two leaves inline in their parent instead of materialising them.
  *   PM_OPT_GRAPH   (default 0): pm_run captures its launch sequence (per-level kernels,
  *                  memsets) into a hipGraph once and replays it while the tree, columns,
  *                  mode and buffers stay the same; kernel_times then reports the whole run
  *                  as class 4.
- *   PM_OPT_CHAINS  (default 0): Fitch passes walk heavy-path chains (one launch per chain
- *                  rank, ~log2 N of them) instead of one launch per tree level
- *                  (experimental: each chain step is a serial chain of dependent loads, so
- *                  it is slower than the level kernels on MI355X so far). */
-#define PM_OPT_FUSED 1
+ * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
+ * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
-#define PM_OPT_CHAINS 4
-/*   PM_OPT_BANDS   (default 0): Fitch passes in bands of 8 tree levels: one launch per
- *                  band, a workgroup per (connected piece, tile) with workgroup barriers
- *                  between the band's levels -- for deep trees (SARS-like ladders). */
-#define PM_OPT_BANDS 5
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

@@ -245,121 +245,6 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
 }
 
-// Post-order along heavy-path chains: wave = (chain, tile), walking the chain bottom-up
-// with the chain child's set carried in registers (it is every node's first child), the
-// other children folded from memory (leaves, virtual leaf-parents, side chains finished
-// by earlier launches), two fetched before either is folded.
-template <bool AP>
-__global__ __launch_bounds__(kBlock) void k_fitch_chain_up(UpArgs a) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
-    if (item >= a.count) return;
-    const int32_t chain = a.chain_base + item;
-    const int32_t s0 = a.chain_off[chain], s1 = a.chain_off[chain + 1];
-    const int tile = blockIdx.y;
-    const int64_t word = (int64_t)tile * kWave + lane;
-    uint32_t prev[16];
-    for (int32_t k = s0; k < s1; ++k) {
-        const NodeDesc& d = a.desc[k];
-        const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-        uint32_t both[16], either[16], vd = 0;
-        if (k > s0) {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) { both[v] = prev[v]; either[v] = prev[v]; }
-        } else {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
-        }
-        if (e1 - e0 > 1)
-            fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
-        for (int32_t e = e0 + 2; e < e1; e += 2) {   // polytomies: two children in flight
-            const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-            const int4 v0 = c0 >= 0 && (c0 & kVirtualBit) ? a.vleaf[c0 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-            UpFetch f0, f1;
-            up_fetch<AP>(a, c0, make_int4(__builtin_amdgcn_readfirstlane(v0.x), __builtin_amdgcn_readfirstlane(v0.y), -1, -1),
-                         tile, lane, word, f0);
-            const bool two = e + 1 < e1;
-            int32_t c1 = 0;
-            if (two) {
-                c1 = __builtin_amdgcn_readfirstlane(a.child_enc[e + 1]);
-                const int4 v1 = c1 >= 0 && (c1 & kVirtualBit) ? a.vleaf[c1 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-                up_fetch<AP>(a, c1,
-                             make_int4(__builtin_amdgcn_readfirstlane(v1.x), __builtin_amdgcn_readfirstlane(v1.y), -1, -1),
-                             tile, lane, word, f1);
-            }
-            up_fold(c0, f0, both, either, vd);
-            if (two) up_fold(c1, f1, both, either, vd);
-        }
-        const uint32_t nz = any_plane(both);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
-        if (n == a.root_dense && a.forced != nullptr) {
-            const uint4 F = a.forced[word];
-            onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
-        }
-        uint64_t mx, ms;   // chain / band pre-order kernels read parents' masks themselves (node_final)
-        store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, true, mx, ms);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) prev[v] = both[v];
-    }
-}
-
-// Post-order over a band of kBand height levels: workgroup = (piece, tile), waves share
-// each level's nodes, workgroup barrier between levels (children's records written by
-// other waves of the same workgroup).  Node body as k_fitch_chain_up's first step.
-template <bool AP>
-__global__ __launch_bounds__(kBandWaves * kWave) void k_fitch_band_up(UpArgs a) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t piece = a.chain_base + blockIdx.x;
-    const int32_t* lv = a.chain_off + (size_t)piece * (kBand + 1);
-    const int tile = blockIdx.y;
-    const int64_t word = (int64_t)tile * kWave + lane;
-    for (int j = 0; j < kBand; ++j) {
-        const int32_t lb = lv[j], le = lv[j + 1];
-        for (int32_t k = lb + wave; k < le; k += kBandWaves) {
-            const NodeDesc& d = a.desc[k];
-            const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-            uint32_t both[16], either[16], vd = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-            fold_child<AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), tile, lane, word, both, either, vd);
-            if (e1 - e0 > 1)
-                fold_child<AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), tile, lane, word, both, either, vd);
-            for (int32_t e = e0 + 2; e < e1; e += 2) {
-                const int32_t c0 = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-                const int4 v0 = c0 >= 0 && (c0 & kVirtualBit) ? a.vleaf[c0 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-                UpFetch f0, f1;
-                up_fetch<AP>(a, c0,
-                             make_int4(__builtin_amdgcn_readfirstlane(v0.x), __builtin_amdgcn_readfirstlane(v0.y), -1, -1),
-                             tile, lane, word, f0);
-                const bool two = e + 1 < e1;
-                int32_t c1 = 0;
-                if (two) {
-                    c1 = __builtin_amdgcn_readfirstlane(a.child_enc[e + 1]);
-                    const int4 v1 = c1 >= 0 && (c1 & kVirtualBit) ? a.vleaf[c1 & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
-                    up_fetch<AP>(a, c1,
-                                 make_int4(__builtin_amdgcn_readfirstlane(v1.x), __builtin_amdgcn_readfirstlane(v1.y), -1,
-                                           -1),
-                                 tile, lane, word, f1);
-                }
-                up_fold(c0, f0, both, either, vd);
-                if (two) up_fold(c1, f1, both, either, vd);
-            }
-            const uint32_t nz = any_plane(both);
-#pragma unroll
-            for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
-            if (n == a.root_dense && a.forced != nullptr) {
-                const uint4 F = a.forced[word];
-                onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
-            }
-            uint64_t mx, ms;
-            store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, true, mx, ms);
-        }
-        __syncthreads();
-    }
-}
-
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
 // LDS (sites fit) or straight into global counters.  1024-thread workgroups: the LDS
 // histogram (4 B per site) admits one workgroup per CU, so the workgroup brings the waves.
@@ -435,37 +320,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.tiles = tiles;
     up.wpad = wpad;
     const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
-    const int cv = virt ? 1 : 0;
-    const int H = (c->chains || c->bands) ? 0 : (int)up_off.size() - 1;
-    if (c->bands) {   // bands of kBand levels, one workgroup per (piece, tile)
-        up.desc = dt.up_band_desc[cv];
-        up.chain_off = dt.up_band_lvl[cv];
-        const std::vector<int32_t>& bo = ht.up_band_off[cv];
-        for (size_t b = 0; b + 1 < bo.size(); ++b) {
-            up.chain_base = bo[b];
-            up.count = bo[b + 1] - bo[b];
-            if (up.count == 0) continue;
-            dim3 grid(up.count, tiles);
-            timer_begin(c, 0);
-            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_band_up<true>, grid, dim3(kBandWaves * kWave), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_fitch_band_up<false>, grid, dim3(kBandWaves * kWave), 0, c->stream, up);
-            timer_end(c, 0);
-        }
-    } else if (c->chains) {   // heavy-path chains, rank by rank
-        up.desc = dt.up_chain_desc[cv];
-        up.chain_off = dt.up_chain_off[cv];
-        const std::vector<int32_t>& ro = ht.up_rank_off[cv];
-        for (size_t r = 0; r + 1 < ro.size(); ++r) {
-            up.chain_base = ro[r];
-            up.count = ro[r + 1] - ro[r];
-            if (up.count == 0) continue;
-            dim3 grid((up.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
-            timer_begin(c, 0);
-            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_chain_up<true>, grid, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_fitch_chain_up<false>, grid, dim3(kBlock), 0, c->stream, up);
-            timer_end(c, 0);
-        }
-    }
+    const int H = (int)up_off.size() - 1;
     for (int h = 0; h < H; ++h) {
         // out-degree <= 3: one wave per (node, tile); wider: one workgroup per (node, tile)
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
@@ -521,42 +376,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.absent_code0 = false;
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
-    if (c->bands) {
-        dn.desc = dt.down_band_desc[cv];
-        dn.chain_off = dt.down_band_lvl[cv];
-        const std::vector<int32_t>& bo = ht.down_band_off[cv];
-        const bool ap = c->leaves_all_present;
-        for (size_t b = 0; b + 1 < bo.size(); ++b) {
-            dn.chain_base = bo[b];
-            dn.count = bo[b + 1] - bo[b];
-            if (dn.count == 0) continue;
-            dim3 grid(dn.count, tiles), wg(kBandWaves * kWave);
-            timer_begin(c, 1);
-            if (block && ap) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, true>), grid, wg, 0, c->stream, dn);
-            else if (block) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, false>), grid, wg, 0, c->stream, dn);
-            else if (ap) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true>), grid, wg, 0, c->stream, dn);
-            else hipLaunchKernelGGL((k_down_band<Mode::kFitch, false>), grid, wg, 0, c->stream, dn);
-            timer_end(c, 1);
-        }
-    } else if (c->chains) {
-        dn.desc = dt.down_chain_desc[cv];
-        dn.chain_off = dt.down_chain_off[cv];
-        const std::vector<int32_t>& ro = ht.down_rank_off[cv];
-        const bool ap = c->leaves_all_present;
-        for (size_t r = 0; r + 1 < ro.size(); ++r) {
-            dn.chain_base = ro[r];
-            dn.count = ro[r + 1] - ro[r];
-            if (dn.count == 0) continue;
-            dim3 grid((dn.count + kWavesPerBlock - 1) / kWavesPerBlock, tiles);
-            timer_begin(c, 1);
-            if (block && ap) hipLaunchKernelGGL((k_down_chain<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-            else if (block) hipLaunchKernelGGL((k_down_chain<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
-            else if (ap) hipLaunchKernelGGL((k_down_chain<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-            else hipLaunchKernelGGL((k_down_chain<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
-            timer_end(c, 1);
-        }
-    }
-    const int D = (c->chains || c->bands) ? 0 : (int)down_off.size() - 1;
+    const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];

@@ -69,27 +69,9 @@ void free_tree(DevTree& t) {
     dev_free(t.down_desc_v);
     dev_free(t.tail_desc);
     dev_free(t.tail_desc_v);
-    for (int v = 0; v < 2; ++v) {
-        dev_free(t.up_chain_desc[v]);
-        dev_free(t.down_chain_desc[v]);
-        dev_free(t.up_chain_off[v]);
-        dev_free(t.down_chain_off[v]);
-        dev_free(t.up_band_desc[v]);
-        dev_free(t.down_band_desc[v]);
-        dev_free(t.up_band_lvl[v]);
-        dev_free(t.down_band_lvl[v]);
-    }
     dev_free(t.vleaf);
-    dev_free(t.rg_node_off);
-    dev_free(t.rg_node_dense);
-    dev_free(t.rg_node_pslot);
-    dev_free(t.rg_node_flags);
-    dev_free(t.rg_child_off);
-    dev_free(t.rg_child);
-    dev_free(t.rg_stage_off);
-    dev_free(t.rg_stage);
-    dev_free(t.rg_up_order);
-    dev_free(t.rg_down_order);
+    dev_free(t.part_desc);
+    dev_free(t.part_desc_v);
     t = DevTree{};
 }
 
@@ -118,9 +100,10 @@ void free_work(pm_ctx* c) {
     dev_free(c->sets);
     dev_free(c->cmask);
     dev_free(c->finals);
+    dev_free(c->sk_parts);
     dev_free(c->recs);
     dev_free(c->shard_cnt);
-    c->sets_bytes = c->finals_bytes = c->cmask_bytes = 0;
+    c->sets_bytes = c->finals_bytes = c->cmask_bytes = c->sk_parts_bytes = 0;
     c->shard_cap = 0;
 }
 
@@ -175,6 +158,17 @@ int alloc_work(pm_ctx* c, int mode) {
             return fail(c, PM_ERR_OOM, std::string("finals: ") + hipGetErrorString(e));
         c->finals_bytes = need_fin;
     }
+    if (!fitch) {   // Sankoff nodes of out-degree > 255: part counters
+        const size_t parts = (size_t)std::max(c->ht.part_off.empty() ? 0 : c->ht.part_off.back(),
+                                              c->ht.part_off_v.empty() ? 0 : c->ht.part_off_v.back());
+        const size_t need = parts * kPartPlanes * wpad * sizeof(uint32_t);
+        if (need > c->sk_parts_bytes) {
+            dev_free(c->sk_parts);
+            if ((e = hipMalloc(reinterpret_cast<void**>(&c->sk_parts), need)) != hipSuccess)
+                return fail(c, PM_ERR_OOM, std::string("Sankoff part counters: ") + hipGetErrorString(e));
+            c->sk_parts_bytes = need;
+        }
+    }
     if (!c->shard_cnt && (e = dev_alloc(&c->shard_cnt, kShards)) != hipSuccess)
         return fail(c, PM_ERR_OOM, "shard counters");
     if (c->shard_cap == 0) {
@@ -191,15 +185,14 @@ int alloc_work(pm_ctx* c, int mode) {
 hipError_t launch_all(pm_ctx* c, int mode) {
     const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
     const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
-    hipError_t e = sankoff ? launch_sankoff(c, block)
-                           : (mode == PM_MODE_FITCH && c->fused) ? launch_fitch_fused(c) : launch_fitch(c, block);
+    hipError_t e = sankoff ? launch_sankoff(c, block) : launch_fitch(c, block);
     if (e == hipSuccess) e = launch_score(c);
     return e;
 }
 
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
-    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->fused, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->chains, (uint64_t)c->bands,
+    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
                               (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals, (uint64_t)(uintptr_t)c->root_final,
@@ -214,9 +207,6 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
 }
 
 int run_once(pm_ctx* c, int mode) {
-    const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
-    if (sankoff && c->max_degree > 4095)
-        return fail(c, PM_ERR_UNSUPPORTED, "Sankoff supports up to 4095 children per node");
     hipError_t e;
     if (!c->use_graph) {
         e = launch_all(c, mode);
@@ -272,145 +262,6 @@ int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
         if (rc != PM_OK) return rc;
     }
     return fail(c, PM_ERR_STATE, "mutation record buffer still overflowing");
-}
-
-// Partition the internal nodes into connected subtree regions of at most kRegionSlots
-// internal nodes and kRegionStage leaf children (greedy, children before parents: cut the
-// heaviest child subtrees until the node fits).  Nodes with more than 4 children or more
-// leaf children than fit the stage form singleton "wide" regions that stream their leaves.
-struct Regions {
-    std::vector<int32_t> node_off{0}, node_dense, node_pslot, node_flags, child_off{0}, child, stage_off{0}, stage;
-    std::vector<int32_t> up_order, down_order, up_level_off, down_level_off;
-};
-
-void build_regions(const std::vector<int32_t>& bfs, const int32_t* off, const int32_t* idx, int32_t root,
-                   const HostTree& ht, Regions& rg) {
-    const int32_t N = (int32_t)bfs.size();
-    std::vector<int32_t> W(N, 0), LF(N, 0);
-    std::vector<uint8_t> cut(N, 0), wide(N, 0);
-    for (int32_t k = N - 1; k >= 0; --k) {
-        const int32_t v = bfs[k];
-        const int32_t deg = off[v + 1] - off[v];
-        if (deg == 0) continue;
-        int32_t leaf_kids = 0;
-        std::vector<std::pair<int32_t, int32_t>> kids;   // (weight, child)
-        for (int32_t e = off[v]; e < off[v + 1]; ++e) {
-            const int32_t c = idx[e];
-            if (off[c + 1] == off[c]) ++leaf_kids;
-            else kids.emplace_back(W[c], c);
-        }
-        if (deg > 4 || leaf_kids > kRegionStage) {
-            wide[v] = 1;
-            for (auto& kc : kids) cut[kc.second] = 1;
-            W[v] = kRegionSlots + 1;   // the parent always cuts a wide node
-            LF[v] = kRegionStage + 1;
-            continue;
-        }
-        int32_t w = 1, lf = leaf_kids;
-        for (auto& kc : kids) { w += W[kc.second]; lf += LF[kc.second]; }
-        std::sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.first > b.first; });
-        for (auto& kc : kids) {
-            if (w <= kRegionSlots && lf <= kRegionStage) break;
-            cut[kc.second] = 1;
-            w -= W[kc.second];
-            lf -= LF[kc.second];
-        }
-        W[v] = w;
-        LF[v] = lf;
-    }
-    cut[root] = 1;
-    // enumerate regions in BFS order of their roots (parents' regions first)
-    std::vector<int32_t> region_of(N, -1), reg_root, reg_depth, reg_parent;
-    for (int32_t k = 0; k < N; ++k) {
-        const int32_t v = bfs[k];
-        if (off[v + 1] == off[v] || !cut[v]) continue;
-        const int32_t r = (int32_t)reg_root.size();
-        reg_root.push_back(v);
-        // post-order of the region's internal nodes
-        std::vector<int32_t> post;
-        std::vector<std::pair<int32_t, int32_t>> st{{v, off[v]}};
-        while (!st.empty()) {
-            auto& top = st.back();
-            const int32_t u = top.first;
-            if (top.second < off[u + 1]) {
-                const int32_t c = idx[top.second++];
-                if (off[c + 1] > off[c] && !cut[c]) st.emplace_back(c, off[c]);
-            } else {
-                post.push_back(u);
-                st.pop_back();
-            }
-        }
-        for (size_t i = 0; i < post.size(); ++i) region_of[post[i]] = r;
-        int32_t nstage = 0;
-        for (size_t i = 0; i < post.size(); ++i) {
-            const int32_t u = post[i];
-            rg.node_dense.push_back(ht.dense_of[u]);
-            int32_t pslot = -1;
-            if (u != v) {
-                const int32_t par = [&] {   // parent of u inside the region
-                    for (size_t j = i + 1; j < post.size(); ++j)
-                        for (int32_t e = off[post[j]]; e < off[post[j] + 1]; ++e)
-                            if (idx[e] == u) return (int32_t)j;
-                    return (int32_t)-1;
-                }();
-                pslot = par;
-            }
-            rg.node_pslot.push_back(pslot);
-            int32_t flags = 0;
-            for (int32_t e = off[u]; e < off[u + 1]; ++e) {
-                const int32_t c = idx[e];
-                if (off[c + 1] == off[c]) {
-                    const int32_t rank = -ht.dense_of[c] - 1;
-                    if (wide[u]) rg.child.push_back((rank << 2) | 1);
-                    else {
-                        rg.stage.push_back(rank);
-                        rg.child.push_back((nstage++ << 2) | 0);
-                    }
-                } else if (cut[c]) {
-                    rg.child.push_back((ht.dense_of[c] << 2) | 3);
-                    flags |= 1;
-                } else {
-                    int32_t sl = 0;
-                    for (size_t j = 0; j < i; ++j)
-                        if (post[j] == c) sl = (int32_t)j;
-                    rg.child.push_back((sl << 2) | 2);
-                }
-            }
-            rg.node_flags.push_back(flags);
-            rg.child_off.push_back((int32_t)rg.child.size());
-        }
-        rg.node_off.push_back((int32_t)rg.node_dense.size());
-        rg.stage_off.push_back((int32_t)rg.stage.size());
-    }
-    const int32_t R = (int32_t)reg_root.size();
-    // region depth (BFS order) and height (reverse)
-    std::vector<int32_t> depth(R, 0), height(R, 0);
-    std::vector<int32_t> parent_node(N, -1);
-    for (int32_t v = 0; v < N; ++v)
-        for (int32_t e = off[v]; e < off[v + 1]; ++e) parent_node[idx[e]] = v;
-    for (int32_t r = 0; r < R; ++r) {
-        const int32_t v = reg_root[r];
-        depth[r] = v == root ? 0 : depth[region_of[parent_node[v]]] + 1;
-    }
-    for (int32_t r = R - 1; r >= 0; --r) {
-        const int32_t v = reg_root[r];
-        if (v != root) {
-            const int32_t pr = region_of[parent_node[v]];
-            height[pr] = std::max(height[pr], height[r] + 1);
-        }
-    }
-    auto bucket = [&](const std::vector<int32_t>& key, std::vector<int32_t>& offs, std::vector<int32_t>& order) {
-        int32_t levels = 0;
-        for (int32_t x : key) levels = std::max(levels, x + 1);
-        offs.assign(levels + 1, 0);
-        for (int32_t x : key) ++offs[x + 1];
-        for (int32_t k = 0; k < levels; ++k) offs[k + 1] += offs[k];
-        order.assign(key.size(), 0);
-        std::vector<int32_t> cur(offs.begin(), offs.end() - 1);
-        for (int32_t r = 0; r < (int32_t)key.size(); ++r) order[cur[key[r]]++] = r;
-    };
-    bucket(height, rg.up_level_off, rg.up_order);
-    bucket(depth, rg.down_level_off, rg.down_order);
 }
 
 }  // namespace
@@ -513,40 +364,11 @@ int pm_set_stream(pm_ctx* c, void* s) {
     return PM_OK;
 }
 
-namespace pm {
-int tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns);
-}
-
-// An experimental schedule switched on after pm_tree_upload: its structures are built by
-// uploading the same tree again, keeping the columns.
-int rebuild_tree(pm_ctx* c) {
-    if (!c->has_tree) return PM_OK;
-    const std::vector<int32_t> off = c->tree_off, idx = c->tree_idx;
-    pm_tree t{};
-    t.num_nodes = (int32_t)off.size() - 1;
-    t.child_offsets = off.data();
-    t.child_index = idx.data();
-    t.root = c->tree_root;
-    return pm::tree_upload(c, &t, true);
-}
-
 int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (!c) return PM_ERR_ARG;
-    if (option == PM_OPT_FUSED) {
-        c->fused = value != 0;
-        return c->fused && !c->built_regions ? rebuild_tree(c) : PM_OK;
-    }
     if (option == PM_OPT_VIRTUAL) {
         c->virtual_leaf_parents = value != 0;
         return PM_OK;
-    }
-    if (option == PM_OPT_BANDS) {
-        c->bands = value != 0;
-        return c->bands && !c->built_bands ? rebuild_tree(c) : PM_OK;
-    }
-    if (option == PM_OPT_CHAINS) {
-        c->chains = value != 0;
-        return c->chains && !c->built_chains ? rebuild_tree(c) : PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
         c->use_graph = value != 0;
@@ -563,11 +385,7 @@ int pm_set_profiling(pm_ctx* c, int enable) {
     return PM_OK;
 }
 
-int pm_tree_upload(pm_ctx* c, const pm_tree* t) { return pm::tree_upload(c, t, false); }
-
-// keep_columns: the same tree again (its leaf ranks and dense indices are the same), so the
-// uploaded columns and work buffers stay valid.
-int pm::tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns) {
+int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     // PM_UPLOAD_TIMING=1: host phase durations on stderr
     const bool timing = std::getenv("PM_UPLOAD_TIMING") != nullptr;
     auto t_last = std::chrono::steady_clock::now();
@@ -840,137 +658,33 @@ int pm::tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns) {
         return tail;
     };
     upload_phase("descriptors");
-    // heavy-path chains over the materialised nodes of each form (PM_OPT_CHAINS only: the
-    // experimental schedules' structures cost seconds of host time on 10^7-node trees)
-    std::vector<NodeDesc> up_chain_desc[2], down_chain_desc[2];
-    std::vector<int32_t> up_chain_off[2], down_chain_off[2];
-    for (int v = 0; v < (c->chains ? 2 : 0); ++v) {
-        const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
-        auto mat = [&](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
-        std::vector<int32_t> first(I, -1);   // next node down the chain
-        std::vector<uint8_t> live(I, 0);
-        for (int32_t d = 0; d < I; ++d) {
-            live[d] = v ? !virt[d] : 1;
-            if (mat(enc[ht.child_off[d]])) first[d] = enc[ht.child_off[d]];
-        }
-        std::vector<int32_t> rank(I, 0);
-        for (int32_t k = N - 1; k >= 0; --k) {
-            const int32_t u = bfs[k];
-            const int32_t d = ht.dense_of[u];
-            if (d < 0 || !live[d]) continue;
-            int32_t r = first[d] >= 0 ? rank[first[d]] : 0;
-            for (int32_t e = ht.child_off[d] + 1; e < ht.child_off[d + 1]; ++e)
-                if (mat(enc[e])) r = std::max(r, rank[enc[e]] + 1);
-            rank[d] = r;
-        }
-        struct Chain { int32_t bottom, top, len, rank; };
-        std::vector<Chain> chains;
-        for (int32_t d = 0; d < I; ++d) {
-            if (!live[d] || first[d] >= 0) continue;   // chains start at their bottom node
-            int32_t cur = d, len = 1;
-            while (parent_dense[cur] >= 0 && first[parent_dense[cur]] == cur) {
-                cur = parent_dense[cur];
-                ++len;
-            }
-            chains.push_back({d, cur, len, rank[cur]});
-        }
-        int32_t R = 0;
-        for (const Chain& ch : chains) R = std::max(R, ch.rank + 1);
-        auto by = [](bool asc) {
-            return [asc](const Chain& x, const Chain& y) {
-                if (x.rank != y.rank) return asc ? x.rank < y.rank : x.rank > y.rank;
-                return x.len > y.len;   // long chains dispatched first within a launch
-            };
-        };
-        for (int dir = 0; dir < 2; ++dir) {   // 0: up (bottom-up nodes), 1: down (top-down)
-            std::sort(chains.begin(), chains.end(), by(dir == 0));
-            std::vector<int32_t> nodes, coff{0}, roff(R + 1, 0);
-            for (const Chain& ch : chains) {
-                const size_t at = nodes.size();
-                for (int32_t cur = ch.bottom, k = 0; k < ch.len; ++k, cur = parent_dense[cur]) nodes.push_back(cur);
-                if (dir == 1) std::reverse(nodes.begin() + at, nodes.end());
-                coff.push_back((int32_t)nodes.size());
-                ++roff[(dir == 0 ? ch.rank : R - 1 - ch.rank) + 1];
-            }
-            for (int32_t r = 0; r < R; ++r) roff[r + 1] += roff[r];
-            (dir == 0 ? up_chain_desc[v] : down_chain_desc[v]) = make_desc(nodes, enc);
-            (dir == 0 ? up_chain_off[v] : down_chain_off[v]) = coff;
-            (dir == 0 ? ht.up_rank_off[v] : ht.down_rank_off[v]) = roff;
-        }
-    }
-
-    upload_phase("chains");
-    // bands of kBand levels and their connected pieces (see DevTree)
-    std::vector<NodeDesc> up_band_desc[2], down_band_desc[2];
-    std::vector<int32_t> up_band_lvl[2], down_band_lvl[2];
-    for (int v = 0; v < (c->bands ? 2 : 0); ++v) {   // (PM_OPT_BANDS only)
-        const std::vector<int32_t>& enc = v ? child_enc_v : ht.child_enc;
-        auto live = [&](int32_t d) { return v ? !virt[d] : true; };
-        for (int dir = 0; dir < 2; ++dir) {   // 0: up (height), 1: down (depth)
-            auto level = [&](int32_t d) {
-                return dir == 0 ? height[ht.internal_id[d]] - 1 : depth[ht.internal_id[d]];
-            };
-            // piece root: parent absent or in another band; pieces gathered by BFS over
-            // same-band children, then their nodes bucketed by level inside the band
-            int32_t B = 0;
-            for (int32_t d = 0; d < I; ++d)
-                if (live(d)) B = std::max(B, level(d) / kBand + 1);
-            std::vector<std::vector<int32_t>> roots(B);
-            for (int32_t k = 0; k < N; ++k) {
-                const int32_t d = ht.dense_of[bfs[k]];
-                if (d < 0 || !live(d)) continue;
-                const int32_t p = parent_dense[d];
-                if (p < 0 || level(p) / kBand != level(d) / kBand) roots[level(d) / kBand].push_back(d);
-            }
-            std::vector<int32_t> nodes, lvl, boff{0}, stack, mine;
-            for (int32_t b = 0; b < B; ++b) {
-                const int32_t band = dir == 0 ? b : b;   // up: band 0 first (leaves); down: root band first
-                for (int32_t r : roots[band]) {
-                    mine.clear();
-                    stack.assign(1, r);
-                    while (!stack.empty()) {
-                        const int32_t d = stack.back();
-                        stack.pop_back();
-                        mine.push_back(d);
-                        for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
-                            const int32_t x = enc[e];
-                            if (x >= 0 && !(x & kVirtualBit) && level(x) / kBand == band) stack.push_back(x);
-                        }
-                    }
-                    std::stable_sort(mine.begin(), mine.end(), [&](int32_t x, int32_t y) { return level(x) < level(y); });
-                    size_t at = 0;
-                    for (int j = 0; j <= kBand; ++j) {
-                        while (at < mine.size() && level(mine[at]) - band * kBand < j) ++at;
-                        lvl.push_back((int32_t)(nodes.size() + at));
-                    }
-                    nodes.insert(nodes.end(), mine.begin(), mine.end());
-                }
-                boff.push_back((int32_t)(lvl.size() / (kBand + 1)));
-            }
-            (dir == 0 ? up_band_desc[v] : down_band_desc[v]) = make_desc(nodes, enc);
-            (dir == 0 ? up_band_lvl[v] : down_band_lvl[v]) = lvl;
-            (dir == 0 ? ht.up_band_off[v] : ht.down_band_off[v]) = boff;
-        }
-    }
-
     const std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
     const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
     ht.num_tail_v = (int32_t)tail_desc_v.size();
 
-    Regions rg;
-    upload_phase("bands");
-    if (c->fused) build_regions(bfs, off, idx, t->root, ht, rg);   // (PM_OPT_FUSED only)
-    upload_phase("regions");
-    ht.rg_up_level_off = rg.up_level_off;
-    ht.rg_down_level_off = rg.down_level_off;
-
-    if (keep_columns) {
-        drop_graph(c);
-    } else {
-        free_work(c);
-        free_columns(c);
+    // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
+    std::vector<PartDesc> part_desc[2];
+    for (int v = 0; v < 2; ++v) {
+        const std::vector<NodeDesc>& ud = v ? up_desc_v : up_desc;
+        std::vector<int32_t>& po = v ? ht.part_off_v : ht.part_off;
+        po.assign(ud.size() + 1, 0);
+        ht.up_degree[v].assign(ud.size(), 0);
+        for (size_t k = 0; k < ud.size(); ++k) {
+            const int32_t deg = ud[k].e1 - ud[k].e0;
+            ht.up_degree[v][k] = deg;
+            const int32_t np = deg > 255 ? (deg + kPartChildren - 1) / kPartChildren : 0;
+            for (int32_t j = 0; j < np; ++j) part_desc[v].push_back(PartDesc{(int32_t)k, j, po[k] + j, 0});
+            po[k + 1] = po[k] + np;
+        }
     }
+    std::vector<NodeDesc> up_desc_p = up_desc, up_desc_vp = up_desc_v;   // pad0 = first part
+    for (size_t k = 0; k < up_desc_p.size(); ++k) up_desc_p[k].pad0 = ht.part_off[k];
+    for (size_t k = 0; k < up_desc_vp.size(); ++k) up_desc_vp[k].pad0 = ht.part_off_v[k];
+    upload_phase("parts");
+
+    free_work(c);
+    free_columns(c);
     free_tree(c->dt);
     DevTree dt;
     dt.num_internal = I;
@@ -990,53 +704,22 @@ int pm::tree_upload(pm_ctx* c, const pm_tree* t, bool keep_columns) {
         (e = upload(&dt.up_order_v, up_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_order_v, down_order_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc, down_desc, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc, up_desc, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_v, up_desc_v, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc, up_desc_p, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_v, up_desc_vp, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_chain_desc[0], up_chain_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_chain_desc[1], up_chain_desc[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_chain_desc[0], down_chain_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_chain_desc[1], down_chain_desc[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_chain_off[0], up_chain_off[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_chain_off[1], up_chain_off[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_chain_off[0], down_chain_off[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_chain_off[1], down_chain_off[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_band_desc[0], up_band_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_band_desc[1], up_band_desc[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_band_desc[0], down_band_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_band_desc[1], down_band_desc[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_band_lvl[0], up_band_lvl[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_band_lvl[1], up_band_lvl[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_band_lvl[0], down_band_lvl[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_band_lvl[1], down_band_lvl[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_node_off, rg.node_off, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_node_dense, rg.node_dense, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_node_pslot, rg.node_pslot, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_node_flags, rg.node_flags, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_child_off, rg.child_off, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_child, rg.child, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_stage_off, rg.stage_off, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_stage, rg.stage, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_up_order, rg.up_order, c->stream)) != hipSuccess ||
-        (e = upload(&dt.rg_down_order, rg.down_order, c->stream)) != hipSuccess) {
+        (e = upload(&dt.part_desc, part_desc[0], c->stream)) != hipSuccess ||
+        (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
-    dt.num_regions = (int32_t)rg.up_order.size();
     c->dt = dt;
     c->ht = std::move(ht);
     c->max_degree = 0;
     for (int32_t d = 0; d < I; ++d) c->max_degree = std::max(c->max_degree, c->ht.child_off[d + 1] - c->ht.child_off[d]);
     c->has_tree = true;
-    c->built_chains = c->chains;
-    c->built_bands = c->bands;
-    c->built_regions = c->fused;
-    c->tree_off.assign(off, off + N + 1);
-    c->tree_idx.assign(idx, idx + E);
-    c->tree_root = t->root;
     upload_phase("device upload");
     return PM_OK;
 }

@@ -33,8 +33,6 @@ constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole gra
 constexpr int kDegreeClasses = 4;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
                                   // complex, parent's simple, 3 pad (one 64-B scalar load)
-constexpr int kBand = 8;          // levels per band (PM_OPT_BANDS)
-constexpr int kBandWaves = 8;     // waves per band workgroup
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
@@ -54,6 +52,17 @@ struct alignas(64) NodeDesc {
 struct alignas(32) TailDesc {
     int32_t parent, enc, pad0, pad1;
     int32_t vl[4];
+};
+
+// Sankoff nodes of out-degree > 255: their children are cut into parts of kPartChildren,
+// counted separately into 8-bit counters (16 codes x 8 planes + the finite plane).
+constexpr int kPartChildren = 255;
+constexpr int kPartPlanes = 16 * 8 + 1;
+struct PartDesc {
+    int32_t item;     // the node's position in its up-order descriptor array
+    int32_t sub;      // children [e0 + sub * kPartChildren, ...)
+    int32_t global;   // scratch slot
+    int32_t pad;
 };
 
 struct DevTree {
@@ -83,39 +92,12 @@ struct DevTree {
     int32_t* vleaf = nullptr;
     TailDesc* tail_desc = nullptr;     // tails over child_enc
     TailDesc* tail_desc_v = nullptr;   // tails over child_enc_v
-    // heavy-path chains ([0] over child_enc, [1] over child_enc_v): the materialised
-    // internal nodes split into chains, each node's first child being the next node down
-    // its chain; descriptors bottom-up (up) / top-down (down), chain c at [off[c], off[c+1])
-    NodeDesc* up_chain_desc[2] = {nullptr, nullptr};
-    NodeDesc* down_chain_desc[2] = {nullptr, nullptr};
-    int32_t* up_chain_off[2] = {nullptr, nullptr};
-    int32_t* down_chain_off[2] = {nullptr, nullptr};
-    // height / depth bands of kBand levels: each band's connected pieces, one workgroup
-    // per (piece, tile) walking the piece's levels with workgroup barriers in between;
-    // descriptors piece by piece, level by level; piece p's level j at
-    // [lvl[p*(kBand+1)+j], lvl[p*(kBand+1)+j+1])
-    NodeDesc* up_band_desc[2] = {nullptr, nullptr};
-    NodeDesc* down_band_desc[2] = {nullptr, nullptr};
-    int32_t* up_band_lvl[2] = {nullptr, nullptr};
-    int32_t* down_band_lvl[2] = {nullptr, nullptr};
-    // subtree regions for the fused Fitch kernels (pm_fused.hip)
-    int32_t num_regions = 0;
-    int32_t* rg_node_off = nullptr;     // [R+1] into the region-node entries (post-order per region)
-    int32_t* rg_node_dense = nullptr;   // [E1] dense internal index
-    int32_t* rg_node_pslot = nullptr;   // [E1] slot of the parent inside the region, -1 = region root
-    int32_t* rg_node_flags = nullptr;   // [E1] bit 0: has children in other regions (publish final)
-    int32_t* rg_child_off = nullptr;    // [E1+1]
-    int32_t* rg_child = nullptr;        // [E2] (value << 2) | kind: 0 staged leaf, 1 direct leaf, 2 slot, 3 other region
-    int32_t* rg_stage_off = nullptr;    // [R+1]
-    int32_t* rg_stage = nullptr;        // [E3] leaf ranks staged in LDS
-    int32_t* rg_up_order = nullptr;     // [R] regions by height
-    int32_t* rg_down_order = nullptr;   // [R] regions by depth
+    // Sankoff parts of the nodes of out-degree > 255 ([0] over child_enc, [1] over child_enc_v)
+    PartDesc* part_desc = nullptr;
+    PartDesc* part_desc_v = nullptr;
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
-
-constexpr int kRegionSlots = 3;   // internal nodes per region (LDS: 4 KiB each per wave)
-constexpr int kRegionStage = 4;   // staged leaves per region (LDS: 1 KiB + 256 B each)
 
 struct HostTree {
     int32_t num_nodes = 0;
@@ -137,14 +119,10 @@ struct HostTree {
     int64_t num_virtual = 0;
     bool down_dense_v = false;            // down_order_v[k] == k (dense order = pre-order levels)
     int32_t num_tail = 0, num_tail_v = 0;
-    // chains per rank: up launches rank 0.. (chains of rank r hang only rank < r chains off
-    // their nodes), down launches in the reverse order; [variant][rank + 1] chain offsets
-    std::vector<int32_t> up_rank_off[2], down_rank_off[2];
-    // pieces per band: [variant][band + 1] piece offsets (up: bands by height from the
-    // leaves, down: by depth from the root)
-    std::vector<int32_t> up_band_off[2], down_band_off[2];
-    std::vector<int32_t> rg_up_level_off;   // [Hr+1] region post-order levels
-    std::vector<int32_t> rg_down_level_off; // [Dr+1] region pre-order levels
+    // Sankoff parts: prefix over the up-order descriptors ([I'+1]; nodes of out-degree <= 255
+    // have none) of each form, and every descriptor's out-degree ([0] plain, [1] virtual form)
+    std::vector<int32_t> part_off, part_off_v;
+    std::vector<int32_t> up_degree[2];
 };
 
 struct Timer {
@@ -165,13 +143,7 @@ struct pm_ctx {
     pm::DevTree dt;
     bool has_tree = false;
     int32_t max_degree = 0;
-    bool fused = false;               // Fitch: subtree-region kernels (PM_OPT_FUSED, experimental)
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
-    bool chains = false;              // heavy-path chain kernels instead of per-level ones (PM_OPT_CHAINS)
-    bool bands = false;               // banded level kernels (PM_OPT_BANDS)
-    bool built_chains = false, built_bands = false, built_regions = false;   // their tree structures exist
-    std::vector<int32_t> tree_off, tree_idx;   // the uploaded tree (rebuilt when an option above is enabled)
-    int32_t tree_root = -1;
 
     // column shard
     int64_t num_sites = 0;
@@ -193,6 +165,8 @@ struct pm_ctx {
     size_t cmask_bytes = 0;
     uint4* finals = nullptr;          // [I][W] synthetic generator scratch (internal sequences)
     size_t finals_bytes = 0;
+    uint32_t* sk_parts = nullptr;     // Sankoff part counters [parts][kPartPlanes][wpad]
+    size_t sk_parts_bytes = 0;
     uint4* root_final = nullptr;      // [W] the root's final codes (other finals live in the records)
     pm_mut* recs = nullptr;           // [kShards][shard_cap]
     int64_t shard_cap = 0;
@@ -227,7 +201,6 @@ void timer_end(pm_ctx* c, int cls);
 
 // kernel launchers (pm_fitch.hip / pm_sankoff.hip / pm_synth.hip)
 hipError_t launch_fitch(pm_ctx* c, bool block);
-hipError_t launch_fitch_fused(pm_ctx* c);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
 // Records of the last run, sorted by (node, site) on the device, copied to host `out`.
 hipError_t sort_records_to_host(pm_ctx* c, const std::vector<uint32_t>& counts, int64_t n, pm_mut* out);

@@ -59,9 +59,7 @@ inline dim3 block_grid(int32_t count, int32_t tiles) {
 
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
-    const NodeDesc* desc;  // Fitch: level items (chain kernels: all chains' descriptors)
-    const int32_t* chain_off;  // chain kernels: chain c's descriptors at [chain_off[c], chain_off[c+1])
-    int32_t chain_base;        // first chain of the launch
+    const NodeDesc* desc;  // level items
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;
@@ -549,9 +547,7 @@ __device__ __forceinline__ uint32_t code_less(const uint32_t* A, const uint32_t*
 }
 
 struct DownArgs {
-    const NodeDesc* desc;  // per level item (chain kernels: all chains' descriptors)
-    const int32_t* chain_off;
-    int32_t chain_base;
+    const NodeDesc* desc;  // per level item
     const TailDesc* tail;  // k_tail items
     int32_t count;
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
@@ -687,24 +683,6 @@ __device__ __forceinline__ void put_records(const Sink& sink, uint32_t& p, uint3
         }
     }
     p += nbits;
-}
-
-// Same records written at out[pos...] (count returned): the region kernels' two-pass form.
-__device__ __forceinline__ uint32_t emit_at(pm_mut* out, int64_t pos, int64_t cap, uint32_t node, uint32_t diff,
-                                            int64_t word, const uint32_t* pc, uint32_t c0, uint32_t c1,
-                                            uint32_t c2, uint32_t c3) {
-    uint32_t k = 0;
-    while (diff) {
-        const int b = __builtin_ctz(diff);
-        diff &= diff - 1;
-        const uint32_t pcode = code_at(pc[0], pc[1], pc[2], pc[3], b);
-        const uint32_t c = code_at(c0, c1, c2, c3, b);
-        const uint32_t type = pcode == 0 ? PM_MUT_NI : (c == 0 ? PM_MUT_ND : PM_MUT_NS);
-        const uint32_t site = (uint32_t)(word * 32 + b);
-        if (pos + k < cap) out[pos + k] = pm_mut{node, (site << 8) | (type << 4) | (type == PM_MUT_ND ? 0u : c)};
-        ++k;
-    }
-    return k;
 }
 
 // A leaf word for emission: its code planes L and the mask of sites where it can carry a
@@ -922,7 +900,7 @@ __device__ __forceinline__ uint4 parent_final(const DownArgs& a, int32_t parent,
     return rec_final(a.sets + ((size_t)parent * a.tiles + tile) * REC, pm, lane, a.cons, word);
 }
 
-// Any internal node's final, its own masks loaded here (tail, chain and band kernels).
+// Any internal node's final, its own masks loaded here (tail kernel).
 template <int REC>
 __device__ __forceinline__ uint4 node_final(const DownArgs& a, int32_t node, int tile, int lane, int64_t word) {
     if (node == a.root_dense) return a.root_final[word];
@@ -1134,169 +1112,6 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
     if (lane == 0) stage_cnt[wave] = 0;
     kid_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
-}
-
-// Pre-order + assignment along heavy-path chains: wave = (chain, tile), walking the
-// chain top-down with the parent's final carried in registers (only the chain top reads
-// its parent's final, written by an earlier launch).  Each step is k_down's body; the
-// records of successive steps share the wave's LDS stage, flushed with one global atomic
-// once it is half full (a step that overflows the stage is redone straight into global).
-template <Mode M, bool AP>
-__global__ __launch_bounds__(kBlock) void k_down_chain(DownArgs a) {
-    __shared__ pm_mut stage[kWavesPerBlock][kStage];
-    __shared__ uint32_t stage_cnt[kWavesPerBlock];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int32_t item = blockIdx.x * kWavesPerBlock + wave;
-    if (item >= a.count) return;
-    if (lane == 0) stage_cnt[wave] = 0;
-    const int32_t chain = a.chain_base + item;
-    const int32_t s0 = a.chain_off[chain], s1 = a.chain_off[chain + 1];
-    const int tile = blockIdx.y;
-    const int64_t word = (int64_t)tile * kWave + lane;
-    const uint32_t valid = valid_mask(a, word);
-    uint32_t pc[4];
-    {
-        const int32_t top_parent = a.desc[s0].parent;
-        const uint4 q = top_parent < 0 ? a.cons[word]
-                                       : node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, top_parent, tile,
-                                                                                                  lane, word);
-        pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
-    }
-    uint32_t flushes = 0;
-    for (int32_t k = s0; k < s1; ++k) {
-        const NodeDesc& d = a.desc[k];
-        const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-        const bool is_root = d.parent < 0;
-        constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
-        const size_t rec = (size_t)n * a.tiles + tile;
-        const RecMask m = rec_mask(a.cmask, rec);
-        uint4* const p = a.sets + rec * REC;
-        const bool dirty = is_root || ((m.d >> lane) & 1ull);
-        Kid kids[2];
-        kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
-        if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
-        uint32_t own[16], z1[16], F[4], pres;
-        if constexpr (M == Mode::kSankoff) load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
-        else load_fitch_set(p, m, a.cons, lane, word, own);
-        resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
-        store_final(a, is_root, p, m, lane, word, F);
-        if (is_root) {
-            for (int b = 0; b < 32; ++b) {
-                const int64_t site = word * 32 + b;
-                if (site < a.sites)
-                    a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
-            }
-        }
-        const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-        const uint32_t before = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-        node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
-        uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-        if (cnt > kStage) {   // this step overflowed the stage: its records go straight to global
-            const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u + k) % kShards;
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], cnt - before);
-            base = __shfl(base, 0, 64);
-            if (lane == 0) stage_cnt[wave] = 0;
-            node_records<M, AP>(a, GlobalSink{a.recs + (size_t)shard * a.shard_cap, (int64_t)base, a.shard_cap,
-                                              &stage_cnt[wave]},
-                                n, e0, e1, kids, word, valid, pc, F, self_diff);
-            if (lane == 0) stage_cnt[wave] = before;
-            cnt = before;
-        }
-        if (cnt > kStage / 2 || (k + 1 == s1 && cnt > 0)) {
-            const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u + 977u * flushes++) % kShards;
-            uint32_t base;
-            pm_mut* out;
-            flush_stage(a, stage[wave], cnt, shard, lane, item, tile, base, out);
-            if (lane == 0) stage_cnt[wave] = 0;
-        }
-        pc[0] = F[0]; pc[1] = F[1]; pc[2] = F[2]; pc[3] = F[3];
-    }
-}
-
-// Pre-order + assignment over a band of kBand depth levels: workgroup = (piece, tile),
-// its waves share each level's nodes and meet at a workgroup barrier before the next level
-// (finals written by one wave are read by another wave of the same workgroup, so the
-// barrier's workgroup-scope ordering suffices).  Each node is k_down's body; records go
-// through the wave's LDS stage as in k_down_chain.
-template <Mode M, bool AP>
-__global__ __launch_bounds__(kBandWaves * kWave) void k_down_band(DownArgs a) {
-    __shared__ pm_mut stage[kBandWaves][kStage];
-    __shared__ uint32_t stage_cnt[kBandWaves];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (lane == 0) stage_cnt[wave] = 0;
-    const int32_t piece = a.chain_base + blockIdx.x;
-    const int32_t* lv = a.chain_off + (size_t)piece * (kBand + 1);
-    const int tile = blockIdx.y;
-    const int64_t word = (int64_t)tile * kWave + lane;
-    const uint32_t valid = valid_mask(a, word);
-    uint32_t flushes = 0;
-    for (int j = 0; j < kBand; ++j) {
-        const int32_t lb = lv[j], le = lv[j + 1];
-        for (int32_t k = lb + wave; k < le; k += kBandWaves) {
-            const NodeDesc& d = a.desc[k];
-            const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-            const bool is_root = d.parent < 0;
-            uint32_t pc[4];
-            {
-                const uint4 q = is_root ? a.cons[word]
-                                        : node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, d.parent, tile,
-                                                                                                   lane, word);
-                pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
-            }
-            constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
-            const size_t rec = (size_t)n * a.tiles + tile;
-            const RecMask m = rec_mask(a.cmask, rec);
-            uint4* const p = a.sets + rec * REC;
-            const bool dirty = is_root || ((m.d >> lane) & 1ull);
-            Kid kids[2];
-            kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
-            if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
-            uint32_t own[16], z1[16], F[4], pres;
-            if constexpr (M == Mode::kSankoff) load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
-            else load_fitch_set(p, m, a.cons, lane, word, own);
-            resolve_final<M>(a, is_root, word, own, z1, pc, F, pres);
-            store_final(a, is_root, p, m, lane, word, F);
-            if (is_root) {
-                for (int b = 0; b < 32; ++b) {
-                    const int64_t site = word * 32 + b;
-                    if (site < a.sites)
-                        a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
-                }
-            }
-            const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-            const uint32_t before = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-            node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
-            uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-            if (cnt > kStage) {   // this node overflowed the stage: its records go straight to global
-                const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + k) % kShards;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], cnt - before);
-                base = __shfl(base, 0, 64);
-                if (lane == 0) stage_cnt[wave] = 0;
-                node_records<M, AP>(a, GlobalSink{a.recs + (size_t)shard * a.shard_cap, (int64_t)base, a.shard_cap,
-                                                  &stage_cnt[wave]},
-                                    n, e0, e1, kids, word, valid, pc, F, self_diff);
-                if (lane == 0) stage_cnt[wave] = before;
-                cnt = before;
-            }
-            if (cnt > kStage / 2) {
-                const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + wave * 131u + 977u * flushes++) % kShards;
-                uint32_t base;
-                pm_mut* out;
-                flush_stage(a, stage[wave], cnt, shard, lane, piece, tile, base, out);
-                if (lane == 0) stage_cnt[wave] = 0;
-            }
-        }
-        __syncthreads();
-    }
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-    if (cnt > 0) {
-        const uint32_t shard = (uint32_t)(piece * 31u + tile * 7919u + wave * 131u + 977u * flushes) % kShards;
-        uint32_t base;
-        pm_mut* out;
-        flush_stage(a, stage[wave], cnt, shard, lane, piece, tile, base, out);
-    }
 }
 
 }  // namespace pm

@@ -231,6 +231,137 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
+// Nodes of any out-degree above 255 (src/fitchSankoff.cpp:391-402 sums over every child,
+// whatever their number): the children are cut into parts of kPartChildren; one wave per
+// (part, tile) counts its part into 8-bit bit-sliced counters (k_sankoff_part) and writes
+// them to scratch; one wave per (node, tile) then adds the parts code by code into BW-bit
+// counters and keeps the running maximum with the codes at the maximum (Z0) and one below
+// it (Z1) as it goes (k_sankoff_merge), so no 16 x BW counter file is ever held.
+__global__ __launch_bounds__(kBlock) void k_sankoff_part(UpArgs a, const PartDesc* parts, int32_t nparts,
+                                                         uint32_t* scratch) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t pi;
+    int tile;
+    wave_item(wave, a.tiles, pi, tile);
+    if (pi >= nparts) return;
+    const PartDesc pd = parts[pi];
+    const NodeDesc& d = a.desc[pd.item];
+    const int32_t lo = d.e0 + pd.sub * kPartChildren, hi = min(d.e1, lo + kPartChildren);
+    const int64_t word = (int64_t)tile * kWave + lane;
+    uint32_t cnt[16][8];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) cnt[v][b] = 0;
+    uint32_t finite = 0;
+    for (int32_t base = lo; base < hi; base += kWave) {
+        const int32_t my = base + lane;
+        const int32_t enc = my < hi ? a.child_enc[my] : 0;
+        const int4 vl = my < hi && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+                                                                   : make_int4(-1, -1, -1, -1);
+        const int cntc = min(kWave, hi - base);
+        for (int k = 0; k < cntc; k += 2) {
+            uint32_t z0[16], z1[16];
+            const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
+            child_z0(a, c0, __builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), tile, lane, word, z0);
+            const bool two = k + 1 < cntc;
+            if (two) {
+                const int32_t c1 = __builtin_amdgcn_readlane(enc, k + 1);
+                child_z0(a, c1, __builtin_amdgcn_readlane(vl.x, k + 1), __builtin_amdgcn_readlane(vl.y, k + 1), tile,
+                         lane, word, z1);
+            }
+            count_child<8>(cnt, finite, z0);
+            if (two) count_child<8>(cnt, finite, z1);
+        }
+    }
+    uint32_t* out = scratch + (size_t)pd.global * kPartPlanes * a.wpad + word;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) out[(size_t)(v * 8 + b) * a.wpad] = cnt[v][b];
+    out[(size_t)128 * a.wpad] = finite;
+}
+
+template <int BW>
+__global__ __launch_bounds__(kBlock) void k_sankoff_merge(UpArgs a, const uint32_t* scratch) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
+    if (item >= a.count) return;
+    const NodeDesc& d = a.desc[item];
+    const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
+    const int32_t p0 = d.pad0, np = (e1 - e0 + kPartChildren - 1) / kPartChildren;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint32_t* base = scratch + (size_t)p0 * kPartPlanes * a.wpad + word;
+    uint32_t finite = 0;
+    for (int32_t p = 0; p < np; ++p) finite |= base[((size_t)p * kPartPlanes + 128) * a.wpad];
+    uint32_t M[BW], z0[16], z1[16];
+#pragma unroll
+    for (int b = 0; b < BW; ++b) M[b] = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) z0[v] = z1[v] = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t acc[BW];
+#pragma unroll
+        for (int b = 0; b < BW; ++b) acc[b] = 0;
+        for (int32_t p = 0; p < np; ++p) {
+            const uint32_t* q = base + ((size_t)p * kPartPlanes + v * 8) * a.wpad;
+            uint32_t x[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) x[b] = q[(size_t)b * a.wpad];
+            uint32_t carry = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t s = acc[b] ^ x[b] ^ carry;
+                carry = (acc[b] & x[b]) | (carry & (acc[b] ^ x[b]));
+                acc[b] = s;
+            }
+#pragma unroll
+            for (int b = 8; b < BW; ++b) {
+                const uint32_t s = acc[b] ^ carry;
+                carry &= acc[b];
+                acc[b] = s;
+            }
+        }
+        // compare the code's count c with the running maximum M: c > M, c == M, c == M + 1,
+        // and c == M - 1 (as c + 1 == M)
+        uint32_t gt = 0, eqs = ~0u, cy_m = ~0u, cy_c = ~0u, eqp1 = ~0u, eqm1 = ~0u;
+#pragma unroll
+        for (int b = BW - 1; b >= 0; --b) {
+            gt |= eqs & acc[b] & ~M[b];
+            eqs &= ~(acc[b] ^ M[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < BW; ++b) {
+            const uint32_t mp1 = M[b] ^ cy_m, cp1 = acc[b] ^ cy_c;
+            cy_m &= M[b];
+            cy_c &= acc[b];
+            eqp1 &= ~(acc[b] ^ mp1);
+            eqm1 &= ~(cp1 ^ M[b]);
+        }
+        // new maximum: Z1 = the old Z0 if it is one below, else empty; Z0 = {v}.
+        // equal: v joins Z0; one below: v joins Z1
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint32_t nz1 = bsel(gt, eqp1 & z0[u], z1[u] | (u == v ? eqm1 : 0u));
+            z0[u] = bsel(gt, u == v ? ~0u : 0u, z0[u] | (u == v ? eqs : 0u));
+            z1[u] = nz1;
+        }
+#pragma unroll
+        for (int b = 0; b < BW; ++b) M[b] = bsel(gt, acc[b], M[b]);
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        z0[v] &= finite;
+        z1[v] &= finite;
+    }
+    uint64_t rx, rs;
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
+}
+
 }  // namespace
 
 hipError_t launch_sankoff(pm_ctx* c, bool block) {
@@ -239,7 +370,6 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const int32_t tiles = (c->words + kWave - 1) / kWave;
     const int64_t wpad = (int64_t)tiles * kWave;
     const int H = (int)ht.up_level_off.size() - 1;
-    if (c->max_degree > 4095) return hipErrorNotSupported;   // 12-bit counters cover 4095 children
 
     // nucleotide Sankoff evaluates leaf-parents of one or two leaves inline, like Fitch
     const bool virt = !block && c->virtual_leaf_parents;
@@ -247,6 +377,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const NodeDesc* up_desc = virt ? dt.up_desc_v : dt.up_desc;
     const NodeDesc* down_desc = virt ? dt.down_desc_v : dt.down_desc;
     const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
+    const std::vector<int32_t>& part_off = virt ? ht.part_off_v : ht.part_off;
+    const PartDesc* parts = virt ? dt.part_desc_v : dt.part_desc;
     const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
     UpArgs up{};
     up.child_off = dt.child_off;
@@ -277,7 +409,17 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, c->stream, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
             else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL((k_sankoff_up<12, false>), grid, dim3(kBlock), 0, c->stream, up);
+            else {   // more than 255 children: parts, then the merge
+                const int32_t p0 = part_off[b], np = part_off[e] - p0;
+                int32_t widest = 0;
+                for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[virt][i]);
+                UpArgs pa = up;
+                pa.desc = up_desc;   // parts name their node by its global up-order position
+                hipLaunchKernelGGL(k_sankoff_part, wave_grid(np, tiles), dim3(kBlock), 0, c->stream, pa, parts + p0, np,
+                                   c->sk_parts);
+                if (widest < (1 << 16)) hipLaunchKernelGGL(k_sankoff_merge<16>, grid, dim3(kBlock), 0, c->stream, up, c->sk_parts);
+                else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, c->stream, up, c->sk_parts);
+            }
             timer_end(c, 0);
         }
     }

@@ -57,17 +57,12 @@ def _random_columns(rng, leaves, sites, absent_frac=0.1, gap=0.2):
     return codes, present
 
 
-VARIANTS = ["virtual", "plain", "regions", "chains", "plain-chains", "bands", "plain-bands"]
+VARIANTS = ["virtual", "plain"]
 
 
 def _variant(engine, variant):
-    """virtual / plain: per-level kernels with or without virtual leaf-parents; chains /
-    plain-chains: the same over heavy-path chains; bands / plain-bands: over 8-level bands;
-    regions: LDS subtree regions."""
-    engine.set_fused(variant == "regions")
-    engine.set_virtual(variant in ("virtual", "chains", "bands"))
-    engine.set_chains(variant in ("chains", "plain-chains"))
-    engine.set_bands(variant in ("bands", "plain-bands"))
+    """virtual / plain: per-level kernels with or without virtual leaf-parents."""
+    engine.set_virtual(variant == "virtual")
 
 
 def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant="virtual"):

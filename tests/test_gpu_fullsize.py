@@ -1,5 +1,5 @@
-"""Parity at the benchmark's full sizes (BASELINE.json north_star N*: 1M leaves x 30k sites,
-random-join tree T1; C3: 100k leaves x 30k sites, SARS-like tree T2; one rank's shard of C4,
+"""Parity at the benchmark's full sizes (BASELINE.json C2: 4k leaves x 15k sites; north_star
+N*: 1M leaves x 30k sites, random-join tree T1; C3: 100k leaves x 30k sites, SARS-like tree T2; one rank's shard of C4,
 8M leaves x 3 750 sites -- SURVEY.md §8d).
 
 The oracle cannot walk every column of these in seconds, so each run is checked by
@@ -19,6 +19,9 @@ from _trees import names_for
 pytestmark = pytest.mark.gpu
 
 CONFIGS = {
+    # C2 (RSV-like, BASELINE.json config 2): 4k leaves x 15k sites -- ragged last word
+    # (15 000 = 468 x 32 + 24) and 8 tiles, the last one partial
+    "c2": (panman_amd.random_join_tree, 4096, 15_000),
     "nstar": (panman_amd.random_join_tree, 1_000_000, 30_000),
     "c3": (panman_amd.sars_like_tree, 100_000, 30_000),
     # C4 (8M leaves x 30k sites over 8 GPUs): one rank's column shard of 3 750 sites

@@ -99,9 +99,10 @@ def test_msa_driver_m2_vs_oracle(oracle, with_ref):
 
 
 @pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
-@pytest.mark.parametrize("width", [16, 300, 1500])
+@pytest.mark.parametrize("width", [16, 300, 1500, 5000, 20000])
 def test_star_polytomy_vs_oracle(engine, oracle, mode, width):
-    """One node with `width` children (SARS-like trees have nodes with thousands)."""
+    """One node with `width` children (SARS-like trees have nodes with thousands; the
+    reference sums over any number of children, src/fitchSankoff.cpp:371-402)."""
     rng = np.random.default_rng(width)
     n = width + 3
     # root(0) -> [star(1), leaf n-1]; star -> leaves 2..width+1
@@ -150,3 +151,49 @@ def test_sankoff_sars_like_tree_vs_oracle(engine, oracle):
     sel = got[(got[:, 1] >= sample.start) & (got[:, 1] < sample.stop)]
     assert sel.shape == want.shape and (sel == want).all()
     assert (rootc[sample] == want_root).all()
+
+
+def _attach_star(off, idx, parent, width):
+    """A new internal node with `width` new leaf children hung under `parent`."""
+    n0 = off.shape[0] - 1
+    kids = [list(idx[off[i]:off[i + 1]]) for i in range(n0)]
+    star = n0
+    kids[parent].append(star)
+    kids.append(list(range(n0 + 1, n0 + 1 + width)))
+    kids += [[] for _ in range(width)]
+    off2 = np.zeros(len(kids) + 1, np.int32)
+    flat = []
+    for i, k in enumerate(kids):
+        flat += k
+        off2[i + 1] = len(flat)
+    return off2, np.array(flat, np.int32)
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_sars_like_tree_with_10k_polytomy_vs_oracle(engine, oracle, mode):
+    """SURVEY.md §8d T2 tree plus one node with 10 000 children (the node-degree range of
+    real SARS-CoV-2 trees), bit-exact against the oracle in both modes."""
+    rng = np.random.default_rng(10_000)
+    off, idx, root = panman_amd.sars_like_tree(3000, seed=4)
+    hang = int(idx[off[root]:off[root + 1]][0])
+    hang = hang if off[hang + 1] > off[hang] else root
+    off, idx = _attach_star(off, idx, hang, 10_000)
+    n = off.shape[0] - 1
+    leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
+    sites = 161
+    codes, present = _random_columns(rng, len(leaf_ids), sites, absent_frac=0.05)
+    codes[rng.random(codes.shape) < 0.5] = 2   # a majority state
+    cons = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=sites)
+    node_row = np.full(n, -1, np.int32)
+    for r, lid in enumerate(leaf_ids):
+        if present[r]:
+            node_row[lid] = r
+    engine.tree_upload(off, idx, root)
+    engine.leaves_upload(codes, node_row)
+    engine.sites_upload(cons)
+    engine.run(mode)
+    got = engine.mutations()
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, None,
+                                            algo=mode, threads=8, with_root=True)
+    assert got.shape == want.shape and (got == want).all()
+    assert (engine.site_results()[1] == want_root).all()
