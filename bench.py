@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--leaves", type=int, default=1_000_000, help="leaves per GPU")
     p.add_argument("--sites", type=int, default=30_000, help="alignment columns in total")
-    p.add_argument("--cpu-sites", type=int, default=48, help="columns timed on the CPU baseline")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-sites", type=int, default=0,
+                   help="columns timed on the all-core CPU baseline (0: 2 per host thread, at least 512)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every core this process may use)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e", action="store_true",
                    help="also time the end-to-end path (H2D of the packed leaf matrix, the run, D2H of "
@@ -57,6 +58,9 @@ def parse():
     p.add_argument("--replay-blocks", type=int, default=500)
     p.add_argument("--replay-block-len", type=int, default=10_000)
     p.add_argument("--cpu-leaves", type=int, default=128, help="leaves replayed on the CPU baseline (~10 s)")
+    p.add_argument("--with", dest="with_", default="sankoff,replay,e2e",
+                   help="secondary blocks in the default run's line: comma list of sankoff (N* Sankoff "
+                        "line), replay (C5 FASTA replay line), e2e (PCIe-inclusive rate), or none")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     a = p.parse_args()
@@ -81,6 +85,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    extra = set() if args.with_ == "none" else set(args.with_.split(","))
 
     L = args.leaves * world
     S = args.sites
@@ -92,7 +97,6 @@ def main():
     else:
         off, idx, root = panman_amd.sars_like_tree(L, seed=1)
     n_nodes = off.shape[0] - 1
-    n_int = n_nodes - L
     log(rank, f"[bench] tree: {L} leaves, {n_nodes} nodes ({time.time() - t0:.1f}s)")
 
     eng = panman_amd.Engine(local)
@@ -102,18 +106,110 @@ def main():
     eng.synth_columns(lo, s_local, seed=2)
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
+    gather = "none (1 GPU)"
+    if world > 1:   # the product's own RCCL communicator (pm_rccl.hip); torch only ships the id
+        box = [panman_amd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        try:
+            eng.comm_init_rank(box[0], world, rank)
+            ok = 1
+        except panman_amd.PanmanError as exc:
+            print(f"[bench] rank {rank}: pm_comm_init_rank failed ({exc})", file=sys.stderr, flush=True)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather = "pm_run_gather (library RCCL communicator)" if flag.item() else \
+            "torch.distributed all_gather (library communicator failed to initialise)"
+    ctx = dict(world=world, rank=rank, L=L, S=S, lo=lo, s_local=s_local, n_nodes=n_nodes,
+               lib_gather=gather.startswith("pm_run_gather"))
 
+    mode = panman_amd.MODE_FITCH if args.mode == "fitch" else panman_amd.MODE_SANKOFF
+    main_block = parsimony_block(args, eng, mode, ctx)
+    secondary = {}
+    if mode == panman_amd.MODE_FITCH and "sankoff" in extra:
+        log(rank, f"[bench] secondary: Sankoff on the same workload ({time.time() - t0:.1f}s)")
+        secondary["sankoff"] = parsimony_block(args, eng, panman_amd.MODE_SANKOFF, ctx)
+        eng.run(mode)   # leave the context as the main line ran it (cpu-baseline parity sample)
+        torch.cuda.synchronize()
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        log(rank, f"[bench] CPU baseline ({time.time() - t0:.1f}s)")
+        cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode)
+    e2e = None
+    if rank == 0 and world == 1 and (args.e2e or "e2e" in extra):
+        log(rank, f"[bench] end to end ({time.time() - t0:.1f}s)")
+        e2e = end_to_end(eng, L, S, n_nodes, mode)
+    eng.close()
+    del eng
+    torch.cuda.empty_cache()
+    if world == 1 and "replay" in extra:
+        log(rank, f"[bench] secondary: C5 replay ({time.time() - t0:.1f}s)")
+        secondary["replay"] = replay_block(args, world, rank, local)
+
+    if rank == 0:
+        out = {
+            "metric": f"Fitch-Sankoff site*node updates/sec ({args.mode} mode)",
+            "value": main_block["value"],
+            "unit": "site*node updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": main_block["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 bit-planes (16-bit one-hot state sets)" if mode == panman_amd.MODE_FITCH
+            else "u32 bit-planes (Z0/Z1 optimal-code sets, exact unit-cost Sankoff)",
+            "data": f"synthetic (seeded on-device tree-evolved columns, {args.tree} tree)",
+            "config": {
+                "workload": (f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)"
+                             if args.tree == "random-join" else
+                             f"{args.mode}: {L} leaves x {S} sites sars-like tree (T2; C3 at 100k leaves)"),
+                "tree": args.tree,
+                "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
+                "parallelism": f"column shards x{world}, one all-gather of per-site score/root",
+                "gather": gather,
+                "mutations_total": main_block["mutations_total"],
+                "launch": ("hipGraph replay" if args.graph else "eager") + ", per-level kernels",
+            },
+            "roofline": main_block["roofline"],
+            "cpu_baseline": cpu,
+            "parity_sample": parity,
+            "end_to_end": e2e,
+            "secondary": {k: {kk: v[kk] for kk in ("value", "unit", "ms_per_step", "metric", "roofline",
+                                                   "config", "cpu_baseline", "parity_sample")
+                              if kk in v}
+                          for k, v in secondary.items()} or None,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def parsimony_block(args, eng, mode, ctx):
+    """Warm up, time exactly `steps` steps of `mode` (barrier + synchronize on both sides,
+    max over ranks), then the per-kernel roofline of the dominant kernel."""
+    world, rank, L, S, s_local, n_nodes = (ctx[k] for k in ("world", "rank", "L", "S", "s_local", "n_nodes"))
+    # per-site (score, root code) of every site of the job, on every rank
+    score_all = torch.zeros(S, dtype=torch.int32, device="cuda")
+    root_all = torch.zeros(S, dtype=torch.uint8, device="cuda")
     score_loc = torch.zeros(s_local, dtype=torch.int32, device="cuda")
     root_loc = torch.zeros(s_local, dtype=torch.uint8, device="cuda")
 
-    mode = panman_amd.MODE_FITCH if args.mode == "fitch" else panman_amd.MODE_SANKOFF
-
     def step():
-        eng.run(mode)
-        eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
-        if world > 1:
+        if world > 1 and ctx["lib_gather"]:   # shard run + ONE RCCL all-gather inside the library
+            eng.run_gather(mode, S, ctx["lo"], score_all.data_ptr(), root_all.data_ptr())
+        elif world > 1:
+            eng.run(mode)
+            eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
             gather_site_results(score_loc, root_loc, S)
+        else:
+            eng.run(mode)
+            eng.site_results_device(score_all.data_ptr(), root_all.data_ptr())
 
+    eng.set_graph(False)
     for _ in range(max(1, args.warmup)):
         step()
     muts = eng.mutation_count()   # sizes the record buffers (re-runs once if a shard overflowed)
@@ -141,6 +237,7 @@ def main():
         torch.cuda.synchronize()
     ms, launches = eng.kernel_times(3)
     eng.set_profiling(False)
+    design = eng.design_bytes()   # counted from the last run's record masks (untimed)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -154,40 +251,53 @@ def main():
     updates = float(S) * n_nodes * args.steps
     value = updates / elapsed
     ms_step = elapsed * 1e3 / args.steps
+    roofline = roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank)
+    name = "fitch" if mode == panman_amd.MODE_FITCH else "sankoff"
+    return {"metric": f"Fitch-Sankoff site*node updates/sec ({name} mode)", "value": value,
+            "unit": "site*node updates/s", "ms_per_step": ms_step, "mutations_total": muts_total,
+            "roofline": roofline,
+            "config": {"workload": f"{name}: {L} leaves x {S} sites ({args.tree} tree)", "sites_per_gpu": s_local}}
 
-    # Roofline of the dominant kernel (SURVEY.md §8d contract bytes, per site of this shard):
-    #   post-order  0.5 L (leaf codes) + 2 I (set write) + 2 (I-1) (set read by parent)
-    #   pre-order   2 I (set read) + 0.5 I (final write) + 0.5 (N-1) (parent final read)
-    #               + 0.5 L (leaf re-read) + 8 B per emitted mutation record
-    if mode == panman_amd.MODE_FITCH:
-        up_bytes = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1))
-        down_bytes = s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
-        names = ("k_fitch_up", "k_down<Fitch>")
-        prof_names = {"k_fitch_up": "k_fitch_up", "k_down<Fitch>": "k_down"}
-    else:
-        # this layout's Sankoff state: Z0 + Z1 planes (4 B/site), parent reads Z0 (2 B/site);
-        # the survey's 16 x u16 cost-vector model (1.5 L + 97 I) is reported beside it
-        up_bytes = s_local * (0.5 * L + 4.0 * n_int + 2.0 * (n_int - 1))
-        down_bytes = s_local * (4.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
-        names = ("k_sankoff_up", "k_down<Sankoff>")
-        prof_names = {"k_sankoff_up": "k_sankoff_up", "k_down<Sankoff>": "k_down"}
+
+def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
+    """Roofline of the dominant kernel.  `achieved` = the bytes THIS design must move per
+    launch (pm_design_bytes: leaf words, compressed records written and read, compact
+    finals, dirty-lane leaf words, 8 B per record -- counted from the run's record masks)
+    / the kernel's average launch time (HIP events on the launch stream).  `traffic` = HBM
+    bytes per launch from the rocprofv3 PMC passes committed under profiles/.  The SURVEY
+    §8d state-through-memory contract (2-B sets per node) is kept as
+    `contract_effective_GBs` only: this layout beats that model, so it is not a roofline."""
+    L, s_local, n_nodes = ctx["L"], ctx["s_local"], ctx["n_nodes"]
+    n_int = n_nodes - L
+    steps = max(1, args.steps)
+    fitch = mode == panman_amd.MODE_FITCH
+    names = ("k_fitch_up", "k_down<Fitch>") if fitch else ("k_sankoff_up", "k_down<Sankoff>")
+    prof_names = {names[0]: names[0], names[1]: "k_down"}
+    key = "fitch" if fitch else "sankoff"
     classes = {
-        names[0]: (ms[0] / args.steps, launches[0] / max(1, args.steps), up_bytes),
-        names[1]: (ms[1] / args.steps, launches[1] / max(1, args.steps), down_bytes),
+        names[0]: (ms[0] / steps, launches[0] / steps, design["up"]),
+        names[1]: (ms[1] / steps, launches[1] / steps, design["down"]),
     }
     dom = max(classes, key=lambda k: classes[k][0])
     dms, dl, dbytes = classes[dom]
     achieved = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
-    # PMC-derived HBM bytes per launch of the same kernel on the same workload, if profiled
-    # (tools/pmc_traffic.py; rocprofv3 summaries live in profiles/)
-    traffic = None
+    traffic_all = {}
     if os.path.exists(args.traffic):
         try:
-            traffic = json.load(open(args.traffic)).get(prof_names[dom], {}).get(f"{args.mode}:{L}x{s_local}")
+            tj = json.load(open(args.traffic))
+            for k, pn in prof_names.items():
+                traffic_all[k] = tj.get(pn, {}).get(f"{key}:{L}x{s_local}")
         except (OSError, ValueError):
-            traffic = None
-    per_launch = dbytes / dl if dl else 0.0
-    roofline = {
+            traffic_all = {}
+    traffic = traffic_all.get(dom)
+    if fitch:   # SURVEY.md §8d contract: 2-B sets through memory
+        contract = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1)) + \
+            s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
+    else:       # 16 x u16 cost vectors
+        contract = s_local * (1.5 * L + 97.0 * n_int)
+    step_design = design["up"] + design["down"] + design["score"]
+    kernel_launch_s = dms / dl * 1e-3 if dl else 0.0
+    out = {
         "bound": "hbm",
         "kernel": dom,
         "achieved": round(achieved, 1),
@@ -195,85 +305,34 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        # measured HBM bytes (PMC) per launch / launch time: the bandwidth actually drawn.
-        # `achieved` uses the SURVEY §8d state-through-memory byte model, which this layout
-        # beats (compressed set records, virtual leaf-parents), so frac can exceed 1.
-        "traffic_GBs": round(traffic / (dms / dl * 1e-3) / 1e9, 1) if traffic and dl and dms else None,
-        "traffic_frac": round(traffic / (dms / dl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic and dl and dms else None,
-        "algorithmic_bytes_per_launch": per_launch,
+        "bytes_model": "pm_design_bytes: bytes this record layout must move (16-B lane granularity)",
+        "design_bytes_per_launch": dbytes / dl if dl else None,
+        "traffic_over_design": round(traffic / (dbytes / dl), 3) if traffic and dl and dbytes else None,
+        "traffic_GBs": round(traffic / kernel_launch_s / 1e9, 1) if traffic and kernel_launch_s else None,
+        "traffic_frac": round(traffic / kernel_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and kernel_launch_s else None,
         "avg_launch_ms": round(dms / dl, 4) if dl else None,
         "launches_per_step": dl,
         "kernel_ms_per_step": round(dms, 3),
         "other_kernels_ms_per_step": {k: round(v[0], 3) for k, v in classes.items() if k != dom},
-        "score_kernel_ms_per_step": round(ms[2] / args.steps, 3),
-        "pipeline_effective_GBs": round((up_bytes + down_bytes) / (ms_step * 1e-3) / 1e9, 1),
+        "score_kernel_ms_per_step": round(ms[2] / steps, 3),
+        "step_design_bytes": step_design,
+        "step_design_GBs": round(step_design / (ms_step * 1e-3) / 1e9, 1),
+        "floor_bytes": design["floor"],
+        "floor_note": "0.5 B per leaf-site (leaf codes read once) + 8 B per mutation record",
+        "design_over_floor": round(step_design / design["floor"], 3),
+        "floor_GBs": round(design["floor"] / (ms_step * 1e-3) / 1e9, 1),
+        "contract_bytes": contract,
+        "contract_effective_GBs": round(contract / (ms_step * 1e-3) / 1e9, 1),
     }
-    if mode == panman_amd.MODE_SANKOFF:
-        roofline["survey_contract_GBs"] = round(s_local * (1.5 * L + 97.0 * n_int) / (ms_step * 1e-3) / 1e9, 1)
-
-    copy_gbs = hbm_copy_bandwidth() if rank == 0 else None
-    roofline["measured_copy_GBs"] = copy_gbs
-    roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
-
-    cpu = None
-    parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode)
-    e2e = None
-    if rank == 0 and world == 1 and args.e2e:
-        e2e = end_to_end(eng, L, S, n_nodes, mode)
-
-    if rank == 0:
-        out = {
-            "metric": f"Fitch-Sankoff site*node updates/sec ({args.mode} mode)",
-            "value": value,
-            "unit": "site*node updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32 bit-planes (16-bit one-hot state sets)" if mode == panman_amd.MODE_FITCH
-            else "u32 bit-planes (Z0/Z1 optimal-code sets, exact unit-cost Sankoff)",
-            "data": f"synthetic (seeded on-device tree-evolved columns, {args.tree} tree)",
-            "config": {
-                "workload": (f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)"
-                             if args.tree == "random-join" else
-                             f"{args.mode}: {L} leaves x {S} sites sars-like tree (T2; C3 at 100k leaves)"),
-                "tree": args.tree,
-                "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
-                "parallelism": f"column shards x{world}, RCCL all-gather of per-site score/root",
-                "mutations_total": muts_total,
-                "launch": ("hipGraph replay" if args.graph else "eager") + ", per-level kernels",
-            },
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "parity_sample": parity,
-            "end_to_end": e2e,
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def hbm_copy_bandwidth(gib: int = 4, reps: int = 10) -> float:
-    """Device-to-device copy rate (read + write bytes / s) of a `gib` GiB buffer: the
-    achievable-bandwidth reference beside the 8 TB/s spec."""
-    n = gib << 30
-    a = torch.empty(n, dtype=torch.uint8, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        b.copy_(a)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    del a, b
-    torch.cuda.empty_cache()
-    return round(2.0 * n * reps / dt / 1e9, 1)
+    if all(traffic_all.get(k) for k in names):
+        step_traffic = sum(traffic_all[k] * classes[k][1] for k in names)
+        out["step_traffic_bytes"] = step_traffic
+        out["traffic_over_floor"] = round(step_traffic / design["floor"], 3)
+    copy_gbs = round(panman_amd.stream_copy_rate(torch.cuda.current_device()), 1) if rank == 0 else None
+    out["measured_copy_GBs"] = copy_gbs
+    out["measured_copy_kernel"] = "k_stream_copy (pm_measure.hip): 16 B per lane, 4 loads in flight, 4 GiB"
+    out["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
+    return out
 
 
 def end_to_end(eng, L, S, n_nodes, mode):
@@ -313,22 +372,39 @@ def end_to_end(eng, L, S, n_nodes, mode):
             "note": "pageable host buffers; records sorted by (node, site) inside pm_mutations_fetch"}
 
 
+def cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cpu.max), or None when unlimited / unknown."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     """Reference-faithful CPU path (oracle: per-column unordered_map<string,int> +
     recursion, src/fitchSankoff.cpp:30-171) on a bounded column sample, plus a bit-exact
     check of the GPU kernels on the same sample at full tree size."""
     sys.path.insert(0, ROOT)
     import oracle as orc
-    ns = args.cpu_sites
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpus()
+    # every CPU this process may run on: the affinity set, capped by the cgroup's CPU quota
+    # (the GPU box exposes 256 CPUs but grants a 16-CPU quota; more threads than that only
+    # time-slice the same 16 CPUs)
+    effective = max(1, min(usable, int(quota))) if quota else usable
+    threads = args.cpu_threads or effective
+    ns = args.cpu_sites or 3 * threads   # ~15 s of CPU work at 1M leaves
     codes = eng.leaf_codes(0, ns, L)
     cons = eng.consensus(0, ns)
     names = [f"s{i}" if i < L else f"node_{i}" for i in range(n_nodes)]
     node_row = np.full(n_nodes, -1, np.int32)
     node_row[:L] = np.arange(L, dtype=np.int32)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     o = orc.load()
+    print(f"[bench] CPU baseline: {ns} columns on {threads} threads", file=sys.stderr, flush=True)
     secs, want = o.csr_columns(off, idx, root, names, codes, node_row, cons, None, algo=mode, threads=threads)
     n1 = max(1, min(args.cpu_sites_1t, ns))
+    print(f"[bench] CPU baseline: {secs:.1f}s; 1-thread sample of {n1} columns", file=sys.stderr, flush=True)
     secs1, _ = o.csr_columns(off, idx, root, names, codes[:, :n1], node_row, cons[:n1], None, algo=mode, threads=1)
     model = ""
     try:
@@ -339,13 +415,16 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     except OSError:
         pass
     cpu = {"value": ns * n_nodes / secs, "unit": "site*node updates/s", "cores": threads,
-           "kind": "port",
+           "kind": "port (reference unbuildable here: oracle/pm_oracle.cpp restates src/fitchSankoff.cpp)",
            "sample": f"first {ns} of the same columns, {L} leaves x {ns} sites, {threads} threads "
-                     f"({secs:.1f}s), oracle/pm_oracle.cpp faithful per-column loop",
+                     f"({secs:.1f}s), oracle/pm_oracle.cpp faithful per-column loop "
+                     f"(unordered_map<string,int> per column + recursion, the reference's tbb::parallel_for body)",
            "single_thread_value": n1 * n_nodes / secs1,
            "single_thread_sample": f"first {n1} columns, 1 thread ({secs1:.1f}s): the reference M1 driver's "
                                    f"sequential loop (src/panman.cpp:1380-1381)",
-           "host": {"nproc": os.cpu_count(), "cpu_model": model, "threads_used": threads}}
+           "host": {"nproc": os.cpu_count(), "usable_cpus": usable, "cgroup_cpu_quota": quota,
+                    "effective_cpus": effective, "cpu_model": model, "threads_used": threads,
+                    "note": "threads = every CPU the cgroup quota grants this process (all of them busy)"}}
     # GPU on the identical sample columns (same kernels, separate context)
     e2 = panman_amd.Engine(0)
     e2.tree_upload(off, idx, root)
@@ -360,12 +439,7 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
 
 
 def replay_main(args):
-    """FASTA replay (R1-R3) on config C5 (E. coli-like PanMAT, synthetic): leaf*column/s of
-    the GPU replay (consensus expansion + path mutations), inputs resident in HBM; host
-    formatting and the end-to-end rate are reported beside it."""
-    import ctypes as C
-
-    from panman_amd.synth import c5_panmat
+    """`--mode replay`: the C5 replay block as the line's main metric."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -374,6 +448,20 @@ def replay_main(args):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    out = replay_block(args, world, rank, local)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def replay_block(args, world, rank, local):
+    """FASTA replay (R1-R3) on config C5 (E. coli-like PanMAT, synthetic): leaf*column/s of
+    the GPU replay (consensus expansion + path mutations), inputs resident in HBM; host
+    formatting and the end-to-end rate are reported beside it."""
+    import ctypes as C
+
+    from panman_amd.synth import c5_panmat
     t0 = time.time()
     # weak scaling over leaves (SURVEY.md §8e): N x replay-leaves leaves, rank r replays
     # its contiguous share; tree and mutations are replicated, no collective
@@ -427,7 +515,10 @@ def replay_main(args):
         if parent[v] >= 0:
             acc[v] += acc[parent[v]]
     path_recs = float(acc[leaf_nodes[lo:hi]].sum())
-    alg_bytes = units * 1.5 + 8.0 * path_recs
+    # bytes the replay must move: every row byte written once, the consensus row read once
+    # (it stays cache-resident across leaves), 5 B (column u32 + char) per edit on each
+    # leaf's root-to-leaf path
+    alg_bytes = units + float(cols) + 5.0 * path_recs
     kms = ms[3] / args.steps
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     # host formatting (aligned FASTA of every leaf)
@@ -472,17 +563,16 @@ def replay_main(args):
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
         "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
+                     "traffic": traffic, "design_bytes_per_launch": alg_bytes,
+                     "bytes_model": "row bytes written once + consensus row once + 5 B per path edit",
                      "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,
                      "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},
         "host_format_s": round(fmt_s, 3),
         "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
         "cpu_baseline": cpu, "parity_sample": parity,
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    eng.close()
+    return out
 
 
 if __name__ == "__main__":

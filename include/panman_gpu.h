@@ -137,6 +137,47 @@ int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_devi
  * 4 whole pm_run replayed from a hipGraph (PM_OPT_GRAPH). */
 int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
 
+/* ---- multi-GPU column shards ----------------------------------------- */
+/* The reference runs one parsimony call per column (src/panman.cpp:1381 Fitch, :1568
+ * Sankoff) -- columns are independent, so each GPU owns a contiguous site range with the
+ * tree replicated.  The per-site results (parsimony score, root code) are reassembled with
+ * ONE RCCL all-gather over xGMI; mutation records stay on their rank (site indices local
+ * to the shard) and merge on the host by (node, site_begin + site).  RCCL is opened at run
+ * time (librccl.so.1; inside a PyTorch process, torch's own copy).
+ *   pm_comm_unique_id   rank 0 makes the id (ncclGetUniqueId); the caller broadcasts it.
+ *   pm_comm_init_rank   one process per GPU: bind ctx to rank `rank` of `nranks`.
+ *   pm_comm_init_all    one process, several GPUs: ncclCommInitAll over the ctxs' devices
+ *                       (distinct devices; rank i = ctxs[i]).
+ *   pm_run_gather       pm_run on this rank's shard [site_begin, site_begin + uploaded
+ *                       sites) of `total_sites`, then the all-gather: score_device
+ *                       [total_sites] int32 and root_device [total_sites] u8 (device
+ *                       memory) receive every rank's sites.  Async on the ctx stream;
+ *                       every rank must call it.  Shards hold at most ceil(total/ranks)+2.
+ *   pm_multi_run        the same for pm_comm_init_all contexts from one thread (RCCL group
+ *                       call); site_begin[i] per ctx; results to host (nullable).
+ *   pm_shard_range      the balanced rule [r*S/n, (r+1)*S/n) bench.py and shard.py use. */
+#define PM_COMM_ID_BYTES 128
+int pm_comm_unique_id(uint8_t* id, int64_t len);
+int pm_comm_init_rank(pm_ctx* ctx, const uint8_t* id, int nranks, int rank);
+int pm_comm_init_all(pm_ctx* const* ctxs, int n);
+int pm_run_gather(pm_ctx* ctx, int mode, int64_t total_sites, int64_t site_begin, void* score_device,
+                  void* root_device);
+int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin, int64_t total_sites,
+                 int32_t* score, uint8_t* root_code);
+int pm_shard_range(int rank, int ranks, int64_t total_sites, int64_t* begin, int64_t* end);
+
+/* ---- measurement (bench.py roofline; not part of the reference interface) ------------ */
+/* Bytes this design must move in the last pm_run (nucleotide modes), counted from the run's
+ * record masks at the kernels' 16-B-per-lane granularity: out[0] post-order (leaf words,
+ * child records read, own record + masks written), out[1] pre-order + assignment (own
+ * record, parent final, dirty-lane leaf words, compact finals, 8 B per mutation record),
+ * out[2] score histogram, out[3] floor = 0.5 B per leaf-site + 8 B per record, out[4] the
+ * record count.  `n` >= 5.  Synchronises the ctx stream. */
+int pm_design_bytes(pm_ctx* ctx, double* out, int n);
+/* Achievable HBM rate on `device`: a 16-B-per-lane streaming copy of `bytes` bytes, `reps`
+ * times; *gbs = (read + write bytes) / s / 1e9. */
+int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs);
+
 /* ---- column drivers ------------------------------------------------------------------ */
 /* Drop-in for Tree(msa, newick, FILE_TYPE::MSA (mode PM_MODE_FITCH, "M1") or
  * FILE_TYPE::MSA_OPTIMIZE (PM_MODE_SANKOFF, "M2"), reference) -- src/panman.cpp:1274-1649:

@@ -79,6 +79,14 @@ _SIGS = {
     "pm_panman_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pm_reroot": (C.c_int, [C.c_void_p, C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "pm_pangraph_build": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "pm_comm_unique_id": (C.c_int, [C.c_void_p, C.c_int64]),
+    "pm_comm_init_rank": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    "pm_comm_init_all": (C.c_int, [C.c_void_p, C.c_int]),
+    "pm_run_gather": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]),
+    "pm_multi_run": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
+    "pm_shard_range": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "pm_design_bytes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "pm_stream_copy_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 

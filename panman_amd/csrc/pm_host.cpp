@@ -347,6 +347,7 @@ void pm_destroy(pm_ctx* c) {
     free_columns(c);
     free_tree(c->dt);
     free_replay(c);
+    comm_release(c);
     for (auto& v : c->timers)
         for (auto& t : v) {
             (void)hipEventDestroy(t.a);

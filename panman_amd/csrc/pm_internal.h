@@ -189,6 +189,12 @@ struct pm_ctx {
 
     // replay (pm_replay.cpp)
     pm::ReplayState* replay = nullptr;
+
+    // multi-GPU column shards (pm_rccl.hip): RCCL communicator + gather buffers
+    void* comm = nullptr;             // ncclComm_t
+    int comm_rank = 0, comm_size = 1;
+    void* gather_buf = nullptr;       // [send chunk | ranks x chunk] packed site results
+    size_t gather_bytes = 0;
 };
 
 namespace pm {
@@ -213,6 +219,7 @@ hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
 void free_replay(pm_ctx* c);
+void comm_release(pm_ctx* c);   // pm_rccl.hip
 int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_stride, const int32_t* node_row);
 
 // replay kernels (pm_replay.hip)

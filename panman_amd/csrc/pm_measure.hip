@@ -1,0 +1,155 @@
+// pm_measure.hip -- measurement helpers for the roofline the bench reports.
+//
+//   pm_stream_copy_rate  the achievable-HBM reference: a 16-B-per-lane streaming copy
+//                        (read + write bytes / s), the access pattern of the level kernels'
+//                        leaf-row and record streams.
+//   pm_design_bytes      the bytes THIS design must move in one pm_run, counted from the
+//                        record masks of the run just made: leaf words, compressed set
+//                        records written and read, compact finals, dirty-lane leaf reads,
+//                        8 B per mutation record -- each at the 16-B-per-lane granularity the
+//                        kernels load and store (cache-resident consensus words excluded).
+//                        `achieved` = these bytes / kernel time can therefore not exceed
+//                        what the kernels really draw from HBM (PMC FETCH / WRITE sizes).
+#include <algorithm>
+#include <vector>
+
+#include "pm_kernels.h"
+
+namespace pm {
+namespace {
+
+constexpr int kCopyUnroll = 4;
+
+__global__ __launch_bounds__(kBlock) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        int64_t n) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * kCopyUnroll + threadIdx.x;
+    uint4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n) dst[i] = v[u];
+    }
+}
+
+inline int popc(uint64_t x) { return __builtin_popcountll(x); }
+
+}  // namespace
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs) {
+    if (!gbs || bytes < (1 << 20) || reps < 1) return PM_ERR_ARG;
+    *gbs = 0.0;
+    if (hipSetDevice(device) != hipSuccess) return PM_ERR_HIP;
+    const int64_t n = bytes / (int64_t)sizeof(uint4);
+    uint4 *a = nullptr, *b = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = PM_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&a), n * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&b), n * sizeof(uint4)) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess) {
+        rc = PM_ERR_OOM;
+    } else {
+        const dim3 grid((unsigned)((n + (int64_t)kBlock * kCopyUnroll - 1) / ((int64_t)kBlock * kCopyUnroll)));
+        (void)hipMemsetAsync(a, 1, n * sizeof(uint4), s);
+        hipLaunchKernelGGL(k_stream_copy, grid, dim3(kBlock), 0, s, a, b, n);   // warm-up
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_stream_copy, grid, dim3(kBlock), 0, s, a, b, n);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.f)
+            rc = PM_ERR_HIP;
+        else
+            *gbs = 2.0 * (double)n * sizeof(uint4) * reps / (ms * 1e-3) / 1e9;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    return rc;
+}
+
+int pm_design_bytes(pm_ctx* c, double* out, int n) {
+    if (!c || !out || n < 5) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    const int mode = c->last_mode;
+    if (mode != PM_MODE_FITCH && mode != PM_MODE_SANKOFF)
+        return fail(c, PM_ERR_UNSUPPORTED, "design bytes are modelled for the nucleotide modes");
+    int64_t records = 0;
+    int rc = pm_mutation_count(c, &records);
+    if (rc != PM_OK) return rc;
+    const HostTree& ht = c->ht;
+    const int32_t I = c->dt.num_internal, L = c->dt.num_leaves;
+    const int32_t tiles = (c->words + kWave - 1) / kWave;
+    std::vector<uint64_t> m((size_t)I * tiles * kMaskWords);
+    hipError_t e = hipMemcpyAsync(m.data(), c->cmask, m.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "record masks");
+    const bool virt = c->virtual_leaf_parents;
+    const int32_t root = c->dt.root_dense;
+    // virtual leaf-parents as pm_tree_upload forms them: not the root, one or two children, all leaves
+    std::vector<uint8_t> vnode(I, 0);
+    if (virt)
+        for (int32_t d = 0; d < I; ++d) {
+            const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
+            bool all = d != root && deg <= 2;
+            for (int32_t k = ht.child_off[d]; k < ht.child_off[d + 1] && all; ++k) all = ht.child_enc[k] < 0;
+            vnode[d] = all;
+        }
+    const double lane = 16.0, word_row = lane * kWave;   // one lane's code planes; one wave's leaf word
+    const double cx_full = mode == PM_MODE_FITCH ? 64.0 : 128.0;   // complex lane: 16 planes / Z0 + Z1
+    const double cx_read_up = 64.0;                                // the parent reads Fitch planes / Z0
+    double up = 0.0, down = 0.0;
+    auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
+    for (int32_t d = 0; d < I; ++d) {
+        if (vnode[d]) continue;
+        const int32_t e0 = ht.child_off[d], e1 = ht.child_off[d + 1];
+        for (int t = 0; t < tiles; ++t) {
+            const uint64_t* q = mk(d, t);
+            const double rec = 64.0 + lane * popc(q[1]) + cx_full * popc(q[0]);
+            // post-order: children in, own record + masks out, parent masks pushed to children
+            up += rec;
+            const double dirty = d == root ? kWave : popc(q[2]);
+            for (int32_t k = e0; k < e1; ++k) {
+                const int32_t ch = ht.child_enc[k];
+                if (ch < 0) {
+                    up += word_row;
+                    down += lane * dirty;
+                } else if (vnode[ch]) {
+                    const int32_t nl = ht.child_off[ch + 1] - ht.child_off[ch];
+                    up += word_row * nl;
+                    down += lane * dirty * nl;
+                } else {
+                    const uint64_t* r = mk(ch, t);
+                    up += 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
+                }
+                if (k >= e0 + 2 && (ch < 0 || vnode[ch]))   // k_tail item: parent masks + parent final
+                    down += 64.0 + lane * popc(q[0] | q[1]);
+            }
+            // pre-order: own record, parent final (non-consensus lanes), compact final out
+            down += rec;
+            if (d == root) down += 2.0 * word_row;   // forced / root final
+            else down += lane * popc(q[3] | q[4]) + lane * popc(q[0]);
+        }
+    }
+    down += 8.0 * (double)records;
+    out[0] = up;
+    out[1] = down;
+    out[2] = 8.0 * (double)records + 4.0 * (double)c->num_sites;   // score histogram
+    out[3] = 0.5 * (double)L * (double)c->num_sites + 8.0 * (double)records;   // floor: leaf codes once + records
+    out[4] = (double)records;
+    return PM_OK;
+}
+
+}  // extern "C"

@@ -188,43 +188,76 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
 
     // columns split into contiguous even-aligned ranges, one host thread + context per
     // device; each range's records are (node, site)-sorted, so appending
-    // the ranges in site order and stable-sorting by node gives the global (node, site) order
+    // the ranges in site order and stable-sorting by node gives the global (node, site) order.
+    // Distinct devices form one RCCL communicator (pm_comm_init_all) and the per-site
+    // (score, root code) are reassembled with one all-gather (pm_multi_run); repeated
+    // devices (several shards on one GPU) run their shards independently.
     const int G = (int)devices.size();
     std::vector<std::vector<pm_mut>> part(G);
     std::vector<std::string> msg(G);
-    std::vector<std::thread> th;
     std::vector<int64_t> lo(G + 1);
     for (int g = 0; g <= G; ++g) lo[g] = std::min<int64_t>(S, (S * g / G + 1) / 2 * 2);
     lo[G] = S;
+    bool distinct = G > 1;
     for (int g = 0; g < G; ++g)
-        th.emplace_back([&, g]() {
-            const int64_t a = lo[g], ns = lo[g + 1] - lo[g];
-            if (ns <= 0) return;
-            CtxGuard cg;
-            if (pm_create(devices[g], &cg.c) != PM_OK) {
-                msg[g] = "no HIP device " + std::to_string(devices[g]);
-                return;
-            }
-            pm_tree tree{N, t.root, off.data(), idx.data()};
+        for (int h = 0; h < g; ++h) distinct &= devices[g] != devices[h];
+    for (int g = 0; g < G && distinct; ++g) distinct &= lo[g + 1] > lo[g];
+    std::vector<CtxGuard> cg(G);
+    for (int g = 0; g < G; ++g)
+        if (pm_create(devices[g], &cg[g].c) != PM_OK) return dump_error("no HIP device " + std::to_string(devices[g]));
+    auto each = [&](auto&& fn) {   // one host thread per shard
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g)
+            th.emplace_back([&, g]() {
+                if (lo[g + 1] > lo[g] && msg[g].empty()) fn(g);
+            });
+        for (auto& x : th) x.join();
+        for (int g = 0; g < G; ++g)
+            if (!msg[g].empty()) return false;
+        return true;
+    };
+    const bool uploaded = each([&](int g) {
+        const int64_t a = lo[g], ns = lo[g + 1] - lo[g];
+        pm_tree tree{N, t.root, off.data(), idx.data()};
+        if (pm_tree_upload(cg[g].c, &tree) != PM_OK ||
+            pm_leaves_upload(cg[g].c, ns, codes.data() + a / 2, stride, node_row.data(), nullptr, 0) != PM_OK ||
+            pm_sites_upload(cg[g].c, cons4.data() + a / 2, ref_row ? force4.data() + a / 2 : nullptr) != PM_OK ||
+            (!distinct && pm_run(cg[g].c, mode) != PM_OK))
+            msg[g] = pm_last_error(cg[g].c);
+    });
+    std::vector<int32_t> score;
+    if (uploaded && distinct) {
+        std::vector<pm_ctx*> ctxs(G);
+        for (int g = 0; g < G; ++g) ctxs[g] = cg[g].c;
+        score.assign(S, 0);
+        if (pm_comm_init_all(ctxs.data(), G) != PM_OK ||
+            pm_multi_run(ctxs.data(), G, mode, lo.data(), S, score.data(), nullptr) != PM_OK)
+            return dump_error(std::string("multi-GPU run: ") + pm_last_error(ctxs[0]));
+    }
+    if (uploaded)
+        each([&](int g) {
             int64_t n = 0;
-            if (pm_tree_upload(cg.c, &tree) != PM_OK ||
-                pm_leaves_upload(cg.c, ns, codes.data() + a / 2, stride, node_row.data(), nullptr, 0) != PM_OK ||
-                pm_sites_upload(cg.c, cons4.data() + a / 2, ref_row ? force4.data() + a / 2 : nullptr) != PM_OK ||
-                pm_run(cg.c, mode) != PM_OK || pm_mutation_count(cg.c, &n) != PM_OK) {
-                msg[g] = pm_last_error(cg.c);
+            if (pm_mutation_count(cg[g].c, &n) != PM_OK) {
+                msg[g] = pm_last_error(cg[g].c);
                 return;
             }
             part[g].resize((size_t)std::max<int64_t>(n, 1));
-            if (pm_mutations_fetch(cg.c, part[g].data(), n, &n) != PM_OK) {
-                msg[g] = pm_last_error(cg.c);
+            if (pm_mutations_fetch(cg[g].c, part[g].data(), n, &n) != PM_OK) {
+                msg[g] = pm_last_error(cg[g].c);
                 return;
             }
             part[g].resize((size_t)n);
-            for (pm_mut& m : part[g]) m.site_info += (uint32_t)a << 8;
+            for (pm_mut& m : part[g]) m.site_info += (uint32_t)lo[g] << 8;
         });
-    for (auto& x : th) x.join();
     for (int g = 0; g < G; ++g)
         if (!msg[g].empty()) return dump_error(msg[g]);
+    if (!score.empty()) {   // the gathered score counts every non-root record exactly once
+        int64_t total = 0, nonroot = 0;
+        for (int32_t v : score) total += v;
+        for (auto& v : part)
+            for (const pm_mut& m : v) nonroot += m.node != (uint32_t)t.root;
+        if (total != nonroot) return dump_error("gathered parsimony score disagrees with the shards' records");
+    }
     std::vector<pm_mut> recs;
     for (auto& v : part) recs.insert(recs.end(), v.begin(), v.end());
     if (G > 1) std::stable_sort(recs.begin(), recs.end(), [](const pm_mut& x, const pm_mut& y) { return x.node < y.node; });

@@ -33,6 +33,25 @@ def gather_site_results(score_local: torch.Tensor, root_local: torch.Tensor, sit
     return s_all[keep], r_all[keep]
 
 
+def merge_mut_records(parts: list[np.ndarray], site_offsets: list[int]) -> np.ndarray:
+    """Per-rank records in the C-ABI layout (pm_mut: [n, 2] uint32 node, site << 8 | type << 4
+    | code, site local to the rank's shard) -> global pm_mut records sorted by (node, site)."""
+    rows = []
+    for recs, off in zip(parts, site_offsets):
+        r = np.ascontiguousarray(recs, dtype=np.uint32).reshape(-1, 2).copy()
+        r[:, 1] += np.uint32(off << 8)
+        rows.append(r)
+    allr = np.concatenate(rows) if rows else np.zeros((0, 2), np.uint32)
+    order = np.lexsort((allr[:, 1], allr[:, 0]))
+    return allr[order]
+
+
+def to_pm_mut(recs4: np.ndarray) -> np.ndarray:
+    """[n, 4] (node, site, type, code) -> [n, 2] pm_mut."""
+    r = np.asarray(recs4, dtype=np.uint32)
+    return np.stack([r[:, 0], (r[:, 1] << 8) | (r[:, 2] << 4) | r[:, 3]], axis=1)
+
+
 def merge_records(parts: list[np.ndarray], site_offsets: list[int]) -> np.ndarray:
     """Per-rank [n,4] (node, local site, type, code) -> global records sorted by (node, site)."""
     rows = []

@@ -104,3 +104,14 @@ def test_bytes_at_past_2gib():
     out = bytes_at(C.c_void_p(C.addressof(buf)), n)
     assert len(out) == n and out[-4:] == b"xxxx" and out[:4] == b"\0\0\0\0"
     del out, buf
+
+
+def test_shard_rule_matches_python():
+    from panman_amd.shard import shard_range
+    for S in (1, 7, 30000, 15001):
+        for n in (1, 2, 3, 8):
+            cover = []
+            for r in range(n):
+                assert panman_amd.shard_range_c(r, n, S) == shard_range(r, n, S)
+                cover.extend(range(*shard_range(r, n, S)))
+            assert cover == list(range(S))

@@ -1,6 +1,8 @@
-"""N>1 path on CPU: column shards on 2 gloo ranks, one all-gather of (score, root code),
-host merge of records -- must equal the single-shard result (oracle as the per-shard
-engine, since this host has no GPU)."""
+"""N>1 path on CPU: column shards on 2 / 3 gloo ranks, one all-gather of (score, root code),
+host merge of the records in the C-ABI layout (pm_mut: node, site << 8 | type << 4 | code,
+sites local to the rank's shard, as pm_mutations_fetch returns them) -- must equal the
+single-shard result.  The oracle is the per-shard engine, since this host has no GPU; the
+GPU side of the same path (pm_run_gather over RCCL) is tests/test_gpu_multi.py."""
 import os
 import socket
 
@@ -34,7 +36,7 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle as orc
-    from panman_amd.shard import gather_site_results, shard_range
+    from panman_amd.shard import gather_site_results, shard_range, to_pm_mut
     off, idx, root, codes, cons, node_row, names = _problem()
     lo, hi = shard_range(rank, world, codes.shape[1])
     _, recs, rootc = orc.load().csr_columns(off, idx, root, names, codes[:, lo:hi], node_row, cons[lo:hi],
@@ -42,7 +44,7 @@ def _worker(rank, world, port, q):
     score = np.bincount(recs[recs[:, 0] != root][:, 1], minlength=hi - lo).astype(np.int32)
     s_all, r_all = gather_site_results(torch.from_numpy(score), torch.from_numpy(rootc), codes.shape[1])
     objs = [None] * world
-    dist.all_gather_object(objs, (lo, recs))
+    dist.all_gather_object(objs, (lo, to_pm_mut(recs)))
     if rank == 0:
         q.put((s_all.numpy(), r_all.numpy(), objs))
     dist.barrier()
@@ -62,7 +64,7 @@ def test_sharded_columns_match_single_shard(world):
     import sys
     sys.path.insert(0, ROOT)
     import oracle as orc
-    from panman_amd.shard import merge_records
+    from panman_amd.shard import merge_mut_records, to_pm_mut
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -79,5 +81,6 @@ def test_sharded_columns_match_single_shard(world):
     want_score = np.bincount(want[want[:, 0] != root][:, 1], minlength=codes.shape[1])
     assert (s_all == want_score).all()
     assert (r_all == want_root).all()
-    merged = merge_records([p[1] for p in parts], [p[0] for p in parts])
-    assert merged.shape == want.shape and (merged == want).all()
+    merged = merge_mut_records([p[1] for p in parts], [p[0] for p in parts])
+    want_mut = to_pm_mut(want)
+    assert merged.shape == want_mut.shape and (merged == want_mut).all()

@@ -1,0 +1,79 @@
+"""Multi-GPU column-shard path through the C-ABI (pm_rccl.hip): a
+single-rank RCCL communicator must reproduce pm_run's per-site results exactly, and the
+measurement helpers behind bench.py's roofline must be self-consistent.  (Two or more
+ranks need two GPUs; the gloo tests in test_distributed.py cover the host-side merge.)"""
+import numpy as np
+import pytest
+import torch
+
+import panman_amd
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(leaves=3000, sites=2500, seed=4):
+    off, idx, root = panman_amd.random_join_tree(leaves, seed=seed)
+    eng = panman_amd.Engine(0)
+    eng.tree_upload(off, idx, root)
+    eng.synth_columns(0, sites, seed=seed + 1)
+    return eng
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_init_all_single_rank_equals_run(mode):
+    eng = _engine()
+    eng.run(mode)
+    want_score, want_root = eng.site_results()
+    want_recs = eng.mutations_raw()
+    score, root = panman_amd.multi_run([eng], mode, [0], eng.num_sites)
+    assert (score == want_score).all() and (root == want_root).all()
+    assert (eng.mutations_raw() == want_recs).all()
+    eng.close()
+
+
+def test_init_rank_run_gather_equals_run():
+    eng = _engine(sites=4097)
+    eng.run(panman_amd.MODE_FITCH)
+    want_score, want_root = eng.site_results()
+    uid = panman_amd.comm_unique_id()
+    assert len(uid) == 128
+    eng.comm_init_rank(uid, 1, 0)
+    s = torch.full((eng.num_sites,), -7, dtype=torch.int32, device="cuda")
+    r = torch.full((eng.num_sites,), 77, dtype=torch.uint8, device="cuda")
+    eng.run_gather(panman_amd.MODE_FITCH, eng.num_sites, 0, s.data_ptr(), r.data_ptr())
+    torch.cuda.synchronize()
+    assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()
+    # a shard claiming sites outside the total is refused
+    with pytest.raises(panman_amd.PanmanError):
+        eng.run_gather(panman_amd.MODE_FITCH, eng.num_sites, 5, s.data_ptr(), r.data_ptr())
+    eng.close()
+
+
+def test_run_gather_needs_a_communicator():
+    eng = _engine(leaves=200, sites=100)
+    s = torch.zeros(100, dtype=torch.int32, device="cuda")
+    r = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    with pytest.raises(panman_amd.PanmanError, match="communicator"):
+        eng.run_gather(panman_amd.MODE_FITCH, 100, 0, s.data_ptr(), r.data_ptr())
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_design_bytes_consistent(mode):
+    leaves, sites = 20000, 3000
+    eng = _engine(leaves, sites)
+    eng.run(mode)
+    d = eng.design_bytes()
+    n = eng.mutation_count()
+    assert d["records"] == n
+    # the post-order pass reads every leaf word once (64-word tiles of 16 B per lane)
+    tiles = ((sites + 31) // 32 + 63) // 64
+    assert d["up"] >= leaves * tiles * 64 * 16
+    assert d["floor"] == pytest.approx(0.5 * leaves * sites + 8 * n)
+    assert d["down"] >= 8 * n and d["score"] == 8 * n + 4 * sites
+    eng.close()
+
+
+def test_stream_copy_rate_is_physical():
+    gbs = panman_amd.stream_copy_rate(0, gib=1, reps=3)
+    assert 1000.0 < gbs < 8000.0

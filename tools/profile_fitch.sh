@@ -13,7 +13,7 @@ mode=fitch
 for a in "$@"; do case $a in sankoff) mode=sankoff;; esac; done
 run() {  # run NAME ROCPROF_ARGS... -- (bench args appended)
   local name=$1; shift
-  timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$out/$name" -o run -- python3 bench.py --no-cpu "${BENCH[@]}" \
+  timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$out/$name" -o run -- python3 bench.py --no-cpu --with none "${BENCH[@]}" \
     > "$out/$name.json" 2> "$out/$name.log"
 }
 BENCH=(--steps 4 --warmup 1 "$@")

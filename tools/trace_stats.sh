@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=$1; shift
 out=gpurun_out/trace_$tag
 mkdir -p "$out"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- python3 bench.py --no-cpu "$@" \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- python3 bench.py --no-cpu --with none "$@" \
   > "$out.json" 2> "$out.log"
 find "$out" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
 python3 - "$out/kernel_stats.csv" <<'P'
