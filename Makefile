@@ -7,8 +7,9 @@ HDR := $(wildcard panman_amd/csrc/*.h) include/panman_gpu.h
 OBJ := $(patsubst panman_amd/csrc/%,build/%.o,$(SRC))
 LIB := panman_amd/libpanman_amd.so
 CLI := bin/panmanUtils
+DEMO := bin/facade_demo
 
-all: $(LIB) $(CLI) oracle
+all: $(LIB) $(CLI) $(DEMO) oracle
 
 build/%.o: panman_amd/csrc/% $(HDR)
 	@mkdir -p build
@@ -19,6 +20,12 @@ $(LIB): $(OBJ)
 
 # panmanUtils-compatible CLI (host C++ over the C-ABI; finds the library next to the package)
 $(CLI): panman_amd/csrc/cli/panmanUtils.cpp include/panman_gpu.h $(LIB)
+	@mkdir -p bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lpanman_amd -l:libpanman_amd.so \
+	    -Wl,-rpath,'$$ORIGIN/../panman_amd'
+
+# the C++ facade (include/panman_tree.hpp) driven like the reference's Tree / TreeGroup
+$(DEMO): panman_amd/csrc/cli/facade_demo.cpp include/panman_tree.hpp include/panman_gpu.h $(LIB)
 	@mkdir -p bin
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lpanman_amd -l:libpanman_amd.so \
 	    -Wl,-rpath,'$$ORIGIN/../panman_amd'

@@ -295,6 +295,22 @@ int pm_reroot(pm_ctx* ctx, const pm_panmat* tree, const char* leaf, pm_panman** 
  * the per-block sequences.  Result: a one-tree pm_panman. */
 int pm_pangraph_build(pm_ctx* ctx, const char* json, const char* newick, const char* reference, pm_panman** out);
 
+/* ---- summary ------------------------------------------------------------------------- */
+/* Drop-in for Tree::printSummary (src/summary.cpp:257-273; CLI --summary, src/panmanUtils.cpp:
+ * 356-384): mutation counts reduced on the GPU from the PanMAT's flat mutation arrays
+ * (getTotalParsimonyParallel, :3-59; getBlockMutationsParallelHelper, :61-109), leaf depths
+ * as the Newick parser computes them (float sum in leaf order, src/panman.cpp:386-394),
+ * block duplications / translocations by the reference's presence walk (:111-193). */
+typedef struct pm_summary {
+    int64_t nodes, samples;                                 /* Total Nodes / Samples in Tree */
+    int64_t substitutions, insertions, deletions, inversions;
+    int64_t max_depth;
+    float mean_depth;
+    int64_t block_insertions, block_deletions, block_inversions;
+    int64_t block_duplications, block_translocations;
+} pm_summary;
+int pm_summary_compute(pm_ctx* ctx, const pm_panmat* tree, pm_summary* out);
+
 /* ---- synthetic inputs (bench / tests; seeded, counter-based) ------------------------ */
 /* Random-join binary tree on `leaves` leaves (SURVEY.md §8d family T1): writes
  * 2*leaves-1 nodes as CSR; leaves are ids [0, leaves), internal nodes follow. */

@@ -38,6 +38,8 @@ def load() -> "Oracle":
         lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
         lib.oracle_pangraph.restype = C.c_void_p
         lib.oracle_pangraph.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+        lib.oracle_summary.restype = C.c_void_p
+        lib.oracle_summary.argtypes = [C.c_void_p]
         lib.oracle_reroot.restype = C.c_void_p
         lib.oracle_reroot.argtypes = [C.c_void_p, C.c_char_p]
         _lib = lib
@@ -87,6 +89,19 @@ class Oracle:
         p = self.lib.oracle_reroot(C.byref(st), leaf.encode())
         del keep
         return _take_string(self.lib, p)
+
+    def summary(self, panmat) -> tuple[str, str]:
+        """Tree::printSummary text (src/summary.cpp:257-273) and the block lines
+        getBlockMutationsParallel prints to std::cout (:203-250)."""
+        st, keep = panmat.as_struct()
+        p = self.lib.oracle_summary(C.byref(st))
+        del keep
+        try:
+            out = C.string_at(p).decode()
+            rest = C.string_at(p + len(out) + 1).decode()
+        finally:
+            self.lib.oracle_free(p)
+        return out, rest
 
     def column(self, newick: str, leaves: str, algo: str, forced: int, parent: int) -> dict:
         p = self.lib.oracle_column(newick.encode(), leaves.encode(), self.ALGO[algo], forced, parent)

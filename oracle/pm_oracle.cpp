@@ -1485,6 +1485,120 @@ char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* s
 // Reroot at `leaf` (Tree::reroot) and dump the new tree: "newick\t<text>" then per node
 // in name order its block mutations (sorted by block) and nucleotide mutations (list
 // order) -- see reroot_dump.
+// ---------------------------------------------------------------- summary ----
+// Tree::printSummary (src/summary.cpp:257-273): counts by getTotalParsimonyParallelHelper
+// (:3-59) -- NS counted by length, NI / ND by record, block insertions of any strand into
+// "Insertions", non-inverting block deletions into "Deletions", every block mutation with
+// the inversion flag into "Inversions" -- and the Newick parser's leaf depths
+// (src/panman.cpp:372-394: float sum in Newick leaf order / leaf count).  Then
+// getBlockMutationsParallel (:203-250, printed to std::cout): block insertions / deletions /
+// inversions and the duplication / translocation walk getOtherBlockMutationsParallelHelper
+// (:111-193) over blocks grouped by identical consensusSeq.  Returns "<out part>\0<cout part>".
+struct SummaryWalk {
+    std::vector<bool> exists, strand;
+    std::vector<std::vector<uint32_t>> dups;
+    std::vector<uint32_t> dups_pos;
+    long long dup = 0, trans = 0;
+    void visit(RNode* n) {
+        std::vector<bool> exists_parent = exists;
+        std::vector<std::tuple<int32_t, bool, bool>> undo;
+        for (auto& m : n->bmuts) {
+            const int32_t b = m.primary;
+            if (m.info) {
+                undo.emplace_back(b, exists[b], strand[b]);
+                exists[b] = true;
+                strand[b] = !m.inversion;
+            } else {
+                undo.emplace_back(b, exists[b], strand[b]);
+                if (m.inversion) {
+                    strand[b] = !strand[b];
+                } else {
+                    exists[b] = false;
+                    strand[b] = true;
+                }
+            }
+        }
+        for (auto& m : n->bmuts) {
+            if (!m.info) continue;
+            for (uint32_t d : dups[dups_pos[m.primary]]) {
+                if (d != (uint32_t)m.primary && exists[d] && exists_parent[d]) { ++dup; break; }
+                if (d != (uint32_t)m.primary && !exists[d] && exists_parent[d]) { ++trans; break; }
+            }
+        }
+        for (RNode* c : n->children) visit(c);
+        for (auto it = undo.rbegin(); it != undo.rend(); ++it) {
+            exists[std::get<0>(*it)] = std::get<1>(*it);
+            strand[std::get<0>(*it)] = std::get<2>(*it);
+        }
+    }
+};
+
+static std::string summary_text(RTree& t, std::string& cout_part) {
+    long long ns = 0, ni = 0, nd = 0, bi = 0, bd = 0, inv = 0, bdi = 0;
+    size_t leaves = 0, max_depth = 0;
+    float mean_depth = 0.f;
+    // pre-order, children in order = the Newick string's leaf order
+    std::vector<std::pair<RNode*, size_t>> stack{{t.root, 0}};
+    while (!stack.empty()) {
+        auto [n, depth] = stack.back();
+        stack.pop_back();
+        for (auto& m : n->nmuts) {
+            if (m.type() == 0) ns += m.length();
+            else if (m.type() == 2) ++ni;
+            else if (m.type() == 1) ++nd;
+        }
+        for (auto& m : n->bmuts) {
+            if (m.info) ++bi;
+            if (!m.info && !m.inversion) ++bd;
+            if (m.inversion) ++inv;
+            if (!m.info && m.inversion) ++bdi;
+        }
+        if (n->children.empty()) {
+            ++leaves;
+            max_depth = std::max(max_depth, depth);
+            mean_depth += depth;
+        }
+        for (auto it = n->children.rbegin(); it != n->children.rend(); ++it) stack.push_back({*it, depth + 1});
+    }
+    mean_depth /= leaves;
+    std::ostringstream out;
+    out << "Total Nodes in Tree: " << t.internal_counter + leaves << std::endl;
+    out << "Total Samples in Tree: " << leaves << std::endl;
+    out << "Total Substitutions: " << ns << std::endl;
+    out << "Total Insertions: " << ni + bi << std::endl;
+    out << "Total Deletions: " << nd + bd << std::endl;
+    out << "Total Inversions: " << inv << std::endl;
+    out << "Max Tree Depth: " << max_depth << std::endl;
+    out << "Mean Tree Depth: " << mean_depth << std::endl;
+    SummaryWalk w;
+    std::map<std::vector<uint32_t>, std::vector<uint32_t>> by_seq;   // grouping only: order-free counts
+    for (auto& b : t.blocks) by_seq[b.seq].push_back((uint32_t)b.primary);
+    w.dups_pos.assign(t.blocks.size(), 0);
+    for (auto& kv : by_seq) {
+        for (uint32_t b : kv.second) w.dups_pos[b] = (uint32_t)w.dups.size();
+        w.dups.push_back(kv.second);
+    }
+    w.exists.assign(t.blocks.size(), false);
+    w.strand.assign(t.blocks.size(), true);
+    w.visit(t.root);
+    std::ostringstream co;
+    co << "Total Block Insertions: " << bi << std::endl;
+    co << "Total Block Deletions: " << bd << std::endl;
+    co << "Total Block Inversion: " << bdi << std::endl;
+    co << "Total Block Duplications: " << w.dup << std::endl;
+    co << "Total Block Translocation: " << w.trans << std::endl;
+    cout_part = co.str();
+    return out.str();
+}
+
+char* oracle_summary(const OraclePanmat* p) {
+    RTree t;
+    build_rtree(p, t);
+    std::string co;
+    const std::string out = summary_text(t, co);
+    return dup_string(out + std::string(1, '\0') + co);
+}
+
 char* oracle_reroot(const OraclePanmat* p, const char* leaf) {
     RTree t;
     build_rtree(p, t);

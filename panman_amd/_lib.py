@@ -29,6 +29,13 @@ class Mut(C.Structure):
     _fields_ = [("node", C.c_uint32), ("site_info", C.c_uint32)]
 
 
+class Summary(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("nodes", "samples", "substitutions", "insertions", "deletions",
+                                          "inversions", "max_depth")] + [("mean_depth", C.c_float)] + \
+               [(n, C.c_int64) for n in ("block_insertions", "block_deletions", "block_inversions",
+                                          "block_duplications", "block_translocations")]
+
+
 class Tree(C.Structure):
     _fields_ = [("num_nodes", C.c_int32), ("root", C.c_int32),
                 ("child_offsets", C.c_void_p), ("child_index", C.c_void_p)]
@@ -85,6 +92,7 @@ _SIGS = {
     "pm_run_gather": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]),
     "pm_multi_run": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
     "pm_shard_range": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "pm_summary_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Summary)]),
     "pm_design_bytes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "pm_stream_copy_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),

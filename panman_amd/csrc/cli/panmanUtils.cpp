@@ -43,6 +43,7 @@ const Spec kSpecs[] = {
     {"input-msa", 'M', true, "Input MSA file (FASTA format) to build a PanMAN"},
     {"input-pangraph", 'P', true, "Input PanGraph JSON file to build a PanMAN"},
     {"input-newick", 'N', true, "Input tree topology as Newick string"},
+    {"summary", 's', false, "Print PanMAN summary"},
     {"newick", 't', false, "Print newick string of all trees in a PanMAN"},
     {"fasta", 'f', false, "Print tip sequences (FASTA format)"},
     {"fasta-aligned", 'm', false, "Print MSA of sequences for each PanMAT in a PanMAN (FASTA format)"},
@@ -59,7 +60,7 @@ const Spec kSpecs[] = {
 
 // Reference commands outside the accelerated path: recognised so the error is explicit.
 const char* const kOther[] = {"input-gfa", "impute", "create-network", "printTips",
-                              "summary", "subnet", "vcf", "gfa", "maf", "annotate",
+                              "subnet", "vcf", "gfa", "maf", "annotate",
                               "aa-translation", "extended-newick", "printMutations", "acr", "index",
                               "toUsher"};
 
@@ -331,6 +332,43 @@ int from_panman(const Options& o, const std::vector<int>& devices) {
         status = reroot(o, file, device);
         pm_panman_free(file);
         return status;
+    }
+    if (o.has("summary")) {   // src/panmanUtils.cpp:356-384, Tree::printSummary (src/summary.cpp:257-273)
+        pm_ctx* ctx = nullptr;
+        if (pm_create(device, &ctx) != PM_OK) {
+            print_error("no HIP device");
+            pm_panman_free(file);
+            return 1;
+        }
+        const auto s0 = Clock::now();
+        for (int i = 0; i < trees && status == 0; ++i) {
+            pm_panmat view;
+            pm_summary sm;
+            if (pm_panman_tree(file, i, &view) != PM_OK || pm_summary_compute(ctx, &view, &sm) != PM_OK) {
+                print_error(pm_last_error(ctx));
+                status = 1;
+                break;
+            }
+            std::ostringstream out;
+            out << "Total Nodes in Tree: " << sm.nodes << std::endl;
+            out << "Total Samples in Tree: " << sm.samples << std::endl;
+            out << "Total Substitutions: " << sm.substitutions << std::endl;
+            out << "Total Insertions: " << sm.insertions << std::endl;
+            out << "Total Deletions: " << sm.deletions << std::endl;
+            out << "Total Inversions: " << sm.inversions << std::endl;
+            out << "Max Tree Depth: " << sm.max_depth << std::endl;
+            out << "Mean Tree Depth: " << sm.mean_depth << std::endl;
+            const std::string text = out.str();
+            if (!sink(".summary", i, text.data(), text.size())) status = 1;
+            // getBlockMutationsParallel prints to std::cout whatever the output file (:203-250)
+            std::cout << "Total Block Insertions: " << sm.block_insertions << std::endl;
+            std::cout << "Total Block Deletions: " << sm.block_deletions << std::endl;
+            std::cout << "Total Block Inversion: " << sm.block_inversions << std::endl;
+            std::cout << "Total Block Duplications: " << sm.block_duplications << std::endl;
+            std::cout << "Total Block Translocation: " << sm.block_translocations << std::endl;
+        }
+        std::cout << "\nSummary creation time: " << ns_since(s0) << " nanoseconds\n";
+        pm_destroy(ctx);
     }
     if (o.has("newick")) {
         for (int i = 0; i < trees; ++i) {
