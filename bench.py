@@ -51,6 +51,8 @@ def parse():
                         "sequence from a hipGraph (PM_OPT_GRAPH, the default; per-kernel times then come "
                         "from an extra untimed eager pass)")
     p.add_argument("--graph", action="store_true", help="(default) hipGraph replay")
+    p.add_argument("--no-subtree", action="store_true",
+                   help="Fitch: leaf-parent form only (PM_OPT_SUBTREE off; A/B of the subtree form)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -104,6 +106,8 @@ def main():
     eng.set_stream(stream.cuda_stream)
     eng.tree_upload(off, idx, root)
     eng.synth_columns(lo, s_local, seed=2)
+    if args.no_subtree:
+        eng.set_subtree(False)
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
     gather = "none (1 GPU)"
@@ -316,6 +320,8 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
         "other_kernels_ms_per_step": {k: round(v[0], 3) for k, v in classes.items() if k != dom},
         "score_kernel_ms_per_step": round(ms[2] / steps, 3),
         "step_design_bytes": step_design,
+        "step_design_parts": {k: round(v / 1e9, 3) for k, v in design.get("parts", {}).items()},
+        "step_design_parts_unit": "GB",
         "step_design_GBs": round(step_design / (ms_step * 1e-3) / 1e9, 1),
         "floor_bytes": design["floor"],
         "floor_note": "0.5 B per leaf-site (leaf codes read once) + 8 B per mutation record",

@@ -89,10 +89,14 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  memsets) into a hipGraph once and replays it while the tree, columns,
  *                  mode and buffers stay the same; kernel_times then reports the whole run
  *                  as class 4.
+ *   PM_OPT_SUBTREE (default 1): Fitch with every leaf present also evaluates, inside its
+ *                  binary parent, any node whose children are leaves or two-leaf cherries
+ *                  (three- and four-leaf subtrees), so those are not materialised either.
  * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
  * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
+#define PM_OPT_SUBTREE 6
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);
@@ -172,7 +176,9 @@ int pm_shard_range(int rank, int ranks, int64_t total_sites, int64_t* begin, int
  * child records read, own record + masks written), out[1] pre-order + assignment (own
  * record, parent final, dirty-lane leaf words, compact finals, 8 B per mutation record),
  * out[2] score histogram, out[3] floor = 0.5 B per leaf-site + 8 B per record, out[4] the
- * record count.  `n` >= 5.  Synchronises the ctx stream. */
+ * record count; with n >= 13, out[5..12] split them: post-order leaf words, child records read,
+ * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
+ * words, finals written, tail items.  `n` >= 5.  Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
 /* Achievable HBM rate on `device`: a 16-B-per-lane streaming copy of `bytes` bytes, `reps`
  * times; *gbs = (read + write bytes) / s / 1e9. */

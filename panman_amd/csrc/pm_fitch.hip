@@ -28,8 +28,16 @@ namespace {
 #ifndef PM_LEAFY_WAVES
 #define PM_LEAFY_WAVES 6
 #endif
-template <bool AP, bool LEAFY>
-__global__ __launch_bounds__(kBlock, LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
+#ifndef PM_SUB_LEAFY_WAVES
+#define PM_SUB_LEAFY_WAVES 4
+#endif
+#ifndef PM_SUB_UP_WAVES
+#define PM_SUB_UP_WAVES 4
+#endif
+// SUB: subtree form -- the first two children may also be S2 / S3 subtrees (three or four
+// leaves each, evaluated in registers: subtree_set_ap).
+template <bool AP, bool LEAFY, bool SUB = false>
+__global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
@@ -46,14 +54,14 @@ __global__ __launch_bounds__(kBlock, LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;
-        fetch_child_ap<kFitchRec, LEAFY>(a, d.c0, vl0, tile, lane, word, f0);
-        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY>(a, d.c1, vl1, tile, lane, word, f1);
+        fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c0, vl0, tile, lane, word, f0);
+        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c1, vl1, tile, lane, word, f1);
         __builtin_amdgcn_sched_barrier(0);
         // after the children's consensus loads: loaded before them, the compiler reuses it
         // for them through register copies that wait on every outstanding load
         cw = a.cons[word];
-        fold_child_ap(d.c0, vl0, f0, both, either, vd);
-        if (e1 - e0 > 1) fold_child_ap(d.c1, vl1, f1, both, either, vd);
+        fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
+        if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
     } else {
         fold_child<AP>(a, d.c0, vl0, tile, lane, word, both, either, vd);
         if (e1 - e0 > 1) fold_child<AP>(a, d.c1, vl1, tile, lane, word, both, either, vd);
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(kBlock, LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k
     }
     for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & ~kVirtualBit] : make_int4(-1, -1, -1, -1);
+        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
         if constexpr (LEAFY) {
             ChildFetch f;
             fetch_child_ap<kFitchRec, true>(a, c, vl, tile, lane, word, f);
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
     for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
         const int32_t my = base + kWavesPerBlock * lane;
         const int32_t enc = my < e1 ? a.child_enc[my] : 0;
-        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask]
                                                                    : make_int4(-1, -1, -1, -1);
         const int cnt = min(kWave, (e1 - base + kWavesPerBlock - 1) / kWavesPerBlock);
         for (int k = 0; k < cnt; k += 2) {
@@ -295,13 +303,15 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const int32_t tiles = (c->words + kWave - 1) / kWave;
     const int64_t wpad = (int64_t)tiles * kWave;
 
-    // Fitch (not block Fitch) may skip materialising leaf-parents
+    // Fitch (not block Fitch) may skip materialising leaf-parents and, with every leaf
+    // present, S2 / S3 subtrees (the subtree form)
     const bool virt = !block && c->virtual_leaf_parents;
-    const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
-    const NodeDesc* up_desc = virt ? dt.up_desc_v : dt.up_desc;
-    const NodeDesc* down_desc = virt ? dt.down_desc_v : dt.down_desc;
-    const std::vector<int32_t>& up_off = virt ? ht.up_level_off_v : ht.up_level_off;
-    const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
+    const bool sub = virt && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
+    const int32_t* child_enc = sub ? dt.child_enc_k : virt ? dt.child_enc_v : dt.child_enc;
+    const NodeDesc* up_desc = sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
+    const NodeDesc* down_desc = sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
+    const std::vector<int32_t>& up_off = sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off;
+    const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
 
     UpArgs up{};
     up.child_off = dt.child_off;
@@ -319,7 +329,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
-    const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
+    const std::vector<int32_t>& class_off = sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
     const int H = (int)up_off.size() - 1;
     for (int h = 0; h < H; ++h) {
         // out-degree <= 3: one wave per (node, tile); wider: one workgroup per (node, tile)
@@ -329,9 +339,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             up.desc = up_desc + b;
             up.count = m - b;
             const dim3 grid = wave_grid(up.count, tiles);
-            const bool leafy = virt && ht.up_leafy_v[h];
+            const bool leafy = sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
             timer_begin(c, 0);
-            if (c->leaves_all_present && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (c->leaves_all_present && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (c->leaves_all_present) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL((k_fitch_up<false, false>), grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
@@ -376,6 +388,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.absent_code0 = false;
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
+    dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         dn.desc = down_desc + down_off[d];
@@ -384,8 +397,12 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
         const bool ap = c->leaves_all_present;
-        const bool dense = virt && ht.down_dense_v;   // level d = dense indices [down_off[d], down_off[d+1])
-        dn.dense_base = dense ? down_off[d] : -1;
+        // level d = one range of dense indices: [down_off[d], down_off[d+1]) in the leaf-parent
+        // form, from down_dense_base_k[d] in the subtree form
+        const bool dense = sub ? ht.down_dense_k : virt && ht.down_dense_v;
+        dn.dense_base = !dense ? -1 : sub ? ht.down_dense_base_k[d] : down_off[d];
+        // (subtree form: the levels' descriptors omit S2 / S3 children, whose records come
+        // from the tail launch, so the lean kernels run every level)
         if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (block) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
@@ -393,13 +410,14 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
-    dn.tail = virt ? dt.tail_desc_v : dt.tail_desc;
-    dn.count = virt ? ht.num_tail_v : ht.num_tail;
+    dn.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
+    dn.count = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
     if (dn.count > 0) {
         const dim3 grid = wave_grid(dn.count, tiles);
         const bool ap = c->leaves_all_present;
         timer_begin(c, 1);
-        if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);

@@ -72,6 +72,11 @@ void free_tree(DevTree& t) {
     dev_free(t.vleaf);
     dev_free(t.part_desc);
     dev_free(t.part_desc_v);
+    dev_free(t.child_enc_k);
+    dev_free(t.up_desc_k);
+    dev_free(t.down_desc_k);
+    dev_free(t.vinner);
+    dev_free(t.tail_desc_k);
     t = DevTree{};
 }
 
@@ -192,7 +197,8 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
-    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)(uintptr_t)c->sk_parts,
+    const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
+                              (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
                               (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals, (uint64_t)(uintptr_t)c->root_final,
@@ -367,6 +373,10 @@ int pm_set_stream(pm_ctx* c, void* s) {
 
 int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (!c) return PM_ERR_ARG;
+    if (option == PM_OPT_SUBTREE) {
+        c->subtree_form = value != 0;
+        return PM_OK;
+    }
     if (option == PM_OPT_VIRTUAL) {
         c->virtual_leaf_parents = value != 0;
         return PM_OK;
@@ -466,6 +476,25 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             if (off[idx[e] + 1] > off[idx[e]]) return false;
         return true;
     };
+    // Subtree form (Fitch, every leaf present): a node whose two children are leaves or
+    // two-leaf cherries, at least one a cherry, under a parent of out-degree <= 2, is also
+    // evaluated inline by its parent (shapes S2 = (cherry, leaf), S3 = (cherry, cherry)).
+    auto cherry2 = [&](int32_t u) {
+        return u != t->root && off[u + 1] - off[u] == 2 && off[idx[off[u]] + 1] == off[idx[off[u]]] &&
+               off[idx[off[u] + 1] + 1] == off[idx[off[u] + 1]];
+    };
+    auto sshape_id = [&](int32_t u) {
+        if (u == t->root || off[u + 1] - off[u] != 2 || parent[u] < 0 || off[parent[u] + 1] - off[parent[u]] > 2)
+            return 0;
+        int cherries = 0;
+        for (int32_t e = off[u]; e < off[u + 1]; ++e) {
+            const int32_t ch = idx[e];
+            if (off[ch + 1] == off[ch]) continue;
+            if (!cherry2(ch)) return 0;
+            ++cherries;
+        }
+        return cherries;   // 1: S2, 2: S3
+    };
     {
         std::vector<int32_t> inner;
         for (const int32_t i : dfs) {
@@ -479,10 +508,20 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         // stable counting sort by (virtual, depth): DFS order kept within a key
         int32_t maxd = 0;
         for (const int32_t i : inner) maxd = std::max(maxd, depth[i]);
-        const int32_t nk = 2 * (maxd + 1);
+        // key (leaf-parent form virtual, depth, subtree-form virtual): a pre-order level of
+        // either form is one contiguous range of dense indices
+        // (subtree form: within a depth, nodes without an S2 / S3 child, then those with one,
+        // then the S2 / S3 nodes -- so each half of a subtree-form level is one range too)
+        auto has_sub_child = [&](int32_t u) {
+            for (int32_t e = off[u]; e < off[u + 1]; ++e)
+                if (sshape_id(idx[e])) return true;
+            return false;
+        };
+        const int32_t nk = 8 * (maxd + 1);
         std::vector<int32_t> key(inner.size()), start(nk + 1, 0);
         for (size_t k = 0; k < inner.size(); ++k) {
-            key[k] = (virtual_id(inner[k]) ? maxd + 1 : 0) + depth[inner[k]];
+            const int32_t u = inner[k];
+            key[k] = (virtual_id(u) ? 4 * (maxd + 1) : 0) + 4 * depth[u] + (sshape_id(u) ? 2 : has_sub_child(u) ? 1 : 0);
             ++start[key[k] + 1];
         }
         for (int32_t k = 0; k < nk; ++k) start[k + 1] += start[k];
@@ -620,6 +659,65 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
 
     upload_phase("virtual form");
+    // subtree form (Fitch, all leaves present): S2 / S3 nodes dropped from the levels as well;
+    // child encodings carry the shape (kShapeShift), vleaf their leaves (a, b[, c[, d]]) and
+    // vinner their cherries (x[, y])
+    std::vector<int32_t> child_enc_k(child_enc_v), up_order_k, down_order_k, vinner((size_t)I * 2, -1);
+    std::vector<uint8_t> sshape(I, 0);
+    {
+        for (int32_t d = 0; d < I; ++d) {
+            const int sh = sshape_id(ht.internal_id[d]);
+            if (!sh) continue;
+            sshape[d] = (uint8_t)sh;
+            // leaves: the cherries' leaves first, then the lone leaf (S2)
+            int32_t nl = 0, ni = 0;
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                const int32_t x = ht.child_enc[e];
+                if (x < 0) continue;
+                vinner[(size_t)d * 2 + ni++] = x;
+                for (int32_t f = ht.child_off[x]; f < ht.child_off[x + 1]; ++f) vleaf[(size_t)d * 4 + nl++] = -ht.child_enc[f] - 1;
+            }
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e)
+                if (ht.child_enc[e] < 0) vleaf[(size_t)d * 4 + nl++] = -ht.child_enc[e] - 1;
+            ht.num_sshape += 1;
+        }
+        for (auto& x : child_enc_k)
+            if (x >= 0 && !(x & kVirtualBit) && sshape[x]) x = (x | kVirtualBit) | (sshape[x] << kShapeShift);
+        auto keep = [&](std::vector<int32_t>& order, std::vector<int32_t>& offs, const std::vector<int32_t>& src_order,
+                        const std::vector<int32_t>& src_offs) {
+            order.clear();
+            offs.assign(1, 0);
+            for (size_t k = 0; k + 1 < src_offs.size(); ++k) {
+                for (int32_t i = src_offs[k]; i < src_offs[k + 1]; ++i)
+                    if (!sshape[src_order[i]]) order.push_back(src_order[i]);
+                offs.push_back((int32_t)order.size());
+            }
+        };
+        keep(up_order_k, ht.up_class_off_k, up_order_v, ht.up_class_off_v);
+        ht.up_level_off_k.assign(H + 1, 0);
+        for (int32_t h = 0; h <= H; ++h) ht.up_level_off_k[h] = ht.up_class_off_k[h * kDegreeClasses];
+        ht.up_leafy_k.assign(H, 0);
+        for (int32_t h = 0; h < H; ++h) {
+            bool leafy = true;
+            for (int32_t i = ht.up_class_off_k[h * kDegreeClasses]; i < ht.up_class_off_k[h * kDegreeClasses + 1] && leafy; ++i)
+                for (int32_t e = ht.child_off[up_order_k[i]]; e < ht.child_off[up_order_k[i] + 1]; ++e)
+                    leafy &= child_enc_k[e] < 0 || (child_enc_k[e] & kVirtualBit) != 0;
+            ht.up_leafy_k[h] = leafy;
+        }
+        keep(down_order_k, ht.down_level_off_k, down_order_v, ht.down_level_off_v);
+        // each subtree-form pre-order level is one dense range (dense key: depth, then S2/S3 last)
+        ht.down_dense_base_k.assign(ht.down_level_off_k.size() - 1, -1);
+        bool dense = true;
+        for (size_t l = 0; l + 1 < ht.down_level_off_k.size(); ++l) {
+            const int32_t a = ht.down_level_off_k[l], b = ht.down_level_off_k[l + 1];
+            if (a == b) continue;
+            for (int32_t i = a; i < b; ++i) dense &= down_order_k[i] == down_order_k[a] + (i - a);
+            ht.down_dense_base_k[l] = down_order_k[a];
+        }
+        ht.down_dense_k = dense;
+    }
+    ht.sshape = sshape;
+    upload_phase("subtree form");
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<NodeDesc> desc(order.size());
         for (size_t k = 0; k < order.size(); ++k) {
@@ -633,9 +731,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             x.c0 = enc[x.e0];
             x.c1 = x.e1 - x.e0 > 1 ? enc[x.e0 + 1] : 0;
             for (int j = 0; j < 4; ++j) {
-                x.vl0[j] = x.c0 >= 0 && (x.c0 & kVirtualBit) ? vleaf[(size_t)(x.c0 & ~kVirtualBit) * 4 + j] : -1;
+                x.vl0[j] = x.c0 >= 0 && (x.c0 & kVirtualBit) ? vleaf[(size_t)(x.c0 & kDenseMask) * 4 + j] : -1;
                 x.vl1[j] = x.e1 - x.e0 > 1 && x.c1 >= 0 && (x.c1 & kVirtualBit)
-                               ? vleaf[(size_t)(x.c1 & ~kVirtualBit) * 4 + j] : -1;
+                               ? vleaf[(size_t)(x.c1 & kDenseMask) * 4 + j] : -1;
             }
         }
         return desc;
@@ -644,6 +742,32 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const std::vector<NodeDesc> down_desc_v = make_desc(down_order_v, child_enc_v);
     const std::vector<NodeDesc> up_desc = make_desc(up_order, ht.child_enc);
     const std::vector<NodeDesc> up_desc_v = make_desc(up_order_v, child_enc_v);
+    const std::vector<NodeDesc> up_desc_k = make_desc(up_order_k, child_enc_k);
+    // subtree-form pre-order descriptors list only the children the level kernel handles:
+    // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
+    // materialised placeholder (c0 = 0, no loads, no records)
+    std::vector<NodeDesc> down_desc_k = make_desc(down_order_k, child_enc_k);
+    for (NodeDesc& x : down_desc_k) {
+        const int32_t deg = x.e1 - x.e0;
+        if (deg > 2) continue;   // S2 / S3 nodes have parents of out-degree <= 2
+        int32_t keep_enc[2], keep_vl[2][4], nk = 0;
+        for (int j = 0; j < deg; ++j) {
+            const int32_t enc = j == 0 ? x.c0 : x.c1;
+            if (enc >= 0 && (enc & kVirtualBit) && ((enc >> kShapeShift) & 3)) continue;
+            keep_enc[nk] = enc;
+            for (int q = 0; q < 4; ++q) keep_vl[nk][q] = j == 0 ? x.vl0[q] : x.vl1[q];
+            ++nk;
+        }
+        if (nk == deg) continue;
+        x.e0 = 0;
+        x.e1 = std::max(nk, 1);
+        x.c0 = nk > 0 ? keep_enc[0] : 0;
+        x.c1 = nk > 1 ? keep_enc[1] : 0;
+        for (int q = 0; q < 4; ++q) {
+            x.vl0[q] = nk > 0 ? keep_vl[0][q] : -1;
+            x.vl1[q] = nk > 1 ? keep_vl[1][q] : -1;
+        }
+    }
     auto make_tail = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<TailDesc> tail;
         for (int32_t d : order)
@@ -653,7 +777,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 TailDesc t{};
                 t.parent = d;
                 t.enc = x;
-                for (int j = 0; j < 4; ++j) t.vl[j] = x >= 0 ? vleaf[(size_t)(x & ~kVirtualBit) * 4 + j] : -1;
+                for (int j = 0; j < 4; ++j) t.vl[j] = x >= 0 ? vleaf[(size_t)(x & kDenseMask) * 4 + j] : -1;
                 tail.push_back(t);
             }
         return tail;
@@ -663,6 +787,16 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
     ht.num_tail_v = (int32_t)tail_desc_v.size();
+    std::vector<TailDesc> tail_desc_k = tail_desc_v;   // + every S2 / S3 node, its parent's final read back
+    for (int32_t d = 0; d < I; ++d) {
+        if (!sshape[d]) continue;
+        TailDesc t{};
+        t.parent = parent_dense[d];
+        t.enc = (d | kVirtualBit) | (sshape[d] << kShapeShift);
+        for (int j = 0; j < 4; ++j) t.vl[j] = vleaf[(size_t)d * 4 + j];
+        tail_desc_k.push_back(t);
+    }
+    ht.num_tail_k = (int32_t)tail_desc_k.size();
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
     std::vector<PartDesc> part_desc[2];
@@ -712,7 +846,12 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.part_desc, part_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess) {
+        (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.child_enc_k, child_enc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_k, up_desc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||
+        (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }

@@ -95,9 +95,19 @@ struct DevTree {
     // Sankoff parts of the nodes of out-degree > 255 ([0] over child_enc, [1] over child_enc_v)
     PartDesc* part_desc = nullptr;
     PartDesc* part_desc_v = nullptr;
+    // subtree form (Fitch, all leaves present): S2 / S3 nodes inline in their parent too
+    int32_t* child_enc_k = nullptr;   // [E] shapes in bits 28-29
+    NodeDesc* up_desc_k = nullptr;
+    NodeDesc* down_desc_k = nullptr;
+    int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
+    TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
+// Subtree form: a virtual child's shape in bits 28-29 of its encoding (0 = one or two leaves,
+// 1 = S2 (cherry, leaf), 2 = S3 (cherry, cherry)); the dense index is the low 28 bits.
+constexpr int kShapeShift = 28;
+constexpr int32_t kDenseMask = (1 << kShapeShift) - 1;
 
 struct HostTree {
     int32_t num_nodes = 0;
@@ -123,6 +133,13 @@ struct HostTree {
     // have none) of each form, and every descriptor's out-degree ([0] plain, [1] virtual form)
     std::vector<int32_t> part_off, part_off_v;
     std::vector<int32_t> up_degree[2];
+    // subtree form: levels without the S2 / S3 nodes, each pre-order level's first dense index
+    std::vector<int32_t> up_level_off_k, up_class_off_k, down_level_off_k, down_dense_base_k;
+    std::vector<uint8_t> up_leafy_k;
+    bool down_dense_k = false;
+    int64_t num_sshape = 0;
+    std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
+    int32_t num_tail_k = 0;
 };
 
 struct Timer {
@@ -144,6 +161,7 @@ struct pm_ctx {
     bool has_tree = false;
     int32_t max_degree = 0;
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
+    bool subtree_form = true;         // Fitch, all leaves present: S2 / S3 inline too (PM_OPT_SUBTREE)
 
     // column shard
     int64_t num_sites = 0;

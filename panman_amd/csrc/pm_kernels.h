@@ -449,7 +449,9 @@ struct ChildFetch {
 };
 
 // LEAFY: the caller knows c is a leaf or a virtual leaf-parent (no record, fewer registers).
-template <int REC = kFitchRec, bool LEAFY = false>
+// SUB: subtree form -- a virtual child may be an S2 / S3 subtree (three or four leaves, in
+// code, v[0], v[1], v[2]).
+template <int REC = kFitchRec, bool LEAFY = false, bool SUB = false>
 __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
                                                ChildFetch& f) {
     f.cx = false;
@@ -459,6 +461,11 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
         f.code = a.leaf_planes[(size_t)l0 * a.wpad + word];
         if (l1 >= 0) f.v[0] = a.leaf_planes[(size_t)l1 * a.wpad + word];
+        if constexpr (SUB) {
+            const int32_t l2 = __builtin_amdgcn_readfirstlane(vl.z), l3 = __builtin_amdgcn_readfirstlane(vl.w);
+            if (l2 >= 0) f.v[1] = a.leaf_planes[(size_t)l2 * a.wpad + word];
+            if (l3 >= 0) f.v[2] = a.leaf_planes[(size_t)l3 * a.wpad + word];
+        }
     } else if (!LEAFY) {
         const size_t rec = (size_t)c * a.tiles + tile;
         const RecMask m = rec_mask(a.cmask, rec);
@@ -472,12 +479,46 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
     }
 }
 
+__device__ __forceinline__ uint32_t code_ne(const uint4& p, const uint4& q) {
+    return (p.x ^ q.x) | (p.y ^ q.y) | (p.z ^ q.z) | (p.w ^ q.w);
+}
+
+// An S2 (cherry (a, b), leaf c) or S3 (cherries (a, b), (c, d)) child's Fitch set, from the
+// union of its cherry's leaves (src/fitchSankoff.cpp:39-55 applied twice):
+//   S2: {c} where c is a or b, else {a, b, c};   S3: X & Y where the cherries share a code,
+//   else X | Y.  vd: sites where the subtree's leaves are not all one code (dirty lanes).
+__device__ __forceinline__ void subtree_set_ap(int shape, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
+    const uint4 A = f.code, B = f.v[0], Cc = f.v[1];
+    const LoHi u = lohi_of(B.x, B.y, B.z, B.w, ~0u), w = lohi_of(Cc.x, Cc.y, Cc.z, Cc.w, ~0u);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];   // X = {a, b}
+    if (shape == 1) {
+        vd |= code_ne(A, B) | code_ne(A, Cc);
+        const uint32_t in_x = ~code_ne(Cc, A) | ~code_ne(Cc, B);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) x[v] = (x[v] & ~in_x) | (w.lo[v & 3] & w.hi[v >> 2]);
+    } else {
+        const uint4 D = f.v[2];
+        vd |= code_ne(A, B) | code_ne(A, Cc) | code_ne(A, D);
+        const LoHi z = lohi_of(D.x, D.y, D.z, D.w, ~0u);
+        const uint32_t nz = ~code_ne(A, Cc) | ~code_ne(A, D) | ~code_ne(B, Cc) | ~code_ne(B, D);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const uint32_t y = (w.lo[v & 3] & w.hi[v >> 2]) | (z.lo[v & 3] & z.hi[v >> 2]);
+            x[v] = (x[v] & y) | ((x[v] | y) & ~nz);
+        }
+    }
+}
+
 // A fetched child's 16-plane set (Fitch) / optimal set Z0 (Sankoff); vd as fold_child's.
+template <bool SUB = false>
 __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
     const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u);
 #pragma unroll
     for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
-    if (c >= 0 && (c & kVirtualBit)) {
+    if (SUB && c >= 0 && (c & kVirtualBit) && ((c >> kShapeShift) & 3)) {
+        subtree_set_ap((c >> kShapeShift) & 3, f, x, vd);
+    } else if (c >= 0 && (c & kVirtualBit)) {
         if (__builtin_amdgcn_readfirstlane(vl.y) >= 0) {
             const uint4 L1 = f.v[0];
             vd |= (f.code.x ^ L1.x) | (f.code.y ^ L1.y) | (f.code.z ^ L1.z) | (f.code.w ^ L1.w);
@@ -493,10 +534,11 @@ __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetc
     }
 }
 
+template <bool SUB = false>
 __device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
                                               uint32_t& vd) {
     uint32_t x[16];
-    child_set_ap(c, vl, f, x, vd);
+    child_set_ap<SUB>(c, vl, f, x, vd);
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         both[v] &= x[v];
@@ -551,6 +593,7 @@ struct DownArgs {
     const TailDesc* tail;  // k_tail items
     int32_t count;
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
+    const int32_t* vinner; // subtree form: an S2 / S3 node's cherries (dense), [I][2]
     const int32_t* child_off;
     const int32_t* child_enc;
     const int32_t* parent_dense;
@@ -724,14 +767,19 @@ struct Kid {
     int4 vl = make_int4(-1, -1, -1, -1);
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = make_uint4(0, 0, 0, 0);
     uint32_t m0 = 0, m1 = 0;
+    // subtree form (S2 / S3 child): third and fourth leaf, node ids of its cherries
+    uint4 L2 = make_uint4(0, 0, 0, 0), L3 = make_uint4(0, 0, 0, 0);
+    int32_t ix = -1, iy = -1;
 };
+
+__device__ __forceinline__ int kid_shape(int32_t enc) { return enc >= 0 && (enc & kVirtualBit) ? (enc >> kShapeShift) & 3 : 0; }
 
 // A clean lane of the parent (not `dirty`, RecMask::d) fetches nothing: its children hold
 // the parent's code there, so their masks stay 0 and they emit no records.
 // Loads are written as "initialise, then exec-masked load" with the leaf choice made on
 // uniform values first: zero-filling a load's registers on a sibling branch instead makes
 // the compiler drain every outstanding load (s_waitcnt vmcnt(0)) between the fetches.
-template <Mode M, bool AP>
+template <Mode M, bool AP, bool SUB = false>
 __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 vl, int64_t word, bool dirty, Kid& k) {
     k.enc = enc;
     int32_t l0 = -1, l1 = -1;
@@ -753,6 +801,17 @@ __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 v
         if (l1 >= 0 && dirty) {
             k.L1 = a.leaf_planes[(size_t)l1 * a.wpad + word];
             k.m1 = ~0u;
+        }
+        if constexpr (SUB) {
+            const int sh = kid_shape(enc);
+            if (sh) {   // S2 / S3: the other leaves and the cherries' ids (scalar loads)
+                k.L2 = k.L3 = make_uint4(0, 0, 0, 0);
+                if (dirty) k.L2 = a.leaf_planes[(size_t)k.vl.z * a.wpad + word];
+                if (sh == 2 && dirty) k.L3 = a.leaf_planes[(size_t)k.vl.w * a.wpad + word];
+                const int32_t v = enc & kDenseMask;
+                k.ix = a.internal_id[a.vinner[2 * v]];
+                if (sh == 2) k.iy = a.internal_id[a.vinner[2 * v + 1]];
+            }
         }
     } else {
         if (l0 >= 0 && dirty) leaf_fetch<AP>(a, l0, word, k.L0, k.m0);
@@ -783,16 +842,104 @@ __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint
 struct KidOut {
     uint32_t F[4];
     uint32_t self, d0, d1;
+    uint32_t nsub;   // subtree form: records of an S2 / S3 child's subtree (rebuilt by kid_put)
 };
 
-template <Mode M>
+__device__ __forceinline__ uint4 sel4(uint32_t t, const uint4& p, const uint4& q) {
+    return make_uint4(bsel(t, p.x, q.x), bsel(t, p.y, q.y), bsel(t, p.z, q.z), bsel(t, p.w, q.w));
+}
+__device__ __forceinline__ uint4 min4(const uint4& p, const uint4& q) {   // lower code per site
+    const uint32_t P[4] = {p.x, p.y, p.z, p.w}, Q[4] = {q.x, q.y, q.z, q.w};
+    return sel4(code_less(Q, P), q, p);
+}
+
+// Fitch finals inside an S2 / S3 child v given its parent's final P (src/fitchSankoff.cpp:
+// 115-123 at v, then at its cherries; leaves keep their codes):
+//   S2 (x = (a, b), c): S_v = {c} if c in {a, b}, else {a, b, c};
+//   S3 (x = (a, b), y = (c, d)): S_v = X & Y if the cherries share a code, else X | Y.
+//   F_v = P if P in S_v else lowest(S_v);  F_x = F_v if F_v in {a, b} else min(a, b); F_y alike.
+// Nothing is kept between counting and writing the records: both recompute from the leaves
+// (VALU is cheaper here than the registers that would hold the finals and masks).
+struct SubFinals {
+    uint4 F, G, H;
+};
+
+__device__ __forceinline__ SubFinals subtree_finals(const Kid& k, int sh, const uint4& P) {
+    const uint4 A = k.L0, B = k.L1, Cc = k.L2;
+    const uint4 mab = min4(A, B);
+    const uint32_t ePa = ~code_ne(P, A), ePb = ~code_ne(P, B), ePc = ~code_ne(P, Cc);
+    SubFinals r;
+    if (sh == 1) {
+        const uint32_t in_x = ~code_ne(Cc, A) | ~code_ne(Cc, B);
+        const uint32_t hit = ePc | (~in_x & (ePa | ePb));
+        r.F = sel4(hit, P, sel4(in_x, Cc, min4(mab, Cc)));
+        r.H = r.F;
+    } else {
+        const uint4 D = k.L3;
+        const uint32_t ia = ~code_ne(A, Cc) | ~code_ne(A, D), ib = ~code_ne(B, Cc) | ~code_ne(B, D), nz = ia | ib;
+        const uint32_t hit = (nz & ((ePa & ia) | (ePb & ib))) | (~nz & (ePa | ePb | ePc | ~code_ne(P, D)));
+        const uint4 mcd = min4(Cc, D);
+        r.F = sel4(hit, P, sel4(nz, sel4(ia & ib, mab, sel4(ia, A, B)), min4(mab, mcd)));
+        r.H = sel4(~code_ne(r.F, Cc) | ~code_ne(r.F, D), r.F, mcd);
+    }
+    r.G = sel4(~code_ne(r.F, A) | ~code_ne(r.F, B), r.F, mab);
+    return r;
+}
+
+// Records of an S2 / S3 subtree per lane: v, x, (y,) a, b, c, (d).
+__device__ __forceinline__ uint32_t subtree_count(const Kid& k, int sh, uint32_t valid, const uint4& P) {
+    const SubFinals f = subtree_finals(k, sh, P);
+    const uint32_t M = valid & k.m0;
+    uint32_t n = __builtin_popcount(M & code_ne(f.F, P)) + __builtin_popcount(M & code_ne(f.G, f.F)) +
+                 __builtin_popcount(M & code_ne(k.L0, f.G)) + __builtin_popcount(M & code_ne(k.L1, f.G)) +
+                 __builtin_popcount(M & code_ne(k.L2, f.H));
+    if (sh == 2) n += __builtin_popcount(M & code_ne(f.H, f.F)) + __builtin_popcount(M & code_ne(k.L3, f.H));
+    return n;
+}
+
+// One record stream per iteration (v, x, a, b, c[, y, d]): a single put_records body serves
+// them all, selected by the wave-uniform stream index.
+template <class Sink>
+__device__ __forceinline__ void subtree_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, int sh,
+                                            uint32_t valid, const uint32_t* Fn, int64_t word) {
+    const uint4 P = make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]);
+    const SubFinals f = subtree_finals(k, sh, P);
+    const uint32_t M = valid & k.m0;
+    const int streams = sh == 1 ? 5 : 7;
+#pragma unroll 1
+    for (int st = 0; st < streams; ++st) {
+        uint4 pc = P, cc = f.F;
+        int32_t node = a.internal_id[k.enc & kDenseMask];
+        switch (st) {
+            case 1: node = k.ix; pc = f.F; cc = f.G; break;
+            case 2: node = a.leaf_id[k.vl.x]; pc = f.G; cc = k.L0; break;
+            case 3: node = a.leaf_id[k.vl.y]; pc = f.G; cc = k.L1; break;
+            case 4: node = a.leaf_id[k.vl.z]; pc = sh == 1 ? f.F : f.H; cc = k.L2; break;
+            case 5: node = k.iy; pc = f.F; cc = f.H; break;
+            case 6: node = a.leaf_id[k.vl.w]; pc = f.H; cc = k.L3; break;
+            default: break;
+        }
+        const uint32_t pcs[4] = {pc.x, pc.y, pc.z, pc.w};
+        put_records(sink, p, (uint32_t)node, M & code_ne(cc, pc), word, pcs, cc.x, cc.y, cc.z, cc.w);
+    }
+}
+
+template <Mode M, bool SUB = false>
 __device__ __forceinline__ void kid_prepare(const Kid& k, uint32_t valid, const uint32_t* Fn, KidOut& o) {
     o.self = o.d0 = o.d1 = 0;
+    if constexpr (SUB) o.nsub = 0;
     if (k.enc < 0) {
         o.d0 = valid & k.m0 & diff4(k.L0, Fn);
         return;
     }
     if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
+    if constexpr (SUB) {
+        const int sh = kid_shape(k.enc);
+        if (sh) {
+            o.nsub = subtree_count(k, sh, valid, make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]));
+            return;
+        }
+    }
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
     virt_fold(k.L0, k.m0, Fn, low, have, hit);
     virt_fold(k.L1, k.m1, Fn, low, have, hit);
@@ -812,11 +959,14 @@ __device__ __forceinline__ void kid_prepare(const Kid& k, uint32_t valid, const 
     o.d1 = valid & k.m1 & diff4(k.L1, o.F);
 }
 
+template <bool SUB = false>
 __device__ __forceinline__ uint32_t kid_count(const KidOut& o) {
-    return (uint32_t)(__builtin_popcount(o.self) + __builtin_popcount(o.d0) + __builtin_popcount(o.d1));
+    uint32_t n = (uint32_t)(__builtin_popcount(o.self) + __builtin_popcount(o.d0) + __builtin_popcount(o.d1));
+    if constexpr (SUB) n += o.nsub;
+    return n;
 }
 
-template <Mode M, class Sink>
+template <Mode M, bool SUB = false, class Sink>
 __device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
                                         int64_t word, const uint32_t* Fn) {
     if (k.enc < 0) {
@@ -824,20 +974,27 @@ __device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uin
         return;
     }
     if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
-    put_records(sink, p, (uint32_t)a.internal_id[k.enc & ~kVirtualBit], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
+    if constexpr (SUB) {
+        const int sh = kid_shape(k.enc);
+        if (sh) {   // S2 / S3: v, its cherries and the leaves (recomputed, subtree_put)
+            subtree_put(a, sink, p, k, sh, valid_mask(a, word), Fn, word);
+            return;
+        }
+    }
+    put_records(sink, p, (uint32_t)a.internal_id[k.enc & kDenseMask], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
     put_records(sink, p, (uint32_t)a.leaf_id[k.vl.x], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
     if (k.vl.y >= 0) put_records(sink, p, (uint32_t)a.leaf_id[k.vl.y], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
 }
 
 // Records of one child (k_tail items): one sink reservation per lane.
-template <Mode M, bool AP, class Sink>
+template <Mode M, bool AP, bool SUB = false, class Sink>
 __device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
                                             uint32_t valid, const uint32_t* F) {
     KidOut o;
-    kid_prepare<M>(k, valid, F, o);
-    const uint32_t n = kid_count(o);
+    kid_prepare<M, SUB>(k, valid, F, o);
+    const uint32_t n = kid_count<SUB>(o);
     uint32_t p = n ? sink.reserve(n) : 0u;   // every lane stays active (put_records expands cooperatively)
-    kid_put<M>(a, sink, p, k, o, word, F);
+    kid_put<M, SUB>(a, sink, p, k, o, word, F);
 }
 
 // Every record of node n's wave: the node itself and its first two children (prefetched
@@ -975,8 +1132,23 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 // two children's words) is issued before any of them is consumed.
 // DENSE: the level's nodes are the dense indices dense_base + item (DevTree down order),
 // so the record masks are fetched alongside the descriptor, not after it.
-template <Mode M, bool AP, bool DENSE>
-__global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
+// Inclusive prefix sum of v over the wave's lanes.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// SUB: subtree form (Fitch, every leaf present) -- the first two children may be S2 / S3
+// subtrees, whose inner finals and records this wave produces (subtree_prepare).
+#ifndef PM_SUB_DOWN_WAVES
+#define PM_SUB_DOWN_WAVES 4
+#endif
+template <Mode M, bool AP, bool DENSE, bool SUB = false>
+__global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1003,8 +1175,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode:
     }
     const bool dirty = is_root || ((m.d >> lane) & 1ull);
     Kid kids[2];
-    kid_fetch<M, AP>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M, AP>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
+    kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
     uint32_t z1[16];
     if constexpr (M == Mode::kSankoff) {
         load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
@@ -1044,11 +1216,11 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode:
     // and the shard reservation's global atomic issued before the records are built, so
     // its round trip overlaps the staging.
     KidOut o0, o1;
-    kid_prepare<M>(kids[0], valid, F, o0);
+    kid_prepare<M, SUB>(kids[0], valid, F, o0);
     const bool two = e1 - e0 > 1;
-    if (two) kid_prepare<M>(kids[1], valid, F, o1);
-    else o1.self = o1.d0 = o1.d1 = 0;
-    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count(o0) + kid_count(o1);
+    if (two) kid_prepare<M, SUB>(kids[1], valid, F, o1);
+    else o1.self = o1.d0 = o1.d1 = o1.nsub = 0;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count<SUB>(o0) + kid_count<SUB>(o1);
     uint32_t incl = cnt;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -1065,8 +1237,8 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode:
     uint32_t rp = p0;
     const LdsSink ls{stage[wave], nullptr};
     put_records(ls, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M>(a, ls, rp, kids[0], o0, word, F);
-    if (two) kid_put<M>(a, ls, rp, kids[1], o1, word, F);
+    kid_put<M, SUB>(a, ls, rp, kids[0], o0, word, F);
+    if (two) kid_put<M, SUB>(a, ls, rp, kids[1], o1, word, F);
     base = __shfl(base, 0, 64);
     pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
     if (total <= kStage) {
@@ -1078,13 +1250,16 @@ __global__ __launch_bounds__(kBlock, (M == Mode::kFitch && AP) ? 8 : (M == Mode:
     const GlobalSink gs{out, (int64_t)base, a.shard_cap, nullptr};
     rp = p0;
     put_records(gs, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M>(a, gs, rp, kids[0], o0, word, F);
-    if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
+    kid_put<M, SUB>(a, gs, rp, kids[0], o0, word, F);
+    if (two) kid_put<M, SUB>(a, gs, rp, kids[1], o1, word, F);
 }
 
 // Records of the leaf / virtual children beyond a node's second (polytomies), after the
 // pre-order levels: wave = (tail item, tile), parent final read back (node_final).
-template <Mode M, bool AP>
+// SUB: subtree form -- the S2 / S3 children are tail items too (their inner finals and
+// records from the parent's final and their leaves, subtree_put), so the level kernels stay
+// lean.
+template <Mode M, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     __shared__ uint32_t stage_cnt[kWavesPerBlock];
@@ -1100,10 +1275,10 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     const bool proot = t.parent == a.root_dense;
     const RecMask pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
     Kid k;
-    kid_fetch<M, AP>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
+    kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
     const uint4 q = node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, t.parent, tile, lane, word);
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
-    kid_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
+    kid_records<M, AP, SUB>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
@@ -1111,7 +1286,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     pm_mut* out;
     if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
     if (lane == 0) stage_cnt[wave] = 0;
-    kid_records<M, AP>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
+    kid_records<M, AP, SUB>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
 }
 
 }  // namespace pm

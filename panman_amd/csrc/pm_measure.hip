@@ -97,20 +97,26 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "record masks");
     const bool virt = c->virtual_leaf_parents;
+    const bool sub = virt && mode == PM_MODE_FITCH && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
     const int32_t root = c->dt.root_dense;
-    // virtual leaf-parents as pm_tree_upload forms them: not the root, one or two children, all leaves
+    // virtual nodes as pm_tree_upload forms them (leaf-parents: not the root, one or two
+    // children, all leaves; subtree form: S2 / S3 too): vnode = the leaves their parent reads
     std::vector<uint8_t> vnode(I, 0);
     if (virt)
         for (int32_t d = 0; d < I; ++d) {
             const int32_t deg = ht.child_off[d + 1] - ht.child_off[d];
             bool all = d != root && deg <= 2;
             for (int32_t k = ht.child_off[d]; k < ht.child_off[d + 1] && all; ++k) all = ht.child_enc[k] < 0;
-            vnode[d] = all;
+            vnode[d] = all ? (uint8_t)deg : 0;
+            if (sub && ht.sshape[d]) vnode[d] = (uint8_t)(ht.sshape[d] + 2);
         }
     const double lane = 16.0, word_row = lane * kWave;   // one lane's code planes; one wave's leaf word
     const double cx_full = mode == PM_MODE_FITCH ? 64.0 : 128.0;   // complex lane: 16 planes / Z0 + Z1
     const double cx_read_up = 64.0;                                // the parent reads Fitch planes / Z0
     double up = 0.0, down = 0.0;
+    // components: up leaf words, up child records, up own records + pushes, down own records,
+    // down parent finals, down dirty leaf words, down finals written, down tail items
+    double part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
     for (int32_t d = 0; d < I; ++d) {
         if (vnode[d]) continue;
@@ -120,27 +126,42 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             const double rec = 64.0 + lane * popc(q[1]) + cx_full * popc(q[0]);
             // post-order: children in, own record + masks out, parent masks pushed to children
             up += rec;
+            part[2] += rec;
             const double dirty = d == root ? kWave : popc(q[2]);
             for (int32_t k = e0; k < e1; ++k) {
                 const int32_t ch = ht.child_enc[k];
                 if (ch < 0) {
                     up += word_row;
                     down += lane * dirty;
+                    part[0] += word_row;
+                    part[5] += lane * dirty;
                 } else if (vnode[ch]) {
-                    const int32_t nl = ht.child_off[ch + 1] - ht.child_off[ch];
+                    const int32_t nl = vnode[ch];
                     up += word_row * nl;
                     down += lane * dirty * nl;
+                    part[0] += word_row * nl;
+                    part[5] += lane * dirty * nl;
                 } else {
                     const uint64_t* r = mk(ch, t);
-                    up += 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
+                    const double b = 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
+                    up += b;
+                    part[1] += b;
                 }
-                if (k >= e0 + 2 && (ch < 0 || vnode[ch]))   // k_tail item: parent masks + parent final
+                if (k >= e0 + 2 && (ch < 0 || vnode[ch])) {   // k_tail item: parent masks + parent final
                     down += 64.0 + lane * popc(q[0] | q[1]);
+                    part[7] += 64.0 + lane * popc(q[0] | q[1]);
+                }
             }
             // pre-order: own record, parent final (non-consensus lanes), compact final out
             down += rec;
-            if (d == root) down += 2.0 * word_row;   // forced / root final
-            else down += lane * popc(q[3] | q[4]) + lane * popc(q[0]);
+            part[3] += rec;
+            if (d == root) {
+                down += 2.0 * word_row;   // forced / root final
+            } else {
+                down += lane * popc(q[3] | q[4]) + lane * popc(q[0]);
+                part[4] += lane * popc(q[3] | q[4]);
+                part[6] += lane * popc(q[0]);
+            }
         }
     }
     down += 8.0 * (double)records;
@@ -149,6 +170,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     out[2] = 8.0 * (double)records + 4.0 * (double)c->num_sites;   // score histogram
     out[3] = 0.5 * (double)L * (double)c->num_sites + 8.0 * (double)records;   // floor: leaf codes once + records
     out[4] = (double)records;
+    for (int k = 0; k < 8 && 5 + k < n; ++k) out[5 + k] = part[k];
     return PM_OK;
 }
 

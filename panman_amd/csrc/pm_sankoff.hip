@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
         const int4 vl = !(c >= 0 && (c & kVirtualBit)) ? make_int4(-1, -1, -1, -1)
                         : e == e0                       ? make_int4(d.vl0[0], d.vl0[1], -1, -1)
                         : e == e0 + 1                   ? make_int4(d.vl1[0], d.vl1[1], -1, -1)
-                                                        : a.vleaf[c & ~kVirtualBit];
+                                                        : a.vleaf[c & kDenseMask];
         child_z0(a, c, __builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y), tile, lane, word, z);
         count_child<B>(cnt, finite, z);   // an all-INF child adds nothing (:398-400)
     }
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
     for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
         const int32_t my = base + kWavesPerBlock * lane;
         const int32_t enc = my < e1 ? a.child_enc[my] : 0;
-        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+        const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask]
                                                                    : make_int4(-1, -1, -1, -1);
         const int cntc = min(kWave, (e1 - base + kWavesPerBlock - 1) / kWavesPerBlock);
         for (int k = 0; k < cntc; k += 2) {
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_part(UpArgs a, const PartDes
     for (int32_t base = lo; base < hi; base += kWave) {
         const int32_t my = base + lane;
         const int32_t enc = my < hi ? a.child_enc[my] : 0;
-        const int4 vl = my < hi && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & ~kVirtualBit]
+        const int4 vl = my < hi && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask]
                                                                    : make_int4(-1, -1, -1, -1);
         const int cntc = min(kWave, hi - base);
         for (int k = 0; k < cntc; k += 2) {

@@ -57,12 +57,15 @@ def _random_columns(rng, leaves, sites, absent_frac=0.1, gap=0.2):
     return codes, present
 
 
-VARIANTS = ["virtual", "plain"]
+VARIANTS = ["virtual", "leafparent", "plain"]
 
 
 def _variant(engine, variant):
-    """virtual / plain: per-level kernels with or without virtual leaf-parents."""
-    engine.set_virtual(variant == "virtual")
+    """virtual (default): leaf-parents and, with every leaf present, three- and four-leaf
+    subtrees evaluated inline by their parent; leafparent: leaf-parents only; plain: every
+    internal node materialised."""
+    engine.set_virtual(variant != "plain")
+    engine.set_subtree(variant == "virtual")
 
 
 def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant="virtual"):
@@ -97,6 +100,26 @@ def test_random_binary_vs_oracle(engine, oracle, sites, variant):
     codes, present = _random_columns(rng, 257, sites)
     cons = rng.integers(0, 16, size=sites).astype(np.uint8)
     _compare(engine, oracle, off, idx, root, codes, present, cons, None, variant)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("seed", range(4))
+def test_all_present_random_codes_vs_oracle(engine, oracle, seed, variant):
+    """Every leaf present (the subtree form's condition) with unrelated random codes, so
+    cherries and three- / four-leaf subtrees disagree everywhere; binary, unary and
+    polytomy trees; forced root on odd seeds."""
+    rng = np.random.default_rng(900 + seed)
+    if seed == 0:
+        off, idx, root = panman_amd.random_join_tree(1500, seed=seed + 3)
+    else:
+        off, idx, root = random_tree(700, rng, max_children=[2, 3, 5][seed - 1], unary=[0.0, 0.1, 0.0][seed - 1])
+    leaves = int((np.diff(off) == 0).sum())
+    sites = [700, 2049, 333, 65][seed]
+    codes, present = _random_columns(rng, leaves, sites, absent_frac=0.0, gap=0.1)
+    assert present.all()
+    cons = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=sites)
+    forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
+    _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)

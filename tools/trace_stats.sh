@@ -14,6 +14,7 @@ python3 - "$out/kernel_stats.csv" <<'P'
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
-    m = re.search(r"\b(k_\w+)", r["Name"]); n = m.group(0) if m else r["Name"][:40]
-    print(f'{n:24s} calls {int(r["Calls"]):6d} total {float(r["TotalDurationNs"])/1e6:9.2f} ms  avg {float(r["AverageNs"])/1e3:9.1f} us')
+    m = re.search(r"\b(k_\w+(<[^(]*>)?)", r["Name"]); n = m.group(0) if m else r["Name"][:40]
+    n = n.replace("(pm::Mode)", "M")
+    print(f'{n:40s} calls {int(r["Calls"]):6d} total {float(r["TotalDurationNs"])/1e6:9.2f} ms  avg {float(r["AverageNs"])/1e3:9.1f} us')
 P
