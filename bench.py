@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--graph", action="store_true", help="(default) hipGraph replay")
     p.add_argument("--no-subtree", action="store_true",
                    help="Fitch: leaf-parent form only (PM_OPT_SUBTREE off; A/B of the subtree form)")
+    p.add_argument("--narrow", type=int, default=-1,
+                   help="Fitch: PM_OPT_NARROW, most nodes per level walked in a band launch (-1: library "
+                        "default 16; 0: one launch per level)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -108,6 +111,9 @@ def main():
     eng.synth_columns(lo, s_local, seed=2)
     if args.no_subtree:
         eng.set_subtree(False)
+    if args.narrow >= 0:
+        eng.set_narrow(args.narrow)
+
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")
     gather = "none (1 GPU)"

@@ -92,11 +92,16 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_SUBTREE (default 1): Fitch with every leaf present also evaluates, inside its
  *                  binary parent, any node whose children are leaves or two-leaf cherries
  *                  (three- and four-leaf subtrees), so those are not materialised either.
+ *   PM_OPT_NARROW  (default 16): Fitch -- a run of consecutive levels with at most this many
+ *                  nodes each (a node of out-degree > 3 counts 4) is walked by one launch,
+ *                  one 1024-thread workgroup per 2048-site tile with a barrier between levels,
+ *                  instead of one launch per level (deep, ladder-like trees); 0 = off.
  * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
  * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
 #define PM_OPT_SUBTREE 6
+#define PM_OPT_NARROW 7
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

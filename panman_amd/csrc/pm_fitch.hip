@@ -37,13 +37,7 @@ namespace {
 // SUB: subtree form -- the first two children may also be S2 / S3 subtrees (three or four
 // leaves each, evaluated in registers: subtree_set_ap).
 template <bool AP, bool LEAFY, bool SUB = false>
-__global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    wave_item(wave, a.tiles, item, tile);
-    if (item >= a.count) return;
-    const NodeDesc& d = a.desc[item];
+__device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
 
@@ -109,6 +103,16 @@ __global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_
         }
     }
 #endif
+}
+
+template <bool AP, bool LEAFY, bool SUB = false>
+__global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
+    if (item >= a.count) return;
+    fitch_up_node<AP, LEAFY, SUB>(a, a.desc[item], tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
@@ -179,26 +183,20 @@ __device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* b
     }
 }
 
-template <bool AP>
-__global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
-    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    block_item(a.tiles, item, tile);
-    const NodeDesc& d = a.desc[item];
-    const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
-    const int64_t word = (int64_t)tile * kWave + lane;
-
-    uint32_t both[16], either[16], vd = 0;
+// One wave's share of a wide node's children: children e0 + wave, e0 + wave + NW, ... folded
+// into (both, either, vd).
+template <bool AP, int NW>
+__device__ __forceinline__ void wide_fold(const UpArgs& a, int32_t e0, int32_t e1, int wave, int tile, int lane,
+                                          int64_t word, uint32_t* both, uint32_t* either, uint32_t& vd) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    for (int32_t base = e0 + wave; base < e1; base += kWavesPerBlock * kWave) {
-        const int32_t my = base + kWavesPerBlock * lane;
+    vd = 0;
+    for (int32_t base = e0 + wave; base < e1; base += NW * kWave) {
+        const int32_t my = base + NW * lane;
         const int32_t enc = my < e1 ? a.child_enc[my] : 0;
         const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask]
                                                                    : make_int4(-1, -1, -1, -1);
-        const int cnt = min(kWave, (e1 - base + kWavesPerBlock - 1) / kWavesPerBlock);
+        const int cnt = min(kWave, (e1 - base + NW - 1) / NW);
         for (int k = 0; k < cnt; k += 2) {
             const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
             const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
@@ -222,6 +220,36 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
             }
         }
     }
+}
+
+// AND if non-empty else OR, forced root, store and mask pushes of a wide node (one wave).
+template <bool AP>
+__device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
+                                            uint32_t* both, const uint32_t* either, uint32_t vd) {
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
+    if (d.node == a.root_dense && a.forced != nullptr) {
+        const uint4 F = a.forced[word];
+        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
+    }
+    uint64_t mx, ms;
+    store_fitch_set(a.sets, a.cmask, a.cons[word], d.node, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
+    push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms);
+}
+
+template <bool AP>
+__global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
+    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    block_item(a.tiles, item, tile);
+    const NodeDesc& d = a.desc[item];
+    const int64_t word = (int64_t)tile * kWave + lane;
+
+    uint32_t both[16], either[16], vd;
+    wide_fold<AP, kWavesPerBlock>(a, d.e0, d.e1, wave, tile, lane, word, both, either, vd);
     if (wave > 0) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
@@ -241,16 +269,52 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
         }
         vd |= part[w][32][lane];
     }
-    const uint32_t nz = any_plane(both);
+    wide_finish<AP>(a, d, tile, lane, word, both, either, vd);
+}
+
+// Narrow levels (PM_OPT_NARROW): a run of consecutive post-order levels with few nodes each
+// is walked by ONE launch -- one 1024-thread workgroup per tile, each level's nodes dealt to
+// its 16 waves (a wide node's children to all of them, accumulators met by LDS AND / OR
+// atomics), a workgroup barrier between levels -- instead of one launch per level, each a
+// dependent chain of HBM round trips behind a kernel boundary (deep, ladder-like trees).  A
+// tile's records and masks are only touched by the waves of its own workgroup, so the
+// barrier's workgroup-scope release / acquire is all the synchronisation the hand-off needs;
+// what earlier launches wrote is visible at kernel start.
+template <bool AP, bool SUB>
+__global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const int32_t* class_off, int32_t h0, int32_t h1) {
+    __shared__ uint32_t acc[33][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int tile = blockIdx.x;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    for (int32_t h = h0; h < h1; ++h) {
+        const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
+                      e = class_off[(h + 1) * kDegreeClasses];
+        for (int32_t i = b + wave; i < m; i += kBandWaves) fitch_up_node<AP, false, SUB>(a, a.desc[i], tile, lane);
+        for (int32_t i = m; i < e; ++i) {   // out-degree > 3
+            if (wave == 0) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
-    if (n == a.root_dense && a.forced != nullptr) {
-        const uint4 F = a.forced[word];
-        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
+                for (int v = 0; v < 16; ++v) { acc[v][lane] = ~0u; acc[16 + v][lane] = 0u; }
+                acc[32][lane] = 0u;
+            }
+            __syncthreads();
+            const NodeDesc& d = a.desc[i];
+            uint32_t both[16], either[16], vd;
+            wide_fold<AP, kBandWaves>(a, d.e0, d.e1, wave, tile, lane, word, both, either, vd);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                atomicAnd(&acc[v][lane], both[v]);
+                atomicOr(&acc[16 + v][lane], either[v]);
+            }
+            atomicOr(&acc[32][lane], vd);
+            __syncthreads();
+            if (wave == 0) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) { both[v] = acc[v][lane]; either[v] = acc[16 + v][lane]; }
+                wide_finish<AP>(a, d, tile, lane, word, both, either, acc[32][lane]);
+            }
+        }
+        __syncthreads();
     }
-    uint64_t mx, ms;
-    store_fitch_set(a.sets, a.cmask, a.cons[word], n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
-    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
 }
 
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
@@ -313,6 +377,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const std::vector<int32_t>& up_off = sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
 
+    const bool ap = c->leaves_all_present;
     UpArgs up{};
     up.child_off = dt.child_off;
     up.child_enc = child_enc;
@@ -330,8 +395,30 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.tiles = tiles;
     up.wpad = wpad;
     const std::vector<int32_t>& class_off = sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
+    const int form = sub ? 2 : virt ? 1 : 0;
     const int H = (int)up_off.size() - 1;
+    // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
+    auto narrow_up = [&](int h) {
+        const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
+                      e = class_off[(h + 1) * kDegreeClasses];
+        return (m - b) + 4 * (e - m) <= c->narrow_max;
+    };
     for (int h = 0; h < H; ++h) {
+        if (c->narrow_max > 0 && narrow_up(h)) {
+            int h1 = h + 1;
+            while (h1 < H && narrow_up(h1)) ++h1;
+            if (h1 - h >= 2) {
+                up.desc = up_desc;
+                const int32_t* tab = dt.lvl + ht.lvl_up[form];
+                timer_begin(c, 0);
+                if (sub) hipLaunchKernelGGL((k_fitch_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else if (ap) hipLaunchKernelGGL((k_fitch_up_band<true, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else hipLaunchKernelGGL((k_fitch_up_band<false, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                timer_end(c, 0);
+                h = h1 - 1;
+                continue;
+            }
+        }
         // out-degree <= 3: one wave per (node, tile); wider: one workgroup per (node, tile)
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
                       e = class_off[(h + 1) * kDegreeClasses];
@@ -343,8 +430,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             timer_begin(c, 0);
             if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (c->leaves_all_present && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (c->leaves_all_present) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (ap && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (ap) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL((k_fitch_up<false, false>), grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
@@ -353,7 +440,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             up.count = e - m;
             const dim3 grid = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (c->leaves_all_present) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, c->stream, up);
+            if (ap) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL(k_fitch_up_wide<false>, grid, dim3(kBlock), 0, c->stream, up);
             timer_end(c, 0);
         }
@@ -391,12 +478,30 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
+        if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {
+            int d1 = d + 1;
+            while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
+            if (d1 - d >= 2) {
+                dn.desc = down_desc;
+                const int32_t* tab = dt.lvl + ht.lvl_down[form];
+                const int32_t* base = sub ? (ht.down_dense_k ? dt.lvl + ht.lvl_base_k : nullptr)
+                                          : (virt && ht.down_dense_v) ? tab : nullptr;
+                timer_begin(c, 1);
+                // (subtree form: the lean body as in the level kernels, S2 / S3 records in k_tail)
+                if (block && ap) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (block) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (ap) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else hipLaunchKernelGGL((k_down_band<Mode::kFitch, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                timer_end(c, 1);
+                d = d1 - 1;
+                continue;
+            }
+        }
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
         const dim3 grid = wave_grid(dn.count, tiles);
         timer_begin(c, 1);
-        const bool ap = c->leaves_all_present;
         // level d = one range of dense indices: [down_off[d], down_off[d+1]) in the leaf-parent
         // form, from down_dense_base_k[d] in the subtree form
         const bool dense = sub ? ht.down_dense_k : virt && ht.down_dense_v;
@@ -412,9 +517,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     }
     dn.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
     dn.count = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
+#ifdef PM_EXP_NOTAIL   // timing experiment: no tail launch
+    dn.count = 0;
+#endif
     if (dn.count > 0) {
         const dim3 grid = wave_grid(dn.count, tiles);
-        const bool ap = c->leaves_all_present;
         timer_begin(c, 1);
         if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
@@ -445,5 +552,11 @@ hipError_t launch_score(pm_ctx* c) {
 #ifdef PM_EXP_COUNT_COMPLEX
 extern "C" int pm_exp_counters(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_words), 32) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef PM_EXP_TAILSTAT
+extern "C" int pm_exp_tail(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_tail), 64) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -77,6 +77,7 @@ void free_tree(DevTree& t) {
     dev_free(t.down_desc_k);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
+    dev_free(t.lvl);
     t = DevTree{};
 }
 
@@ -198,6 +199,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
+                              (uint64_t)c->narrow_max,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -379,6 +381,11 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     }
     if (option == PM_OPT_VIRTUAL) {
         c->virtual_leaf_parents = value != 0;
+        return PM_OK;
+    }
+    if (option == PM_OPT_NARROW) {
+        if (value < 0 || value > 1024) return fail(c, PM_ERR_ARG, "PM_OPT_NARROW: 0..1024 items per level");
+        c->narrow_max = (int32_t)value;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
@@ -817,6 +824,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     for (size_t k = 0; k < up_desc_p.size(); ++k) up_desc_p[k].pad0 = ht.part_off[k];
     for (size_t k = 0; k < up_desc_vp.size(); ++k) up_desc_vp[k].pad0 = ht.part_off_v[k];
     upload_phase("parts");
+    std::vector<int32_t> lvl;
+    {
+        const std::vector<int32_t>* up[3] = {&ht.up_class_off, &ht.up_class_off_v, &ht.up_class_off_k};
+        const std::vector<int32_t>* dn[3] = {&ht.down_level_off, &ht.down_level_off_v, &ht.down_level_off_k};
+        for (int f = 0; f < 3; ++f) {
+            ht.lvl_up[f] = (int64_t)lvl.size();
+            lvl.insert(lvl.end(), up[f]->begin(), up[f]->end());
+            ht.lvl_down[f] = (int64_t)lvl.size();
+            lvl.insert(lvl.end(), dn[f]->begin(), dn[f]->end());
+        }
+        ht.lvl_base_k = (int64_t)lvl.size();
+        lvl.insert(lvl.end(), ht.down_dense_base_k.begin(), ht.down_dense_base_k.end());
+    }
 
     free_work(c);
     free_columns(c);
@@ -851,7 +871,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.up_desc_k, up_desc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||
-        (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess) {
+        (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.lvl, lvl, c->stream)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }

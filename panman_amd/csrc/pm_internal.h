@@ -101,6 +101,9 @@ struct DevTree {
     NodeDesc* down_desc_k = nullptr;
     int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
+    // level tables on the device (the narrow-band launches walk several levels): the host
+    // arrays up_class_off{,_v,_k}, down_level_off{,_v,_k}, down_dense_base_k back to back
+    int32_t* lvl = nullptr;
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
@@ -140,6 +143,8 @@ struct HostTree {
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
+    // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form
+    int64_t lvl_up[3] = {0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
 };
 
 struct Timer {
@@ -162,6 +167,7 @@ struct pm_ctx {
     int32_t max_degree = 0;
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
     bool subtree_form = true;         // Fitch, all leaves present: S2 / S3 inline too (PM_OPT_SUBTREE)
+    int32_t narrow_max = 16;          // Fitch: runs of levels this narrow go to one band launch (PM_OPT_NARROW)
 
     // column shard
     int64_t num_sites = 0;

@@ -57,6 +57,10 @@ inline dim3 block_grid(int32_t count, int32_t tiles) {
 #endif
 }
 
+// Narrow-level band launches (PM_OPT_NARROW): one workgroup of 16 waves per tile.
+constexpr int kBandWaves = 16;
+constexpr int kBandBlock = kBandWaves * kWave;
+
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
     const NodeDesc* desc;  // level items
@@ -899,8 +903,8 @@ __device__ __forceinline__ uint32_t subtree_count(const Kid& k, int sh, uint32_t
 
 // One record stream per iteration (v, x, a, b, c[, y, d]): a single put_records body serves
 // them all, selected by the wave-uniform stream index.
-template <class Sink>
-__device__ __forceinline__ void subtree_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, int sh,
+template <class Args, class Sink>
+__device__ __forceinline__ void subtree_put(const Args& a, const Sink& sink, uint32_t& p, const Kid& k, int sh,
                                             uint32_t valid, const uint32_t* Fn, int64_t word) {
     const uint4 P = make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]);
     const SubFinals f = subtree_finals(k, sh, P);
@@ -966,8 +970,8 @@ __device__ __forceinline__ uint32_t kid_count(const KidOut& o) {
     return n;
 }
 
-template <Mode M, bool SUB = false, class Sink>
-__device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
+template <Mode M, bool SUB = false, class Args, class Sink>
+__device__ __forceinline__ void kid_put(const Args& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
                                         int64_t word, const uint32_t* Fn) {
     if (k.enc < 0) {
         put_records(sink, p, (uint32_t)a.leaf_id[-k.enc - 1], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
@@ -1147,18 +1151,11 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
 #ifndef PM_SUB_DOWN_WAVES
 #define PM_SUB_DOWN_WAVES 4
 #endif
-template <Mode M, bool AP, bool DENSE, bool SUB = false>
-__global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
-    __shared__ pm_mut stage[kWavesPerBlock][kStage];
-    __shared__ uint32_t stage_cnt[kWavesPerBlock];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    wave_item(wave, a.tiles, item, tile);
-    if (item >= a.count) return;   // whole wave leaves together
-    if (lane == 0) stage_cnt[wave] = 0;
-    const NodeDesc& d = a.desc[item];
-    const int32_t n = DENSE ? a.dense_base + item : d.node;
+// One pre-order wave: node `n` (its descriptor d) x tile; `salt` spreads the waves over the
+// record shards; `stage` is the wave's LDS record stage (kStage records).
+template <Mode M, bool AP, bool SUB>
+__device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, int32_t n, uint32_t salt, int tile,
+                                          int lane, pm_mut* stage) {
     const int32_t parent = d.parent, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
@@ -1173,7 +1170,11 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
         const uint4 q = is_root ? a.cons[word] : parent_final<REC>(a, parent, m, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
+#ifdef PM_EXP_NODIRTY   // timing experiment: no leaf-ish child loads in the pre-order pass
+    const bool dirty = false;
+#else
     const bool dirty = is_root || ((m.d >> lane) & 1ull);
+#endif
     Kid kids[2];
     kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
     if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
@@ -1207,11 +1208,6 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
         return;
     }
 #endif
-#ifdef PM_EXP_NOFLUSH     // timing experiment: records staged in LDS, not written out
-    node_records<M, AP>(a, LdsSink{stage[wave], &stage_cnt[wave]}, n, e0, e1, kids, word, valid, pc, F, self_diff);
-    if (__builtin_amdgcn_readfirstlane(stage_cnt[wave]) == 0xFFFFFFFFu) a.shard_cnt[0] = 0;
-    return;
-#endif
     // Records: every lane's count first, positions by a wave prefix sum (no LDS counter),
     // and the shard reservation's global atomic issued before the records are built, so
     // its round trip overlaps the staging.
@@ -1230,12 +1226,12 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
     const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
     if (total == 0) return;
     const uint32_t p0 = incl - cnt;
-    const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
+    const uint32_t shard = (salt * 31u + tile * 7919u) % kShards;
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
     const uint32_t node_id = (uint32_t)a.internal_id[n];
     uint32_t rp = p0;
-    const LdsSink ls{stage[wave], nullptr};
+    const LdsSink ls{stage, nullptr};
     put_records(ls, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
     kid_put<M, SUB>(a, ls, rp, kids[0], o0, word, F);
     if (two) kid_put<M, SUB>(a, ls, rp, kids[1], o1, word, F);
@@ -1243,7 +1239,7 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
     pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
     if (total <= kStage) {
         for (uint32_t i = lane; i < total; i += kWave)
-            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
+            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[i];
         return;
     }
     // overflowed the stage: the same records at the same positions, straight into global
@@ -1254,11 +1250,47 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
     if (two) kid_put<M, SUB>(a, gs, rp, kids[1], o1, word, F);
 }
 
+template <Mode M, bool AP, bool DENSE, bool SUB = false>
+__global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
+    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
+    if (item >= a.count) return;   // whole wave leaves together
+    const NodeDesc& d = a.desc[item];
+    down_node<M, AP, SUB>(a, d, DENSE ? a.dense_base + item : d.node, (uint32_t)item, tile, lane, stage[wave]);
+}
+
+// Narrow pre-order levels (PM_OPT_NARROW; see k_fitch_up_band): levels [d0, d1) of the
+// level table `level_off` (descriptor ranges) walked by one launch, one 1024-thread workgroup
+// per tile, a workgroup barrier between levels.  `dense_base` (nullable): each level's first
+// dense index when the level is one dense range.
+template <Mode M, bool AP, bool SUB = false>
+__global__ __launch_bounds__(kBandBlock) void k_down_band(DownArgs a, const int32_t* level_off, const int32_t* dense_base,
+                                                          int32_t d0, int32_t d1) {
+    __shared__ pm_mut stage[kBandWaves][kStage];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int tile = blockIdx.x;
+    for (int32_t l = d0; l < d1; ++l) {
+        const int32_t b = level_off[l], e = level_off[l + 1];
+        const int32_t base = dense_base ? dense_base[l] : -1;
+        for (int32_t i = b + wave; i < e; i += kBandWaves) {
+            const NodeDesc& d = a.desc[i];
+            down_node<M, AP, SUB>(a, d, base >= 0 ? base + (i - b) : d.node, (uint32_t)i, tile, lane, stage[wave]);
+        }
+        __syncthreads();
+    }
+}
+
 // Records of the leaf / virtual children beyond a node's second (polytomies), after the
 // pre-order levels: wave = (tail item, tile), parent final read back (node_final).
 // SUB: subtree form -- the S2 / S3 children are tail items too (their inner finals and
 // records from the parent's final and their leaves, subtree_put), so the level kernels stay
 // lean.
+#ifdef PM_EXP_TAILSTAT   // experiment: k_tail lane classes (lanes, dirty, own non-uniform, with records)
+static __device__ unsigned long long g_exp_tail[8];
+#endif
 template <Mode M, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
@@ -1274,12 +1306,28 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     const uint32_t valid = valid_mask(a, word);
     const bool proot = t.parent == a.root_dense;
     const RecMask pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
+    if (!proot && pm.d == 0) return;   // no dirty lane: the child holds the parent's code everywhere
     Kid k;
     kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
     const uint4 q = node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, t.parent, tile, lane, word);
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
     kid_records<M, AP, SUB>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
     const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
+#ifdef PM_EXP_TAILSTAT
+    {
+        const bool dirty = proot || ((pm.d >> lane) & 1ull);
+        const int sh = kid_shape(t.enc);
+        const uint32_t nu = code_ne(k.L0, k.L1) | (sh ? code_ne(k.L0, k.L2) : 0u) | (sh == 2 ? code_ne(k.L0, k.L3) : 0u);
+        const uint32_t pne = code_ne(k.L0, make_uint4(F[0], F[1], F[2], F[3]));
+        const unsigned long long bd = __ballot(dirty), bn = __ballot(dirty && nu), bp = __ballot(dirty && !nu && pne);
+        if (lane == 0) {
+            atomicAdd(&g_exp_tail[sh], 64ull);
+            atomicAdd(&g_exp_tail[3 + sh], (unsigned long long)__popcll(bd));
+            atomicAdd(&g_exp_tail[6], (unsigned long long)__popcll(bn));
+            atomicAdd(&g_exp_tail[7], (unsigned long long)__popcll(bp));
+        }
+    }
+#endif
     if (total == 0) return;
     const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
     uint32_t base;
