@@ -275,6 +275,12 @@ typedef struct pm_panman pm_panman;
  * :1661-1751, mutations assigned in pre-order :576-618).  Host only, no device needed.
  * On failure `err` (nullable, err_len bytes) receives the reason. */
 int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len);
+/* The older Google Protobuf PanMAN (`panmanOld.treeGroup`, panman.proto; xz-compressed or
+ * raw), as TreeGroup(istream, isOld = true) reads it (src/panman.cpp:6865-6876 with
+ * Tree::protoMATToTree(panmanOld::tree), :1803-1866) -- into the same handle as
+ * pm_panman_load, so pm_panman_write converts it (the reference's --protobuf2capnp,
+ * src/panmanUtils.cpp:939-952). */
+int pm_panman_load_old(const char* path, pm_panman** out, char* err, int64_t err_len);
 int pm_panman_tree_count(const pm_panman* file);
 /* View of tree `index` as a pm_panmat (pointers into `file`, valid until pm_panman_free);
  * node ids are pre-order positions of the stored Newick, names follow the reference's

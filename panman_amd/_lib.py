@@ -79,6 +79,7 @@ _SIGS = {
     "pm_replay_run": (C.c_int, [C.c_void_p]),
     "pm_replay_format": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "pm_panman_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int64]),
+    "pm_panman_load_old": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int64]),
     "pm_panman_tree_count": (C.c_int, [C.c_void_p]),
     "pm_panman_tree": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "pm_panman_newick": (C.c_char_p, [C.c_void_p, C.c_int]),

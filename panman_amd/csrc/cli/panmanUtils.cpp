@@ -49,6 +49,7 @@ const Spec kSpecs[] = {
     {"fasta-aligned", 'm', false, "Print MSA of sequences for each PanMAT in a PanMAN (FASTA format)"},
     {"reroot", 'r', false, "Reroot a PanMAT in a PanMAN based on the input sequence id (--reference)"},
     {"treeID", 'd', true, "Tree ID, required for --reroot"},
+    {"protobuf2capnp", 0, false, "Converts a Google Protobuf PanMAN (-I) to a Cap'n Proto PanMAN (-o)"},
     {"low-mem-mode", 0, false, "Build with the Sankoff driver (the reference's batched low-memory mode)"},
     {"reference", 'n', true, "Identifier of reference sequence for PanMAN construction (optional) or reroot (required)"},
     {"output-file", 'o', true, "Prefix of the output file name"},
@@ -302,9 +303,46 @@ int build_from_pangraph(const Options& o, int device) {
     return 0;
 }
 
+// --protobuf2capnp -I old.panman -o out (src/panmanUtils.cpp:939-952, 1267-1268): the older
+// Protobuf PanMAN read and written back as ./panman/<out>.panman (writePanMAN, :271-299).
+int protobuf2capnp(const Options& o) {
+    if (!o.has("output-file")) {
+        print_error("Output file not provided!");
+        usage(std::cout);
+        return 1;
+    }
+    const std::string path = o.get("input-panman");
+    std::cout << "starting reading panman" << std::endl;
+    pm_panman* file = nullptr;
+    char err[512] = {0};
+    if (pm_panman_load_old(path.c_str(), &file, err, sizeof err) != PM_OK) {
+        print_error(err[0] ? err : ("cannot load " + path));
+        return 1;
+    }
+    std::vector<pm_panmat> views(pm_panman_tree_count(file));
+    std::vector<const pm_panmat*> list;
+    for (int i = 0; i < (int)views.size(); ++i) {
+        pm_panman_tree(file, i, &views[i]);
+        list.push_back(&views[i]);
+    }
+    std::cout << "Writing PanMAN" << std::endl;
+    ::mkdir("./panman", 0777);
+    const std::string out = "./panman/" + o.get("output-file") + ".panman";
+    const auto w0 = Clock::now();
+    const int rc = pm_panman_write(out.c_str(), list.data(), (int)list.size(), 1);
+    std::cout << "\nNetwork Write execution time: " << ns_since(w0) << " nanoseconds\n";
+    pm_panman_free(file);
+    if (rc != PM_OK) {
+        print_error("cannot write " + out);
+        return 1;
+    }
+    return 0;
+}
+
 int from_panman(const Options& o, const std::vector<int>& devices) {
     const int device = devices[0];
     const std::string path = o.get("input-panman");
+    if (o.has("protobuf2capnp")) return protobuf2capnp(o);
     std::cout << "starting reading panman" << std::endl;
     const auto t0 = Clock::now();
     pm_panman* file = nullptr;

@@ -555,8 +555,3 @@ extern "C" int pm_exp_counters(unsigned long long* out) {
 }
 #endif
 
-#ifdef PM_EXP_TAILSTAT
-extern "C" int pm_exp_tail(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_tail), 64) == hipSuccess ? 0 : -1;
-}
-#endif

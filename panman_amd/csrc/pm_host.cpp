@@ -784,7 +784,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 TailDesc t{};
                 t.parent = d;
                 t.enc = x;
+                t.ix = t.iy = -1;
                 for (int j = 0; j < 4; ++j) t.vl[j] = x >= 0 ? vleaf[(size_t)(x & kDenseMask) * 4 + j] : -1;
+                t.id[0] = x < 0 ? ht.leaf_id[-x - 1] : ht.internal_id[x & kDenseMask];
+                for (int j = 0; j < 4; ++j) t.id[1 + j] = t.vl[j] >= 0 ? ht.leaf_id[t.vl[j]] : -1;
                 tail.push_back(t);
             }
         return tail;
@@ -801,6 +804,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         t.parent = parent_dense[d];
         t.enc = (d | kVirtualBit) | (sshape[d] << kShapeShift);
         for (int j = 0; j < 4; ++j) t.vl[j] = vleaf[(size_t)d * 4 + j];
+        t.ix = ht.internal_id[vinner[(size_t)d * 2]];
+        t.iy = vinner[(size_t)d * 2 + 1] >= 0 ? ht.internal_id[vinner[(size_t)d * 2 + 1]] : -1;
+        t.id[0] = ht.internal_id[d];
+        for (int j = 0; j < 4; ++j) t.id[1 + j] = t.vl[j] >= 0 ? ht.leaf_id[t.vl[j]] : -1;
         tail_desc_k.push_back(t);
     }
     ht.num_tail_k = (int32_t)tail_desc_k.size();

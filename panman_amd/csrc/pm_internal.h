@@ -49,9 +49,13 @@ struct alignas(64) NodeDesc {
 // A leaf or virtual child beyond a node's first two (polytomies): its records need only
 // the parent's final, so they are emitted by one flat launch after the pre-order levels
 // instead of serially inside the parent's wave.
-struct alignas(32) TailDesc {
-    int32_t parent, enc, pad0, pad1;
-    int32_t vl[4];
+// Everything the tail wave needs is in the descriptor (one 64-B scalar load): no dependent
+// id lookups (leaf_id[vl], internal_id[vinner]) between the descriptor and the records.
+struct alignas(64) TailDesc {
+    int32_t parent, enc, ix, iy;   // ix / iy: an S2 / S3 child's cherries (caller node ids), else -1
+    int32_t vl[4];                 // a virtual child's leaves (ranks), -1 padded
+    int32_t id[5];                 // caller node ids: the child itself, then its leaves vl[0..3]
+    int32_t pad[3];
 };
 
 // Sankoff nodes of out-degree > 255: their children are cut into parts of kPartChildren,

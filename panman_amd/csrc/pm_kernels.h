@@ -808,13 +808,10 @@ __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 v
         }
         if constexpr (SUB) {
             const int sh = kid_shape(enc);
-            if (sh) {   // S2 / S3: the other leaves and the cherries' ids (scalar loads)
+            if (sh) {   // S2 / S3: the other leaves (the cherries' ids come with the tail descriptor)
                 k.L2 = k.L3 = make_uint4(0, 0, 0, 0);
                 if (dirty) k.L2 = a.leaf_planes[(size_t)k.vl.z * a.wpad + word];
                 if (sh == 2 && dirty) k.L3 = a.leaf_planes[(size_t)k.vl.w * a.wpad + word];
-                const int32_t v = enc & kDenseMask;
-                k.ix = a.internal_id[a.vinner[2 * v]];
-                if (sh == 2) k.iy = a.internal_id[a.vinner[2 * v + 1]];
             }
         }
     } else {
@@ -903,8 +900,8 @@ __device__ __forceinline__ uint32_t subtree_count(const Kid& k, int sh, uint32_t
 
 // One record stream per iteration (v, x, a, b, c[, y, d]): a single put_records body serves
 // them all, selected by the wave-uniform stream index.
-template <class Args, class Sink>
-__device__ __forceinline__ void subtree_put(const Args& a, const Sink& sink, uint32_t& p, const Kid& k, int sh,
+template <class Sink>
+__device__ __forceinline__ void subtree_put(const TailDesc& t, const Sink& sink, uint32_t& p, const Kid& k, int sh,
                                             uint32_t valid, const uint32_t* Fn, int64_t word) {
     const uint4 P = make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]);
     const SubFinals f = subtree_finals(k, sh, P);
@@ -913,14 +910,14 @@ __device__ __forceinline__ void subtree_put(const Args& a, const Sink& sink, uin
 #pragma unroll 1
     for (int st = 0; st < streams; ++st) {
         uint4 pc = P, cc = f.F;
-        int32_t node = a.internal_id[k.enc & kDenseMask];
+        int32_t node = t.id[0];
         switch (st) {
-            case 1: node = k.ix; pc = f.F; cc = f.G; break;
-            case 2: node = a.leaf_id[k.vl.x]; pc = f.G; cc = k.L0; break;
-            case 3: node = a.leaf_id[k.vl.y]; pc = f.G; cc = k.L1; break;
-            case 4: node = a.leaf_id[k.vl.z]; pc = sh == 1 ? f.F : f.H; cc = k.L2; break;
-            case 5: node = k.iy; pc = f.F; cc = f.H; break;
-            case 6: node = a.leaf_id[k.vl.w]; pc = f.H; cc = k.L3; break;
+            case 1: node = t.ix; pc = f.F; cc = f.G; break;
+            case 2: node = t.id[1]; pc = f.G; cc = k.L0; break;
+            case 3: node = t.id[2]; pc = f.G; cc = k.L1; break;
+            case 4: node = t.id[3]; pc = sh == 1 ? f.F : f.H; cc = k.L2; break;
+            case 5: node = t.iy; pc = f.F; cc = f.H; break;
+            case 6: node = t.id[4]; pc = f.H; cc = k.L3; break;
             default: break;
         }
         const uint32_t pcs[4] = {pc.x, pc.y, pc.z, pc.w};
@@ -970,35 +967,17 @@ __device__ __forceinline__ uint32_t kid_count(const KidOut& o) {
     return n;
 }
 
-template <Mode M, bool SUB = false, class Args, class Sink>
-__device__ __forceinline__ void kid_put(const Args& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
+template <Mode M, class Sink>
+__device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
                                         int64_t word, const uint32_t* Fn) {
     if (k.enc < 0) {
         put_records(sink, p, (uint32_t)a.leaf_id[-k.enc - 1], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
         return;
     }
     if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
-    if constexpr (SUB) {
-        const int sh = kid_shape(k.enc);
-        if (sh) {   // S2 / S3: v, its cherries and the leaves (recomputed, subtree_put)
-            subtree_put(a, sink, p, k, sh, valid_mask(a, word), Fn, word);
-            return;
-        }
-    }
     put_records(sink, p, (uint32_t)a.internal_id[k.enc & kDenseMask], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
     put_records(sink, p, (uint32_t)a.leaf_id[k.vl.x], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
     if (k.vl.y >= 0) put_records(sink, p, (uint32_t)a.leaf_id[k.vl.y], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
-}
-
-// Records of one child (k_tail items): one sink reservation per lane.
-template <Mode M, bool AP, bool SUB = false, class Sink>
-__device__ __forceinline__ void kid_records(const DownArgs& a, const Sink& sink, const Kid& k, int64_t word,
-                                            uint32_t valid, const uint32_t* F) {
-    KidOut o;
-    kid_prepare<M, SUB>(k, valid, F, o);
-    const uint32_t n = kid_count<SUB>(o);
-    uint32_t p = n ? sink.reserve(n) : 0u;   // every lane stays active (put_records expands cooperatively)
-    kid_put<M, SUB>(a, sink, p, k, o, word, F);
 }
 
 // Every record of node n's wave: the node itself and its first two children (prefetched
@@ -1233,8 +1212,8 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     uint32_t rp = p0;
     const LdsSink ls{stage, nullptr};
     put_records(ls, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M, SUB>(a, ls, rp, kids[0], o0, word, F);
-    if (two) kid_put<M, SUB>(a, ls, rp, kids[1], o1, word, F);
+    kid_put<M>(a, ls, rp, kids[0], o0, word, F);
+    if (two) kid_put<M>(a, ls, rp, kids[1], o1, word, F);
     base = __shfl(base, 0, 64);
     pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
     if (total <= kStage) {
@@ -1246,8 +1225,8 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     const GlobalSink gs{out, (int64_t)base, a.shard_cap, nullptr};
     rp = p0;
     put_records(gs, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M, SUB>(a, gs, rp, kids[0], o0, word, F);
-    if (two) kid_put<M, SUB>(a, gs, rp, kids[1], o1, word, F);
+    kid_put<M>(a, gs, rp, kids[0], o0, word, F);
+    if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
 }
 
 template <Mode M, bool AP, bool DENSE, bool SUB = false>
@@ -1288,53 +1267,76 @@ __global__ __launch_bounds__(kBandBlock) void k_down_band(DownArgs a, const int3
 // SUB: subtree form -- the S2 / S3 children are tail items too (their inner finals and
 // records from the parent's final and their leaves, subtree_put), so the level kernels stay
 // lean.
-#ifdef PM_EXP_TAILSTAT   // experiment: k_tail lane classes (lanes, dirty, own non-uniform, with records)
-static __device__ unsigned long long g_exp_tail[8];
-#endif
+// A tail child's records, node ids from its descriptor.
+template <Mode M, bool SUB, class Sink>
+__device__ __forceinline__ void tail_put(const TailDesc& t, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
+                                         int64_t word, uint32_t valid, const uint32_t* Fn) {
+    if (k.enc < 0) {
+        put_records(sink, p, (uint32_t)t.id[0], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
+        return;
+    }
+    if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
+    if constexpr (SUB) {
+        const int sh = kid_shape(k.enc);
+        if (sh) {   // S2 / S3: v, its cherries and the leaves (subtree_put)
+            subtree_put(t, sink, p, k, sh, valid, Fn, word);
+            return;
+        }
+    }
+    put_records(sink, p, (uint32_t)t.id[0], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
+    put_records(sink, p, (uint32_t)t.id[1], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
+    if (k.vl.y >= 0) put_records(sink, p, (uint32_t)t.id[2], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
+}
+
 template <Mode M, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
-    __shared__ uint32_t stage_cnt[kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    if (lane == 0) stage_cnt[wave] = 0;
     const TailDesc& t = a.tail[item];
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
     const bool proot = t.parent == a.root_dense;
-    const RecMask pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
+    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    const size_t prec = (size_t)t.parent * a.tiles + tile;
+    const RecMask pm = rec_mask(a.cmask, prec);
     if (!proot && pm.d == 0) return;   // no dirty lane: the child holds the parent's code everywhere
+    const bool dirty = proot || ((pm.d >> lane) & 1ull);
     Kid k;
-    kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, proot || ((pm.d >> lane) & 1ull), k);
-    const uint4 q = node_final<M == Mode::kSankoff ? kSankoffRec : kFitchRec>(a, t.parent, tile, lane, word);
+    kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
+    // the parent's final, dirty lanes only (elsewhere the child emits nothing)
+    const uint4* fsrc = proot ? a.root_final + word
+                              : ((pm.x >> lane) & 1ull) ? a.sets + prec * REC + kWave + lanes_below(pm.x)
+                              : ((pm.s >> lane) & 1ull) ? a.sets + prec * REC + lanes_below(pm.s) : a.cons + word;
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (dirty) q = *fsrc;
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
-    kid_records<M, AP, SUB>(a, LdsSink{stage[wave], &stage_cnt[wave]}, k, word, valid, F);
-    const uint32_t total = __builtin_amdgcn_readfirstlane(stage_cnt[wave]);
-#ifdef PM_EXP_TAILSTAT
-    {
-        const bool dirty = proot || ((pm.d >> lane) & 1ull);
-        const int sh = kid_shape(t.enc);
-        const uint32_t nu = code_ne(k.L0, k.L1) | (sh ? code_ne(k.L0, k.L2) : 0u) | (sh == 2 ? code_ne(k.L0, k.L3) : 0u);
-        const uint32_t pne = code_ne(k.L0, make_uint4(F[0], F[1], F[2], F[3]));
-        const unsigned long long bd = __ballot(dirty), bn = __ballot(dirty && nu), bp = __ballot(dirty && !nu && pne);
-        if (lane == 0) {
-            atomicAdd(&g_exp_tail[sh], 64ull);
-            atomicAdd(&g_exp_tail[3 + sh], (unsigned long long)__popcll(bd));
-            atomicAdd(&g_exp_tail[6], (unsigned long long)__popcll(bn));
-            atomicAdd(&g_exp_tail[7], (unsigned long long)__popcll(bp));
-        }
-    }
-#endif
+    // records: counts, positions by a wave prefix sum, the shard reservation issued before
+    // the records are staged (as in down_node)
+    KidOut o;
+    kid_prepare<M, SUB>(k, valid, F, o);
+    const uint32_t cnt = kid_count<SUB>(o);
+    const uint32_t incl = wave_incl_sum(cnt, lane);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
     if (total == 0) return;
+    const uint32_t p0 = incl - cnt;
     const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
-    uint32_t base;
-    pm_mut* out;
-    if (flush_stage(a, stage[wave], total, shard, lane, item, tile, base, out)) return;
-    if (lane == 0) stage_cnt[wave] = 0;
-    kid_records<M, AP, SUB>(a, GlobalSink{out, (int64_t)base, a.shard_cap, &stage_cnt[wave]}, k, word, valid, F);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
+    uint32_t rp = p0;
+    tail_put<M, SUB>(t, LdsSink{stage[wave], nullptr}, rp, k, o, word, valid, F);
+    base = __shfl(base, 0, 64);
+    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
+    if (total <= kStage) {
+        for (uint32_t i = lane; i < total; i += kWave)
+            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
+        return;
+    }
+    rp = p0;
+    tail_put<M, SUB>(t, GlobalSink{out, (int64_t)base, a.shard_cap, nullptr}, rp, k, o, word, valid, F);
 }
 
 }  // namespace pm

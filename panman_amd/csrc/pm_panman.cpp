@@ -15,6 +15,13 @@
 //   Node(0,2) ConsensusSeqToBlockIds(0,4) GapList(2,2: blockId i64@0, blockGapExist bit64)
 //   BlockGapList(0,2) CircularOffset / RotationIndex(1,1: i32@0) SequenceInverted(1,1: bit0)
 //   Tree(0,8) TreeGroup(0,2) ComplexMutation(10,3)
+// Old format (pm_panman_load_old): an xz-compressed Google Protobuf `panmanOld.treeGroup`
+//   (panman.proto), read by TreeGroup(istream, isOld = true) + Tree::protoMATToTree(
+//   panmanOld::tree) + assignMutationsToNodes (src/panman.cpp:6865-6876, :1803-1866,
+//   :1773-1801; NucMut / BlockMut from panmanOld: src/panman.hpp:212-230, :454-465) and
+//   converted by the commented-out CLI command --protobuf2capnp (src/panmanUtils.cpp:939-952).
+//   Decoded by hand from the protobuf wire format (varint / 64-bit / length-delimited /
+//   32-bit records; repeated scalars packed or not), into the same PanmanTree as a .panman.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -402,6 +409,272 @@ bool load_tree(Msg& m, const Struct& t, PanmanTree& out) {
     return true;
 }
 
+// ---- Protobuf (panmanOld, panman.proto) ------------------------------------------------
+struct Pb {
+    const uint8_t* p;
+    const uint8_t* end;
+    std::string* err;
+    bool fail(const char* what) {
+        if (err && err->empty()) *err = std::string("protobuf: ") + what;
+        return false;
+    }
+    bool varint(uint64_t& v) {
+        v = 0;
+        for (int sh = 0; sh < 64; sh += 7) {
+            if (p >= end) return fail("truncated varint");
+            const uint8_t b = *p++;
+            v |= (uint64_t)(b & 0x7F) << sh;
+            if (!(b & 0x80)) return true;
+        }
+        return fail("varint too long");
+    }
+    // next field: number, wire type; length-delimited payloads in [sub, sub_end)
+    bool next(uint32_t& field, uint32_t& wire, uint64_t& value, const uint8_t*& sub, const uint8_t*& sub_end) {
+        uint64_t key;
+        if (!varint(key)) return false;
+        field = (uint32_t)(key >> 3);
+        wire = (uint32_t)(key & 7);
+        if (field == 0) return fail("field number 0");
+        switch (wire) {
+            case 0: return varint(value);
+            case 1:
+                if (end - p < 8) return fail("truncated fixed64");
+                std::memcpy(&value, p, 8);
+                p += 8;
+                return true;
+            case 5: {
+                if (end - p < 4) return fail("truncated fixed32");
+                uint32_t v32;
+                std::memcpy(&v32, p, 4);
+                value = v32;
+                p += 4;
+                return true;
+            }
+            case 2: {
+                uint64_t n;
+                if (!varint(n)) return false;
+                if (n > (uint64_t)(end - p)) return fail("length past the end");
+                sub = p;
+                sub_end = p + n;
+                p += n;
+                return true;
+            }
+            default: return fail("unsupported wire type (groups)");
+        }
+    }
+};
+
+// A repeated varint field, packed (wire 2) or not (wire 0): append its value(s).
+template <class T>
+bool pb_repeated(Pb& r, uint32_t wire, uint64_t value, const uint8_t* sub, const uint8_t* sub_end, std::vector<T>& out) {
+    if (wire == 0) {
+        out.push_back((T)value);
+        return true;
+    }
+    if (wire != 2) return r.fail("repeated scalar with a bad wire type");
+    Pb q{sub, sub_end, r.err};
+    while (q.p < q.end) {
+        uint64_t v;
+        if (!q.varint(v)) return false;
+        out.push_back((T)v);
+    }
+    return true;
+}
+
+// Walk a message's fields, calling f(field, wire, value, sub, sub_end) for each.
+template <class F>
+bool pb_fields(const uint8_t* b, const uint8_t* e, std::string& err, F&& f) {
+    Pb r{b, e, &err};
+    while (r.p < r.end) {
+        uint32_t field, wire;
+        uint64_t value = 0;
+        const uint8_t *sub = nullptr, *sub_end = nullptr;
+        if (!r.next(field, wire, value, sub, sub_end)) return false;
+        if (!f(r, field, wire, value, sub, sub_end)) return false;
+    }
+    return true;
+}
+
+struct PbNucMut {
+    int32_t pos = 0, gap_pos = 0;
+    bool gap_exist = false;
+    uint32_t info = 0;
+};
+struct PbMutation {
+    int64_t block_id = 0;
+    bool gap_exist = false, mut_exist = false, mut_info = false, inversion = false;
+    std::vector<PbNucMut> nucs;
+};
+
+bool pb_mutation(const uint8_t* b, const uint8_t* e, std::string& err, PbMutation& mu) {
+    return pb_fields(b, e, err, [&](Pb& r, uint32_t f, uint32_t w, uint64_t v, const uint8_t* sb, const uint8_t* se) {
+        switch (f) {
+            case 1: mu.block_id = (int64_t)v; return true;
+            case 2: mu.gap_exist = v != 0; return true;
+            case 3: mu.mut_exist = v != 0; return true;
+            case 4: mu.mut_info = v != 0; return true;
+            case 5: mu.inversion = v != 0; return true;
+            case 6: {
+                if (w != 2) return r.fail("nucMutation is not a message");
+                PbNucMut nm;
+                const bool ok = pb_fields(sb, se, err, [&](Pb&, uint32_t g, uint32_t, uint64_t x, const uint8_t*, const uint8_t*) {
+                    if (g == 1) nm.pos = (int32_t)x;           // int32: 64-bit two's complement varint
+                    else if (g == 2) nm.gap_pos = (int32_t)x;
+                    else if (g == 3) nm.gap_exist = x != 0;
+                    else if (g == 4) nm.info = (uint32_t)x;
+                    return true;
+                });
+                if (ok) mu.nucs.push_back(nm);
+                return ok;
+            }
+            default: return true;   // unknown fields are skipped, as protobuf does
+        }
+    });
+}
+
+bool load_tree_pb(const uint8_t* b, const uint8_t* e, PanmanTree& out, std::string& err) {
+    // the tree's fields, gathered first (protobuf field order is free)
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> nodes, cmaps, gaps, named[3];
+    bool have_newick = false;
+    const bool ok = pb_fields(b, e, err, [&](Pb& r, uint32_t f, uint32_t w, uint64_t, const uint8_t* sb, const uint8_t* se) {
+        if (f == 1 || f == 2 || (f >= 4 && f <= 9)) {
+            if (w != 2) return r.fail("tree field is not length-delimited");
+        }
+        switch (f) {
+            case 1: out.newick.assign((const char*)sb, (size_t)(se - sb)); have_newick = true; return true;
+            case 2: nodes.emplace_back(sb, se); return true;
+            case 4: cmaps.emplace_back(sb, se); return true;
+            case 5: gaps.emplace_back(sb, se); return true;
+            case 6: return true;   // blockGaps: never used by the drivers (see load_tree)
+            case 7: named[0].emplace_back(sb, se); return true;
+            case 8: named[1].emplace_back(sb, se); return true;
+            case 9: named[2].emplace_back(sb, se); return true;
+            default: return true;
+        }
+    });
+    if (!ok) return false;
+    if (!have_newick) { err = "protobuf: tree without a newick string"; return false; }
+    Topology topo;
+    if (!parse_topology(out.newick, topo, err)) { err = "newick: " + err; return false; }
+    const int32_t N = (int32_t)topo.name.size();
+    out.num_nodes = N;
+    out.root = topo.root;
+    out.length = topo.length;
+    out.child_off.assign(N + 1, 0);
+    for (int32_t i = 0; i < N; ++i) {
+        out.child_idx.insert(out.child_idx.end(), topo.kids[i].begin(), topo.kids[i].end());
+        out.child_off[i + 1] = (int32_t)out.child_idx.size();
+    }
+    std::unordered_map<std::string, int32_t> index;
+    for (int32_t i = 0; i < N; ++i) {
+        out.names_blob += topo.name[i];
+        out.names_blob.push_back('\0');
+        index[topo.name[i]] = i;
+    }
+    // nodes: i-th stored node = i-th node in pre-order (assignMutationsToNodes)
+    out.bm_off.assign(N + 1, 0);
+    out.nm_off.assign(N + 1, 0);
+    for (int32_t v = 0; v < N; ++v) {
+        if ((size_t)v < nodes.size()) {
+            std::vector<PbMutation> muts;
+            if (!pb_fields(nodes[v].first, nodes[v].second, err,
+                           [&](Pb& r, uint32_t f, uint32_t w, uint64_t, const uint8_t* sb, const uint8_t* se) {
+                               if (f != 1) return true;   // annotations (2) are not on this path
+                               if (w != 2) return r.fail("mutation is not a message");
+                               muts.emplace_back();
+                               return pb_mutation(sb, se, err, muts.back());
+                           }))
+                return false;
+            // NucMuts of every mutation first, then the block mutations (src/panman.cpp:1775-1790)
+            for (const PbMutation& mu : muts) {
+                const int32_t primary = (int32_t)(mu.block_id >> 32);
+                const int32_t secondary = mu.gap_exist ? (int32_t)(mu.block_id & 0xFFFFFFFF) : -1;
+                for (const PbNucMut& nm : mu.nucs) {
+                    const uint32_t info = nm.info & 0xFF, len = info >> 4;
+                    out.nm_primary.push_back(primary);
+                    out.nm_secondary.push_back(secondary);
+                    out.nm_pos.push_back(nm.pos);
+                    out.nm_gap.push_back(nm.gap_exist ? nm.gap_pos : -1);
+                    out.nm_info.push_back((uint8_t)info);
+                    out.nm_nucs.push_back(len <= 6 ? (nm.info >> 8) << (24 - 4 * len) : 0);
+                }
+            }
+            for (const PbMutation& mu : muts)
+                if (mu.mut_exist) {
+                    out.bm_primary.push_back((int32_t)(mu.block_id >> 32));
+                    out.bm_info.push_back(mu.mut_info);
+                    out.bm_inv.push_back(mu.inversion);
+                }
+        }
+        out.bm_off[v + 1] = (int64_t)out.bm_primary.size();
+        out.nm_off[v + 1] = (int64_t)out.nm_primary.size();
+    }
+    // blocks in (primary, secondary) order (std::map, src/panman.cpp:1806-1822, :1829-1832)
+    std::map<std::pair<int32_t, int32_t>, std::vector<uint32_t>> blocks;
+    for (const auto& c : cmaps) {
+        std::vector<int64_t> ids;
+        std::vector<uint32_t> seq;
+        std::vector<uint8_t> gapx;
+        if (!pb_fields(c.first, c.second, err, [&](Pb& r, uint32_t f, uint32_t w, uint64_t v, const uint8_t* sb, const uint8_t* se) {
+                if (f == 1) return pb_repeated(r, w, v, sb, se, ids);
+                if (f == 2) return pb_repeated(r, w, v, sb, se, seq);
+                if (f == 3) return pb_repeated(r, w, v, sb, se, gapx);
+                return true;   // chromosomeName (4)
+            }))
+            return false;
+        for (size_t j = 0; j < ids.size(); ++j) {
+            const bool gx = j < gapx.size() && gapx[j];
+            blocks[{(int32_t)(ids[j] >> 32), gx ? (int32_t)(ids[j] & 0xFFFFFFFF) : -1}] = seq;
+        }
+    }
+    out.block_seq_off.push_back(0);
+    for (auto& bk : blocks) {
+        out.block_primary.push_back(bk.first.first);
+        out.block_seq.insert(out.block_seq.end(), bk.second.begin(), bk.second.end());
+        out.block_seq_off.push_back((int64_t)out.block_seq.size());
+    }
+    // gaps (src/panman.cpp:1835-1845)
+    out.gap_off.push_back(0);
+    for (const auto& g : gaps) {
+        int64_t block_id = 0;
+        std::vector<int32_t> len, pos;
+        if (!pb_fields(g.first, g.second, err, [&](Pb& r, uint32_t f, uint32_t w, uint64_t v, const uint8_t* sb, const uint8_t* se) {
+                if (f == 1) block_id = (int64_t)v;
+                else if (f == 3) return pb_repeated(r, w, v, sb, se, len);
+                else if (f == 4) return pb_repeated(r, w, v, sb, se, pos);
+                return true;
+            }))
+            return false;
+        out.gap_primary.push_back((int32_t)(block_id >> 32));
+        for (size_t j = 0; j < pos.size(); ++j) {
+            out.gap_pos.push_back((uint32_t)pos[j]);
+            out.gap_len.push_back(j < len.size() ? (uint32_t)len[j] : 0);
+        }
+        out.gap_off.push_back((int64_t)out.gap_pos.size());
+    }
+    // circular offsets, rotation indexes, inversions by sequence id (:1847-1860)
+    out.circular.assign(N, -1);
+    out.rotation.assign(N, 0);
+    out.inverted.assign(N, 0);
+    for (int k = 0; k < 3; ++k)
+        for (const auto& x : named[k]) {
+            std::string id;
+            int64_t value = 0;
+            if (!pb_fields(x.first, x.second, err, [&](Pb&, uint32_t f, uint32_t, uint64_t v, const uint8_t* sb, const uint8_t* se) {
+                    if (f == 1) id.assign((const char*)sb, (size_t)(se - sb));
+                    else if (f == 2) value = (int64_t)v;
+                    return true;
+                }))
+                return false;
+            auto it = index.find(id);
+            if (it == index.end()) continue;
+            if (k == 0) out.circular[it->second] = (int32_t)value;
+            else if (k == 1) out.rotation[it->second] = (int32_t)value;
+            else out.inverted[it->second] = value != 0;
+        }
+    return true;
+}
+
 // ---- Cap'n Proto writer (one segment) ---------------------------------------------------
 struct Writer {
     std::vector<uint64_t> w{0};   // word 0: root pointer
@@ -609,6 +882,51 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
     for (uint32_t t = 0; t < trees.count; ++t)
         if (!load_tree(m, trees.at(t), pm_->trees[t])) {
             set_err(m.err);
+            delete pm_;
+            return PM_ERR_ARG;
+        }
+    *out = pm_;
+    return PM_OK;
+}
+
+int pm_panman_load_old(const char* path, pm_panman** out, char* err, int64_t err_len) {
+    auto set_err = [&](const std::string& e) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+    };
+    if (!path || !out) return PM_ERR_ARG;
+    *out = nullptr;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return PM_ERR_ARG; }
+    std::vector<uint8_t> raw, bytes;
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
+    std::fclose(f);
+    std::string e;
+    const bool is_xz = raw.size() >= 6 && raw[0] == 0xFD && raw[1] == '7' && raw[2] == 'z' && raw[3] == 'X';
+    if (is_xz) {
+        if (!xz_decode(raw, bytes, e)) { set_err(e); return PM_ERR_ARG; }
+    } else {
+        bytes.swap(raw);   // an uncompressed message is accepted too
+    }
+    // treeGroup: trees (1), complexMutations (2: not on this path, as in pm_panman_load)
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> trees;
+    const uint8_t* b = bytes.data();
+    if (!pb_fields(b, b + bytes.size(), e, [&](Pb& r, uint32_t fld, uint32_t w, uint64_t, const uint8_t* sb, const uint8_t* se) {
+            if (fld != 1) return true;
+            if (w != 2) return r.fail("tree is not a message");
+            trees.emplace_back(sb, se);
+            return true;
+        })) {
+        set_err(e);
+        return PM_ERR_ARG;
+    }
+    if (trees.empty()) { set_err("protobuf: no tree in the tree group"); return PM_ERR_ARG; }
+    auto* pm_ = new pm_panman();
+    pm_->trees.resize(trees.size());
+    for (size_t t = 0; t < trees.size(); ++t)
+        if (!load_tree_pb(trees[t].first, trees[t].second, pm_->trees[t], e)) {
+            set_err(e);
             delete pm_;
             return PM_ERR_ARG;
         }

@@ -184,9 +184,10 @@ def from_msa_dump(dump: str, names, child_offsets, child_index, root) -> PanMAT:
 
 
 class PanmanFile:
-    """A loaded .panman (libpanman_amd: xz + Cap'n Proto reader, host only)."""
+    """A loaded .panman (libpanman_amd: xz + Cap'n Proto reader, host only); old=True reads
+    the older Protobuf PanMAN (panmanOld.treeGroup) instead."""
 
-    def __init__(self, path: str = None, handle: C.c_void_p = None):
+    def __init__(self, path: str = None, handle: C.c_void_p = None, old: bool = False):
         from ._lib import PanmanError, load
         self.lib = load()
         self.h = C.c_void_p()
@@ -194,9 +195,10 @@ class PanmanFile:
             self.h = handle
             return
         err = C.create_string_buffer(512)
-        rc = self.lib.pm_panman_load(path.encode(), C.byref(self.h), err, 512)
+        fn = self.lib.pm_panman_load_old if old else self.lib.pm_panman_load
+        rc = fn(path.encode(), C.byref(self.h), err, 512)
         if rc != 0:
-            raise PanmanError(f"pm_panman_load({path}): {err.value.decode()}")
+            raise PanmanError(f"{'pm_panman_load_old' if old else 'pm_panman_load'}({path}): {err.value.decode()}")
 
     def __len__(self):
         return self.lib.pm_panman_tree_count(self.h)

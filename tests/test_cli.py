@@ -158,3 +158,32 @@ def test_pangraph_build_then_fasta(tmp_path):
         elif line:
             want[name] += line.upper()
     assert got == want
+
+
+def test_protobuf2capnp_converts_old_panman(tmp_path):
+    """--protobuf2capnp -I old -o out (src/panmanUtils.cpp:939-952): ./panman/out.panman holds
+    the same trees as the Cap'n Proto file the old one was encoded from (tests/_protobuf.py)."""
+    from _protobuf import encode_tree, encode_tree_group
+    rng = np.random.default_rng(12)
+    pms = []
+    for _ in range(2):
+        off, idx, root = random_tree(20, rng, max_children=3)
+        pms.append(random_panmat(rng, off, idx, root, names_for(off), blocks=3))
+    ref = str(tmp_path / "ref.panman")
+    write_panman(ref, pms)
+    f = PanmanFile(ref)
+    old = tmp_path / "old.pb.xz"
+    old.write_bytes(encode_tree_group([encode_tree(f.to_panmat(i), f.newick(i)) for i in range(len(f))]))
+    r = _run(["-I", str(old), "--protobuf2capnp", "-o", "conv"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Writing PanMAN" in r.stdout and "Network Write execution time" in r.stdout
+    g = PanmanFile(str(tmp_path / "panman" / "conv.panman"))
+    assert len(g) == len(f)
+    for i in range(len(f)):
+        a, b = f.to_panmat(i), g.to_panmat(i)
+        assert a.names == b.names and (a.child_offsets == b.child_offsets).all()
+        assert (a.child_index == b.child_index).all()
+        for k in a._arrays:
+            assert np.array_equal(a._arrays[k], b._arrays[k]), k
+    r = _run(["-I", str(old), "--protobuf2capnp"], tmp_path)
+    assert r.returncode == 1 and "Output file not provided" in r.stderr

@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of two library builds on the same box, interleaved: tools/ab_lib.sh VARIANT [bench args]
+#   (VARIANT = build_var/VARIANT/libpanman_amd.so vs panman_amd/libpanman_amd.so)
+set -o pipefail
+var=$1; shift
+mkdir -p gpurun_out/ab
+for rep in 1 2; do
+  for v in cur $var; do
+    if [ $v = cur ]; then L=panman_amd/libpanman_amd.so; else L=build_var/$v/libpanman_amd.so; fi
+    PANMAN_AMD_LIB=$L timeout -k 10 200 python bench.py --no-cpu --with none --steps 10 --warmup 3 "$@" > gpurun_out/ab/$v.json 2> gpurun_out/ab/$v.err || { tail -3 gpurun_out/ab/$v.err; exit 1; }
+    python3 -c "import json;d=json.load(open('gpurun_out/ab/$v.json'));r=d['roofline'];print('$v', round(d['ms_per_step'],3), r['kernel'], r['kernel_ms_per_step'], r['other_kernels_ms_per_step'])"
+  done
+done
