@@ -114,6 +114,9 @@ def load():
             raise PanmanError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            # an experiment build given by PANMAN_AMD_LIB may predate newer entry points
+            if os.environ.get("PANMAN_AMD_LIB") and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
