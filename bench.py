@@ -282,7 +282,11 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
     steps = max(1, args.steps)
     fitch = mode == panman_amd.MODE_FITCH
     names = ("k_fitch_up", "k_down<Fitch>") if fitch else ("k_sankoff_up", "k_down<Sankoff>")
-    prof_names = {names[0]: names[0], names[1]: "k_down"}
+    # each timed class is a pass: every launch of these kernels (levels, narrow bands, wide
+    # nodes, Sankoff parts, the tail of leaf-ish children) -- PMC bytes are summed per run
+    up_k = ("k_fitch_up", "k_fitch_up_wide", "k_fitch_up_band") if fitch else \
+        ("k_sankoff_up", "k_sankoff_up_wide", "k_sankoff_part", "k_sankoff_merge")
+    prof_names = {names[0]: up_k, names[1]: ("k_down", "k_down_band", "k_tail")}
     key = "fitch" if fitch else "sankoff"
     classes = {
         names[0]: (ms[0] / steps, launches[0] / steps, design["up"]),
@@ -291,15 +295,18 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
     dom = max(classes, key=lambda k: classes[k][0])
     dms, dl, dbytes = classes[dom]
     achieved = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
-    traffic_all = {}
+    traffic_all, score_traffic = {}, None   # HBM bytes per run of each pass (PMC)
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            for k, pn in prof_names.items():
-                traffic_all[k] = tj.get(pn, {}).get(f"{key}:{L}x{s_local}")
+            wk = f"{key}:{L}x{s_local}:step"
+            for k, kernels in prof_names.items():
+                got = [tj[n][wk] for n in kernels if wk in tj.get(n, {})]
+                traffic_all[k] = sum(got) if got else None
+            score_traffic = tj.get("k_site_score", {}).get(wk)
         except (OSError, ValueError):
             traffic_all = {}
-    traffic = traffic_all.get(dom)
+    traffic = traffic_all[dom] / dl if traffic_all.get(dom) and dl else None   # per launch of the pass
     if fitch:   # SURVEY.md §8d contract: 2-B sets through memory
         contract = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1)) + \
             s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
@@ -310,6 +317,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
     out = {
         "bound": "hbm",
         "kernel": dom,
+        "kernel_note": "the pass's launches: " + " + ".join(prof_names[dom]),
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -337,8 +345,9 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
         "contract_effective_GBs": round(contract / (ms_step * 1e-3) / 1e9, 1),
     }
     if all(traffic_all.get(k) for k in names):
-        step_traffic = sum(traffic_all[k] * classes[k][1] for k in names)
+        step_traffic = sum(traffic_all[k] for k in names) + (score_traffic or 0.0)
         out["step_traffic_bytes"] = step_traffic
+        out["step_traffic_GBs"] = round(step_traffic / (ms_step * 1e-3) / 1e9, 1)
         out["traffic_over_floor"] = round(step_traffic / design["floor"], 3)
     copy_gbs = round(panman_amd.stream_copy_rate(torch.cuda.current_device()), 1) if rank == 0 else None
     out["measured_copy_GBs"] = copy_gbs

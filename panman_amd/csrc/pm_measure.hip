@@ -147,9 +147,14 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                     up += b;
                     part[1] += b;
                 }
-                if (k >= e0 + 2 && (ch < 0 || vnode[ch])) {   // k_tail item: parent masks + parent final
-                    down += 64.0 + lane * popc(q[0] | q[1]);
-                    part[7] += 64.0 + lane * popc(q[0] | q[1]);
+                // k_tail item (a leaf-ish child beyond the second, or an S2 / S3 child in the
+                // subtree form): descriptor + parent masks (64 B each), the parent's final on
+                // its dirty non-consensus lanes
+                const bool tail = (k >= e0 + 2 && (ch < 0 || vnode[ch])) || (sub && ch >= 0 && vnode[ch] > 2);
+                if (tail) {
+                    const double b = 128.0 + lane * popc((q[0] | q[1]) & (d == root ? ~0ull : q[2]));
+                    down += b;
+                    part[7] += b;
                 }
             }
             // pre-order: own record, parent final (non-consensus lanes), compact final out

@@ -41,13 +41,20 @@ def main():
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
     res = json.load(open(out)) if os.path.exists(out) else {}
+    # runs of the profiled command: k_site_score is launched exactly once per parsimony run,
+    # so "<key>:step" = a kernel's HBM bytes per run (all its launches: levels, bands, tail)
+    runs = fetch.get("k_site_score", [0])[0]
     for k in sorted(set(fetch) & set(write)):
         nf, bf = fetch[k]
         nw, bw = write[k]
         per_launch = 2.0 * bf / nf + bw / nw
         res.setdefault(k, {})[key] = per_launch
+        step = ""
+        if runs:
+            res[k][key + ":step"] = (2.0 * bf + bw * nf / nw) / runs
+            step = f"  {res[k][key + ':step'] / 1e9:8.3f} GB/run ({nf / runs:.1f} launches)"
         print(f"{k:32s} launches {nf:5d}  fetch(x2) {2 * bf / nf / 1e6:10.2f} MB  write {bw / nw / 1e6:10.2f} MB"
-              f"  -> {per_launch / 1e6:10.2f} MB/launch")
+              f"  -> {per_launch / 1e6:10.2f} MB/launch{step}")
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
 
 

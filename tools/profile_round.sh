@@ -1,0 +1,17 @@
+#!/bin/bash
+# The round's evidence set (GPU box, repo root): default bench line, N* Fitch / Sankoff
+# rocprofv3 stats + PMC passes, C3 / C2 kernel traces, replay PMC traffic.
+#   tools/profile_round.sh TAG   ->  gpurun_out/{bench_default_TAG.json, prof_TAG*, trace_TAG_*}
+set -o pipefail
+cd "$(dirname "$0")/.."
+tag=$1
+mkdir -p gpurun_out
+timeout -k 10 600 python bench.py > gpurun_out/bench_default_$tag.json 2> gpurun_out/bench_default_$tag.err || { echo "bench failed"; tail -5 gpurun_out/bench_default_$tag.err; exit 1; }
+echo "default bench ok"
+bash tools/profile_fitch.sh $tag || exit 2
+bash tools/profile_fitch.sh ${tag}_sankoff --mode sankoff || exit 3
+bash tools/trace_stats.sh ${tag}_c3 --tree sars-like --leaves 100000 --steps 5 --warmup 2 || exit 4
+bash tools/trace_stats.sh ${tag}_c3_sankoff --tree sars-like --leaves 100000 --mode sankoff --steps 5 --warmup 2 || exit 5
+bash tools/trace_stats.sh ${tag}_c2 --leaves 4096 --sites 15000 --steps 10 --warmup 3 || exit 6
+bash tools/profile_replay.sh $tag || exit 7
+echo "profile_round $tag done"
