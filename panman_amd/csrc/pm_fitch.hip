@@ -238,16 +238,11 @@ __device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, 
     push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms);
 }
 
+// One workgroup = one wide node x tile.
 template <bool AP>
-__global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
-    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    block_item(a.tiles, item, tile);
-    const NodeDesc& d = a.desc[item];
+__device__ __forceinline__ void wide_node(const UpArgs& a, const NodeDesc& d, int tile, int wave, int lane,
+                                          uint32_t (*part)[33][kWave]) {
     const int64_t word = (int64_t)tile * kWave + lane;
-
     uint32_t both[16], either[16], vd;
     wide_fold<AP, kWavesPerBlock>(a, d.e0, d.e1, wave, tile, lane, word, both, either, vd);
     if (wave > 0) {
@@ -270,6 +265,36 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
         vd |= part[w][32][lane];
     }
     wide_finish<AP>(a, d, tile, lane, word, both, either, vd);
+}
+
+template <bool AP>
+__global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
+    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    block_item(a.tiles, item, tile);
+    wide_node<AP>(a, a.desc[item], tile, wave, lane, part);
+}
+
+// A level holding nodes of both kinds (polytomies, deep trees) in ONE launch instead of two
+// dependent ones: blocks [0, narrow_blocks) are k_fitch_up's (a wave per (node, tile) over
+// a.desc), the rest k_fitch_up_wide's (a workgroup per (wide node, tile) over wdesc).
+static_assert(PM_TILE_FAST, "k_fitch_up_mixed numbers its blocks on one grid axis");
+template <bool AP, bool SUB>
+__global__ __launch_bounds__(kBlock) void k_fitch_up_mixed(UpArgs a, const NodeDesc* wdesc, int32_t narrow_blocks) {
+    __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if ((int32_t)blockIdx.x < narrow_blocks) {
+        int32_t item;
+        int tile;
+        wave_item(wave, a.tiles, item, tile);
+        if (item < a.count) fitch_up_node<AP, false, SUB>(a, a.desc[item], tile, lane);
+        return;
+    }
+    const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
+    const int32_t item = b / a.tiles;
+    wide_node<AP>(a, wdesc[item], b - item * a.tiles, wave, lane, part);
 }
 
 // Narrow levels (PM_OPT_NARROW): a run of consecutive post-order levels with few nodes each
@@ -422,6 +447,18 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         // out-degree <= 3: one wave per (node, tile); wider: one workgroup per (node, tile)
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
                       e = class_off[(h + 1) * kDegreeClasses];
+        if (m > b && e > m && (int64_t)(m - b) * tiles <= kMixedMaxWaves) {   // both kinds: one launch
+            up.desc = up_desc + b;
+            up.count = m - b;
+            const int32_t nb = (int32_t)wave_grid(up.count, tiles).x;
+            const dim3 grid((unsigned)(nb + (int64_t)(e - m) * tiles));
+            timer_begin(c, 0);
+            if (sub) hipLaunchKernelGGL((k_fitch_up_mixed<true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+            else if (ap) hipLaunchKernelGGL((k_fitch_up_mixed<true, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+            else hipLaunchKernelGGL((k_fitch_up_mixed<false, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+            timer_end(c, 0);
+            continue;
+        }
         if (m > b) {
             up.desc = up_desc + b;
             up.count = m - b;

@@ -53,13 +53,7 @@ __device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& fi
 // AP: every leaf present -- the first two children's loads are issued together (see
 // fetch_child_ap), the third (if any) after.
 template <int B, bool AP>
-__global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    wave_item(wave, a.tiles, item, tile);
-    if (item >= a.count) return;
-    const NodeDesc& d = a.desc[item];
+__device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node;
     const int64_t word = (int64_t)tile * kWave + lane;
 
@@ -132,19 +126,24 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
+template <int B, bool AP>
+__global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    wave_item(wave, a.tiles, item, tile);
+    if (item >= a.count) return;
+    sankoff_up_node<B, AP>(a, a.desc[item], tile, lane);
+}
+
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
 // to its 4 waves (64 encodings per vector load, two children fetched before either is
 // counted); the waves' bit-sliced counters are summed through LDS (the sum of the
 // per-wave counts is the node's count: src/fitchSankoff.cpp:391-402 is a sum over
 // children), then Z0 / Z1 as in k_sankoff_up.
 template <int B>
-__global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
-    __shared__ uint32_t part[16 * B + 1][kWave];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    int32_t item;
-    int tile;
-    block_item(a.tiles, item, tile);
-    const NodeDesc& d = a.desc[item];
+__device__ __forceinline__ void sankoff_wide_node(const UpArgs& a, const NodeDesc& d, int tile, int wave, int lane,
+                                                  uint32_t (*part)[kWave]) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     uint32_t cnt[16][B];
@@ -229,6 +228,37 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
     uint64_t rx, rs;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
+}
+
+template <int B>
+__global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
+    __shared__ uint32_t part[16 * B + 1][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int32_t item;
+    int tile;
+    block_item(a.tiles, item, tile);
+    sankoff_wide_node<B>(a, a.desc[item], tile, wave, lane, part);
+}
+
+// A small level holding nodes of out-degree <= 3 and 4..255 in ONE launch instead of two or
+// three dependent ones (deep trees with polytomies): blocks [0, narrow_blocks) are
+// k_sankoff_up's waves over a.desc, the rest one workgroup per (wide node, tile) over wdesc
+// with BW-bit counters (the 16-child class counted at the wider width: same sums).
+static_assert(PM_TILE_FAST, "k_sankoff_up_mixed numbers its blocks on one grid axis");
+template <int BW, bool AP>
+__global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const NodeDesc* wdesc, int32_t narrow_blocks) {
+    __shared__ uint32_t part[16 * BW + 1][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if ((int32_t)blockIdx.x < narrow_blocks) {
+        int32_t item;
+        int tile;
+        wave_item(wave, a.tiles, item, tile);
+        if (item < a.count) sankoff_up_node<2, AP>(a, a.desc[item], tile, lane);
+        return;
+    }
+    const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
+    const int32_t item = b / a.tiles;
+    sankoff_wide_node<BW>(a, wdesc[item], b - item * a.tiles, wave, lane, part);
 }
 
 // Nodes of any out-degree above 255 (src/fitchSankoff.cpp:391-402 sums over every child,
@@ -396,7 +426,46 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
+    // nodes [b, e) of one level with more than 255 children: parts, then the merge
+    auto launch_parts = [&](int32_t b, int32_t e) {
+        const int32_t p0 = part_off[b], np = part_off[e] - p0;
+        int32_t widest = 0;
+        for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[virt][i]);
+        UpArgs pa = up;
+        pa.desc = up_desc;   // parts name their node by its global up-order position
+        UpArgs mg = up;
+        mg.desc = up_desc + b;
+        mg.count = e - b;
+        const dim3 grid = wave_grid(mg.count, tiles);
+        timer_begin(c, 0);
+        hipLaunchKernelGGL(k_sankoff_part, wave_grid(np, tiles), dim3(kBlock), 0, c->stream, pa, parts + p0, np, c->sk_parts);
+        if (widest < (1 << 16)) hipLaunchKernelGGL(k_sankoff_merge<16>, grid, dim3(kBlock), 0, c->stream, mg, c->sk_parts);
+        else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, c->stream, mg, c->sk_parts);
+        timer_end(c, 0);
+    };
     for (int h = 0; h < H; ++h) {
+        {   // a small level with narrow and wide (<= 255 children) nodes: one launch
+            const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
+                          w4 = class_off[h * kDegreeClasses + 2], w8 = class_off[h * kDegreeClasses + 3];
+            if (m > b && w8 > m && (int64_t)(m - b) * tiles <= kMixedMaxWaves) {
+                up.desc = up_desc + b;
+                up.count = m - b;
+                const int32_t nb = (int32_t)wave_grid(up.count, tiles).x;
+                const dim3 grid((unsigned)(nb + (int64_t)(w8 - m) * tiles));
+                timer_begin(c, 0);
+                if (w8 > w4 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (w8 > w4) hipLaunchKernelGGL((k_sankoff_up_mixed<8, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<4, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else hipLaunchKernelGGL((k_sankoff_up_mixed<4, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                timer_end(c, 0);
+                // the level's nodes above 255 children (if any) still go to the parts below
+                for (int k = 3; k < kDegreeClasses; ++k) {
+                    const int32_t pb = class_off[h * kDegreeClasses + k], pe = class_off[h * kDegreeClasses + k + 1];
+                    if (pe > pb) launch_parts(pb, pe);
+                }
+                continue;
+            }
+        }
         for (int k = 0; k < kDegreeClasses; ++k) {
             const int32_t b = class_off[h * kDegreeClasses + k];
             const int32_t e = class_off[h * kDegreeClasses + k + 1];
@@ -410,15 +479,9 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
             else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, c->stream, up);
             else {   // more than 255 children: parts, then the merge
-                const int32_t p0 = part_off[b], np = part_off[e] - p0;
-                int32_t widest = 0;
-                for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[virt][i]);
-                UpArgs pa = up;
-                pa.desc = up_desc;   // parts name their node by its global up-order position
-                hipLaunchKernelGGL(k_sankoff_part, wave_grid(np, tiles), dim3(kBlock), 0, c->stream, pa, parts + p0, np,
-                                   c->sk_parts);
-                if (widest < (1 << 16)) hipLaunchKernelGGL(k_sankoff_merge<16>, grid, dim3(kBlock), 0, c->stream, up, c->sk_parts);
-                else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, c->stream, up, c->sk_parts);
+                timer_end(c, 0);
+                launch_parts(b, e);
+                continue;
             }
             timer_end(c, 0);
         }
@@ -454,7 +517,23 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     const int D = (int)down_off.size() - 1;
+    const bool dense_all = virt && ht.down_dense_v;
     for (int d = 0; d < D; ++d) {
+        if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {   // PM_OPT_NARROW
+            int d1 = d + 1;
+            while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
+            if (d1 - d >= 2) {
+                dn.desc = down_desc;
+                const int32_t* tab = dt.lvl + ht.lvl_down[virt ? 1 : 0];
+                const int32_t* base = dense_all ? tab : nullptr;
+                timer_begin(c, 1);
+                if (c->leaves_all_present) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else hipLaunchKernelGGL((k_down_band<Mode::kSankoff, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                timer_end(c, 1);
+                d = d1 - 1;
+                continue;
+            }
+        }
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;

@@ -1,6 +1,7 @@
 """PM_OPT_NARROW: runs of narrow levels walked by one band launch (k_fitch_up_band /
-k_down_band, one workgroup per tile, barriers between levels) give exactly the records,
-scores and root codes of one launch per level -- and of the oracle."""
+k_down_band, one workgroup per tile, barriers between levels) and small levels with both
+narrow and wide nodes in one mixed launch give exactly the records, scores and root codes
+of one launch per level -- and of the oracle."""
 import numpy as np
 import pytest
 
@@ -24,6 +25,33 @@ def _run(engine, mode, narrow):
     got = engine.mutations()
     score, rootc = engine.site_results()
     return got, score, rootc
+
+
+@pytest.mark.parametrize("narrow", [16, 1024])
+@pytest.mark.parametrize("virtual", [True, False])
+def test_sankoff_sars_like_bands_equal_levels(engine, oracle, narrow, virtual):
+    """Sankoff on T2 trees: pre-order bands and the mixed (narrow + wide) post-order launches
+    of small levels give the records of one launch per level and class -- and the oracle's."""
+    off, idx, root = panman_amd.sars_like_tree(3000, seed=12)
+    engine.set_virtual(virtual)
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, 2200, seed=4)
+    want = _run(engine, panman_amd.MODE_SANKOFF, 0)
+    got = _run(engine, panman_amd.MODE_SANKOFF, narrow)
+    engine.set_narrow(16)
+    engine.set_virtual(True)
+    assert got[0].shape == want[0].shape and (got[0] == want[0]).all()
+    assert (got[1] == want[1]).all() and (got[2] == want[2]).all()
+    sample = slice(300, 364)
+    codes = engine.leaf_codes(sample.start, sample.stop - sample.start, 3000)
+    cons = engine.consensus(sample.start, sample.stop - sample.start)
+    n = off.shape[0] - 1
+    node_row = np.full(n, -1, np.int32)
+    node_row[:3000] = np.arange(3000)
+    _, ref = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, None, algo=1, threads=8)
+    ref[:, 1] += sample.start
+    sel = got[0][(got[0][:, 1] >= sample.start) & (got[0][:, 1] < sample.stop)]
+    assert sel.shape == ref.shape and (sel == ref).all()
 
 
 @pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
@@ -64,7 +92,7 @@ def test_bands_vs_oracle_absent_and_polytomies(engine, oracle, variant, seed):
 
 @pytest.mark.parametrize("mode", [panman_amd.MODE_BLOCK_FITCH, panman_amd.MODE_SANKOFF])
 def test_block_and_sankoff_unaffected(engine, mode):
-    """Block Fitch also walks its narrow levels in bands; Sankoff ignores the option."""
+    """Block Fitch walks its narrow levels in bands; Sankoff its narrow pre-order levels."""
     rng = np.random.default_rng(77)
     off, idx, root = random_tree(300, rng, max_children=4, unary=0.1)
     n = off.shape[0] - 1
