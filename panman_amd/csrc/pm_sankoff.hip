@@ -261,6 +261,20 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
     sankoff_wide_node<BW>(a, wdesc[item], b - item * a.tiles, wave, lane, part);
 }
 
+// Narrow post-order levels (PM_OPT_NARROW, see k_fitch_up_band): a run of levels whose
+// nodes all have out-degree <= 3, at most narrow_max of them per level, walked by one
+// launch, one 1024-thread workgroup per tile, a barrier between levels.
+template <bool AP>
+__global__ __launch_bounds__(kBandBlock) void k_sankoff_up_band(UpArgs a, const int32_t* class_off, int32_t h0, int32_t h1) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int tile = blockIdx.x;
+    for (int32_t h = h0; h < h1; ++h) {
+        const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1];
+        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP>(a, a.desc[i], tile, lane);
+        __syncthreads();
+    }
+}
+
 // Nodes of any out-degree above 255 (src/fitchSankoff.cpp:391-402 sums over every child,
 // whatever their number): the children are cut into parts of kPartChildren; one wave per
 // (part, tile) counts its part into 8-bit bit-sliced counters (k_sankoff_part) and writes
@@ -443,7 +457,27 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, c->stream, mg, c->sk_parts);
         timer_end(c, 0);
     };
+    // runs of >= 2 narrow levels with only out-degree <= 3 nodes (PM_OPT_NARROW): one band each
+    auto narrow_up = [&](int h) {
+        const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
+                      e = class_off[(h + 1) * kDegreeClasses];
+        return e == m && m - b <= c->narrow_max;
+    };
     for (int h = 0; h < H; ++h) {
+        if (c->narrow_max > 0 && narrow_up(h)) {
+            int h1 = h + 1;
+            while (h1 < H && narrow_up(h1)) ++h1;
+            if (h1 - h >= 2) {
+                up.desc = up_desc;
+                const int32_t* tab = dt.lvl + ht.lvl_up[virt ? 1 : 0];
+                timer_begin(c, 0);
+                if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_band<true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else hipLaunchKernelGGL((k_sankoff_up_band<false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                timer_end(c, 0);
+                h = h1 - 1;
+                continue;
+            }
+        }
         {   // a small level with narrow and wide (<= 255 children) nodes: one launch
             const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
                           w4 = class_off[h * kDegreeClasses + 2], w8 = class_off[h * kDegreeClasses + 3];
