@@ -187,3 +187,22 @@ def test_protobuf2capnp_converts_old_panman(tmp_path):
             assert np.array_equal(a._arrays[k], b._arrays[k]), k
     r = _run(["-I", str(old), "--protobuf2capnp"], tmp_path)
     assert r.returncode == 1 and "Output file not provided" in r.stderr
+
+
+@pytest.mark.gpu
+def test_protobuf2capnp_then_fasta_on_gpu(tmp_path, oracle):
+    """An old Protobuf PanMAN converted by --protobuf2capnp replays on the GPU to the same
+    aligned FASTA the oracle gives for the tree it was encoded from."""
+    from _protobuf import encode_tree, encode_tree_group
+    rng = np.random.default_rng(21)
+    off, idx, root = random_tree(30, rng, max_children=3, unary=0.1)
+    ref = str(tmp_path / "ref.panman")
+    write_panman(ref, [random_panmat(rng, off, idx, root, names_for(off), blocks=4)])
+    f = PanmanFile(ref)
+    (tmp_path / "old.pb.xz").write_bytes(encode_tree_group([encode_tree(f.to_panmat(0), f.newick(0))]))
+    r = _run(["-I", "old.pb.xz", "--protobuf2capnp", "-o", "conv"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    r = _run(["-I", "panman/conv.panman", "-m", "-o", "conv"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    got = parse_records(open(tmp_path / "info" / "conv_0.msa").read())
+    assert got == parse_records(oracle.fasta(f.to_panmat(0), True))
