@@ -56,6 +56,10 @@ def parse():
     p.add_argument("--narrow", type=int, default=-1,
                    help="Fitch: PM_OPT_NARROW, most nodes per level walked in a band launch (-1: library "
                         "default 16; 0: one launch per level)")
+    p.add_argument("--group", type=int, default=-1,
+                   help="Fitch: PM_OPT_GROUP_WAVES, most waves of grouped pre-order levels in one launch "
+                        "(-1: library default, 0: off)")
+    p.add_argument("--group-levels", type=int, default=3, help="Fitch: PM_OPT_GROUP_LEVELS (2 or 3)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -113,6 +117,8 @@ def main():
         eng.set_subtree(False)
     if args.narrow >= 0:
         eng.set_narrow(args.narrow)
+    if args.group >= 0 or args.group_levels != 3:
+        eng.set_group(args.group if args.group >= 0 else 32768, args.group_levels)
 
     torch.cuda.synchronize()
     log(rank, f"[bench] columns {lo}..{hi} generated ({time.time() - t0:.1f}s)")

@@ -96,12 +96,18 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  nodes each (a node of out-degree > 3 counts 4) is walked by one launch,
  *                  one 1024-thread workgroup per 2048-site tile with a barrier between levels,
  *                  instead of one launch per level (deep, ladder-like trees); 0 = off.
+ *   PM_OPT_GROUP_WAVES (default 32768): Fitch -- up to PM_OPT_GROUP_LEVELS consecutive
+ *                  pre-order levels of at most this many (node, tile) waves together go to one
+ *                  launch, the lower levels' waves recomputing their ancestors' finals; 0 = off.
+ *   PM_OPT_GROUP_LEVELS (default 3): 2 or 3 levels per such launch.
  * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
  * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
 #define PM_OPT_SUBTREE 6
 #define PM_OPT_NARROW 7
+#define PM_OPT_GROUP_WAVES 8
+#define PM_OPT_GROUP_LEVELS 9
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

@@ -537,12 +537,39 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
-        const dim3 grid = wave_grid(dn.count, tiles);
-        timer_begin(c, 1);
         // level d = one range of dense indices: [down_off[d], down_off[d+1]) in the leaf-parent
         // form, from down_dense_base_k[d] in the subtree form
         const bool dense = sub ? ht.down_dense_k : virt && ht.down_dense_v;
         dn.dense_base = !dense ? -1 : sub ? ht.down_dense_base_k[d] : down_off[d];
+        // levels d .. d + g - 1 in one launch (PM_OPT_GROUP_*), none of them starting a band
+        auto narrow_down = [&](int l) { return c->narrow_max > 0 && down_off[l + 1] - down_off[l] <= c->narrow_max; };
+        auto band_at = [&](int l) { return narrow_down(l) && l + 1 < D && narrow_down(l + 1); };
+        int g = 1;
+        int64_t items = dn.count;
+        while (!block && c->group_waves > 0 && g < std::min(c->group_levels, kGroupLevels) && d + g < D) {
+            const int32_t ng = down_off[d + g + 1] - down_off[d + g];
+            if (ng == 0 || (items + ng) * tiles > c->group_waves || band_at(d + g)) break;
+            items += ng;
+            ++g;
+        }
+        if (g > 1) {
+            for (int k = 0; k < kGroupLevels; ++k) {
+                const int l = std::min(d + k, d + g - 1);
+                if (k > 0) dn.split[k - 1] = k < g ? down_off[d + k] - down_off[d] : (int32_t)items;
+                dn.dense_g[k] = !dense ? -1 : sub ? ht.down_dense_base_k[l] : down_off[l];
+            }
+            dn.count = (int32_t)items;
+            const dim3 grid = wave_grid(dn.count, tiles);
+            timer_begin(c, 1);
+            if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            timer_end(c, 1);
+            d += g - 1;
+            continue;
+        }
+        const dim3 grid = wave_grid(dn.count, tiles);
+        timer_begin(c, 1);
         // (subtree form: the levels' descriptors omit S2 / S3 children, whose records come
         // from the tail launch, so the lean kernels run every level)
         if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);

@@ -199,7 +199,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
-                              (uint64_t)c->narrow_max,
+                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -386,6 +386,16 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_NARROW) {
         if (value < 0 || value > 1024) return fail(c, PM_ERR_ARG, "PM_OPT_NARROW: 0..1024 items per level");
         c->narrow_max = (int32_t)value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_GROUP_WAVES) {
+        if (value < 0) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_WAVES: >= 0 waves");
+        c->group_waves = value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_GROUP_LEVELS) {
+        if (value < 2 || value > 3) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_LEVELS: 2 or 3");
+        c->group_levels = (int32_t)value;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
@@ -745,15 +755,24 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
         return desc;
     };
-    const std::vector<NodeDesc> down_desc = make_desc(down_order, ht.child_enc);
-    const std::vector<NodeDesc> down_desc_v = make_desc(down_order_v, child_enc_v);
+    // pre-order descriptors carry the grandparent and great-grandparent (k_down level groups
+    // recompute the ancestors' finals)
+    auto with_gp = [&](std::vector<NodeDesc> desc) {
+        for (NodeDesc& x : desc) {
+            x.pad0 = x.parent >= 0 ? parent_dense[x.parent] : -1;
+            x.pad1 = x.pad0 >= 0 ? parent_dense[x.pad0] : -1;
+        }
+        return desc;
+    };
+    const std::vector<NodeDesc> down_desc = with_gp(make_desc(down_order, ht.child_enc));
+    const std::vector<NodeDesc> down_desc_v = with_gp(make_desc(down_order_v, child_enc_v));
     const std::vector<NodeDesc> up_desc = make_desc(up_order, ht.child_enc);
     const std::vector<NodeDesc> up_desc_v = make_desc(up_order_v, child_enc_v);
     const std::vector<NodeDesc> up_desc_k = make_desc(up_order_k, child_enc_k);
     // subtree-form pre-order descriptors list only the children the level kernel handles:
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)
-    std::vector<NodeDesc> down_desc_k = make_desc(down_order_k, child_enc_k);
+    std::vector<NodeDesc> down_desc_k = with_gp(make_desc(down_order_k, child_enc_k));
     for (NodeDesc& x : down_desc_k) {
         const int32_t deg = x.e1 - x.e0;
         if (deg > 2) continue;   // S2 / S3 nodes have parents of out-degree <= 2

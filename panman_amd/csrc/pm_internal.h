@@ -42,7 +42,7 @@ enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
 // and, for virtual leaf-parent children, their leaves).
 struct alignas(64) NodeDesc {
     int32_t node, parent, e0, e1;
-    int32_t c0, c1, pad0, pad1;
+    int32_t c0, c1, pad0, pad1;    // pad0: Sankoff up parts -- the first part; pre-order -- the grandparent, pad1 the great-grandparent (dense, -1)
     int32_t vl0[4], vl1[4];
 };
 
@@ -172,6 +172,8 @@ struct pm_ctx {
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
     bool subtree_form = true;         // Fitch, all leaves present: S2 / S3 inline too (PM_OPT_SUBTREE)
     int32_t narrow_max = 16;          // Fitch: runs of levels this narrow go to one band launch (PM_OPT_NARROW)
+    int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
+    int32_t group_levels = 3;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
 
     // column shard
     int64_t num_sites = 0;

@@ -609,10 +609,12 @@ struct DownArgs {
     const uint8_t* leaf_flag;
     const uint4* leaf_planes;
     const uint32_t* leaf_present;
-    uint4* sets;           // records; after a node's step its complex lanes hold its final
+    uint4* sets;           // records; after a node's step its complex lanes' finals sit in final_slot
     const uint64_t* cmask;
     uint4* root_final;     // [W] the root's final codes (a forced root's differ from its set)
     int32_t dense_base;    // k_down<.., DENSE>: the level's first dense index (item k = dense base + k)
+    int32_t split[2];      // k_down<.., GROUP>: the first items of the group's levels 1 and 2
+    int32_t dense_g[3];    // k_down<.., DENSE, .., GROUP>: each level's first dense index
     const uint4* cons;
     int32_t root_dense;
     int32_t tiles;
@@ -1021,15 +1023,24 @@ __device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* sta
     return true;
 }
 
+// Where a complex lane's final goes: the record's simple area past the simple lanes' codes
+// (slots popc(s) .. popc(s) + popc(x) - 1 are never used by the set, x and s being
+// disjoint), so the set's complex planes stay intact after the node's pre-order step and a
+// descendant's wave in the same launch may still recompute the node's final from them
+// (k_down level groups).
+__device__ __forceinline__ uint32_t final_slot(const RecMask& m) {
+    return (uint32_t)__builtin_popcountll(m.s) + lanes_below(m.x);
+}
+
 // Compact finals.  After an internal node's pre-order step its final codes are: the
-// root's in root_final; a complex lane's in quad 0 of that lane's record slot (the set is
-// not read again); every other lane's its record code -- a single-code set resolves to
+// root's in root_final; a complex lane's in its final_slot of the record's simple area;
+// every other lane's its record code -- a single-code set resolves to
 // its code whatever the parent holds (src/fitchSankoff.cpp:115-123 and :513-530 with
 // Z0 = {c}, Z1 = {}).  Only complex lanes are written; a child reads 16 B per lane only
 // for its parent's non-consensus lanes, locating them with the parent's x / s masks
 // (pushed into its own mask record by the post-order pass, RecMask::px / ps).
 __device__ __forceinline__ uint4 rec_final(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
-    const uint4* src = ((m.x >> lane) & 1ull) ? p + kWave + lanes_below(m.x)
+    const uint4* src = ((m.x >> lane) & 1ull) ? p + final_slot(m)
                                               : ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
     return *src;
 }
@@ -1054,7 +1065,7 @@ __device__ __forceinline__ uint4 node_final(const DownArgs& a, int32_t node, int
 __device__ __forceinline__ void store_final(const DownArgs& a, bool is_root, uint4* p, const RecMask& m, int lane,
                                             int64_t word, const uint32_t* F) {
     if (is_root) a.root_final[word] = make_uint4(F[0], F[1], F[2], F[3]);
-    else if ((m.x >> lane) & 1ull) p[kWave + lanes_below(m.x)] = make_uint4(F[0], F[1], F[2], F[3]);
+    else if ((m.x >> lane) & 1ull) p[final_slot(m)] = make_uint4(F[0], F[1], F[2], F[3]);
 }
 
 // The node's final codes F (code planes) and the sites where it is resolved (pres), from
@@ -1135,9 +1146,16 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
 #endif
 // One pre-order wave: node `n` (its descriptor d) x tile; `salt` spreads the waves over the
 // record shards; `stage` is the wave's LDS record stage (kStage records).
-template <Mode M, bool AP, bool SUB>
+// GROUP (Fitch modes): the launch holds up to kGroupLevels consecutive levels; a wave of
+// the group's level g > 0 does not wait for its ancestors' finals to be stored -- it
+// recomputes them top down, each from the ancestor's set (intact: final_slot) and the final
+// above it, starting from the last final stored before the launch (descriptor: pad0 =
+// grandparent, pad1 = great-grandparent), so g + 1 levels cost one launch.
+constexpr int kGroupLevels = 3;
+template <Mode M, bool AP, bool SUB, bool GROUP = false>
 __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, int32_t n, uint32_t salt, int tile,
-                                          int lane, pm_mut* stage) {
+                                          int lane, pm_mut* stage, int gen = 0) {
+    static_assert(!GROUP || M != Mode::kSankoff, "level groups: Fitch modes only");
     const int32_t parent = d.parent, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
@@ -1148,7 +1166,26 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     const RecMask m = rec_mask(a.cmask, rec);
     uint4* const p = a.sets + rec * REC;
     uint32_t own[16], pc[4], F[4];
-    {
+    if (GROUP && gen > 0) {
+        // ancestors inside the group, top first: chain[0 .. gen-1], chain[gen-1] = parent
+        const int32_t chain[2] = {gen == 2 ? d.pad0 : parent, parent};
+        const int32_t above = gen == 2 ? d.pad1 : d.pad0;   // its final is stored (-1: chain[0] is the root)
+        uint4 q;
+        for (int k = 0; k < gen; ++k) {
+            const int32_t v = chain[k + 2 - gen];
+            const size_t vrec = (size_t)v * a.tiles + tile;
+            const RecMask mv = rec_mask(a.cmask, vrec);   // its (x, s) and the final above's (px, ps)
+            const bool vroot = k == 0 && above < 0;
+            if (k == 0) q = vroot ? a.cons[word] : parent_final<REC>(a, above, mv, tile, lane, word);
+            SetFetch f;
+            fetch_fitch_set(a.sets + vrec * REC, mv, a.cons, lane, word, f);
+            uint32_t vown[16], vz1[16], gc[4] = {q.x, q.y, q.z, q.w}, VF[4], vpres;
+            expand_fitch_set(f, vown);
+            resolve_final<M>(a, vroot, word, vown, vz1, gc, VF, vpres);
+            q = make_uint4(VF[0], VF[1], VF[2], VF[3]);
+        }
+        pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
+    } else {
         const uint4 q = is_root ? a.cons[word] : parent_final<REC>(a, parent, m, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
@@ -1232,8 +1269,10 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
 }
 
-template <Mode M, bool AP, bool DENSE, bool SUB = false>
-__global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
+// GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, split[2] =
+// count), dense from dense_g[g].
+template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
+__global__ __launch_bounds__(kBlock, GROUP ? 8 : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
@@ -1241,7 +1280,10 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitc
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;   // whole wave leaves together
     const NodeDesc& d = a.desc[item];
-    down_node<M, AP, SUB>(a, d, DENSE ? a.dense_base + item : d.node, (uint32_t)item, tile, lane, stage[wave]);
+    const int gen = !GROUP ? 0 : item >= a.split[1] ? 2 : item >= a.split[0] ? 1 : 0;
+    const int32_t first = gen == 0 ? 0 : a.split[gen - 1];
+    const int32_t n = !DENSE ? d.node : (GROUP ? a.dense_g[gen] : a.dense_base) + (item - first);
+    down_node<M, AP, SUB, GROUP>(a, d, n, (uint32_t)item, tile, lane, stage[wave], gen);
 }
 
 // Narrow pre-order levels (PM_OPT_NARROW; see k_fitch_up_band): levels [d0, d1) of the
@@ -1312,7 +1354,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
     kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
     // the parent's final, dirty lanes only (elsewhere the child emits nothing)
     const uint4* fsrc = proot ? a.root_final + word
-                              : ((pm.x >> lane) & 1ull) ? a.sets + prec * REC + kWave + lanes_below(pm.x)
+                              : ((pm.x >> lane) & 1ull) ? a.sets + prec * REC + final_slot(pm)
                               : ((pm.s >> lane) & 1ull) ? a.sets + prec * REC + lanes_below(pm.s) : a.cons + word;
     uint4 q = make_uint4(0, 0, 0, 0);
     if (dirty) q = *fsrc;

@@ -1,0 +1,85 @@
+"""PM_OPT_GROUP_*: two or three consecutive pre-order levels in one k_down launch, the lower
+levels' waves recomputing their ancestors' finals from the ancestors' intact sets and the
+last stored final, give exactly the records, scores and root codes of one launch per level
+-- and of the oracle."""
+import numpy as np
+import pytest
+
+import panman_amd
+from _trees import random_tree
+from test_gpu_fitch import _compare, _random_columns, _variant
+
+pytestmark = pytest.mark.gpu
+
+ALL = 1 << 40   # every level grouped
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = panman_amd.Engine(0)
+    yield e
+    e.close()
+
+
+def _run(engine, waves, narrow, levels=3):
+    engine.set_group(waves, levels)
+    engine.set_narrow(narrow)
+    engine.run(panman_amd.MODE_FITCH)
+    got = engine.mutations()
+    score, rootc = engine.site_results()
+    return got, score, rootc
+
+
+@pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
+@pytest.mark.parametrize("narrow", [0, 16])
+@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("tree", ["sars-like", "random-join"])
+def test_groups_equal_levels(engine, variant, narrow, levels, tree):
+    """T2 (deep ladder, polytomies) and T1 trees, with and without narrow bands between
+    the groups: identical records to one launch per level."""
+    if tree == "sars-like":
+        off, idx, root = panman_amd.sars_like_tree(5000, seed=21)
+    else:
+        off, idx, root = panman_amd.random_join_tree(6000, seed=22)
+    _variant(engine, variant)
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, 4500, seed=5)
+    try:
+        want = _run(engine, 0, 0)
+        got = _run(engine, ALL, narrow, levels)
+    finally:
+        engine.set_group(32768, 3)
+        engine.set_narrow(16)
+    assert want[0].shape[0] > 0
+    assert got[0].shape == want[0].shape and (got[0] == want[0]).all()
+    assert (got[1] == want[1]).all() and (got[2] == want[2]).all()
+
+
+@pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("levels", [2, 3])
+def test_groups_vs_oracle_absent_and_polytomies(engine, oracle, variant, seed, levels):
+    """Absent leaves (the non-AP kernels), unary nodes, polytomies, forced root; every
+    level grouped, no bands."""
+    rng = np.random.default_rng(5000 + seed)
+    off, idx, root = random_tree(500, rng, max_children=[2, 5, 9, 40][seed], unary=[0.0, 0.2, 0.0, 0.1][seed])
+    leaves = int((np.diff(off) == 0).sum())
+    sites = [97, 2049, 4100, 65][seed]
+    codes, present = _random_columns(rng, leaves, sites, absent_frac=[0.0, 0.1, 0.3, 0.0][seed])
+    cons = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=sites)
+    forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
+    engine.set_group(ALL, levels)
+    engine.set_narrow(0)
+    try:
+        _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant)
+    finally:
+        engine.set_group(32768, 3)
+        engine.set_narrow(16)
+
+
+def test_group_option_range(engine):
+    with pytest.raises(panman_amd.PanmanError):
+        engine.set_group(-1)
+    with pytest.raises(panman_amd.PanmanError):
+        engine.set_group(32768, 4)
+    engine.set_group(32768, 3)
