@@ -60,6 +60,8 @@ def parse():
                    help="Fitch: PM_OPT_GROUP_WAVES, most waves of grouped pre-order levels in one launch "
                         "(-1: library default, 0: off)")
     p.add_argument("--group-levels", type=int, default=3, help="Fitch: PM_OPT_GROUP_LEVELS (2 or 3)")
+    p.add_argument("--no-up-group", action="store_true",
+                   help="Fitch: post-order launches by height (PM_OPT_UP_GROUP off)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -117,6 +119,8 @@ def main():
         eng.set_subtree(False)
     if args.narrow >= 0:
         eng.set_narrow(args.narrow)
+    if args.no_up_group:
+        eng.set_up_group(False)
     if args.group >= 0 or args.group_levels != 3:
         eng.set_group(args.group if args.group >= 0 else 32768, args.group_levels)
 

@@ -100,6 +100,9 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  pre-order levels of at most this many (node, tile) waves together go to one
  *                  launch, the lower levels' waves recomputing their ancestors' finals; 0 = off.
  *   PM_OPT_GROUP_LEVELS (default 3): 2 or 3 levels per such launch.
+ *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
+ *                  latest children have out-degree <= 3 runs in their post-order launch,
+ *                  recomputing them, instead of one launch per height; 0 = by height.
  * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
  * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
@@ -108,6 +111,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_NARROW 7
 #define PM_OPT_GROUP_WAVES 8
 #define PM_OPT_GROUP_LEVELS 9
+#define PM_OPT_UP_GROUP 10
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

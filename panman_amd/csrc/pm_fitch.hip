@@ -34,9 +34,37 @@ namespace {
 #ifndef PM_SUB_UP_WAVES
 #define PM_SUB_UP_WAVES 4
 #endif
+// GROUP (grouped post-order launches, all leaves present): a child computed in this same
+// launch (descriptor cd, out-degree <= 3, its own children all from earlier launches): its
+// set as its own wave computes it (fitch_up_node), in registers, without the store.
+template <bool SUB>
+__device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc& cd, int tile, int lane, int64_t word,
+                                                uint32_t* x) {
+    uint32_t both[16], either[16], vd = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
+    const int4 vl0 = make_int4(cd.vl0[0], cd.vl0[1], cd.vl0[2], cd.vl0[3]), vl1 = make_int4(cd.vl1[0], cd.vl1[1], cd.vl1[2], cd.vl1[3]);
+    ChildFetch f0, f1;
+    fetch_child_ap<kFitchRec, false, SUB>(a, cd.c0, vl0, tile, lane, word, f0);
+    if (cd.e1 - cd.e0 > 1) fetch_child_ap<kFitchRec, false, SUB>(a, cd.c1, vl1, tile, lane, word, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    fold_child_ap<SUB>(cd.c0, vl0, f0, both, either, vd);
+    if (cd.e1 - cd.e0 > 1) fold_child_ap<SUB>(cd.c1, vl1, f1, both, either, vd);
+    for (int32_t e = cd.e0 + 2; e < cd.e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
+        fold_child<true>(a, c, vl, tile, lane, word, both, either, vd);
+    }
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = both[v] | (either[v] & ~nz);
+}
+
 // SUB: subtree form -- the first two children may also be S2 / S3 subtrees (three or four
 // leaves each, evaluated in registers: subtree_set_ap).
-template <bool AP, bool LEAFY, bool SUB = false>
+// GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
+// launch, recomputed here (child_recompute) instead of loaded.
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
 __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
@@ -46,7 +74,31 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
-    if constexpr (AP) {   // both children's loads in flight together
+    if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
+        static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
+        // the recomputed children first (while the accumulators are still one set), then
+        // the other of the first two children, loaded
+        uint32_t x0[16];
+        child_recompute<SUB>(a, a.desc_all[d.pad0 >= 0 ? d.pad0 : d.pad1], tile, lane, word, x0);
+        if (d.pad0 >= 0 && d.pad1 >= 0) {
+            uint32_t x1[16];
+            child_recompute<SUB>(a, a.desc_all[d.pad1], tile, lane, word, x1);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) { both[v] = x0[v] & x1[v]; either[v] = x0[v] | x1[v]; }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) { both[v] = x0[v]; either[v] = x0[v]; }
+            if (d.pad0 < 0 || e1 - e0 > 1) {
+                const bool first = d.pad0 < 0;   // the loaded one: slot 0 or slot 1
+                const int32_t c = first ? d.c0 : d.c1;
+                const int4 vl = first ? vl0 : vl1;
+                ChildFetch f;
+                fetch_child_ap<kFitchRec, false, SUB>(a, c, vl, tile, lane, word, f);
+                fold_child_ap<SUB>(c, vl, f, both, either, vd);
+            }
+        }
+        cw = a.cons[word];
+    } else if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;
         fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c0, vl0, tile, lane, word, f0);
         if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c1, vl1, tile, lane, word, f1);
@@ -105,14 +157,14 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
 #endif
 }
 
-template <bool AP, bool LEAFY, bool SUB = false>
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    fitch_up_node<AP, LEAFY, SUB>(a, a.desc[item], tile, lane);
+    fitch_up_node<AP, LEAFY, SUB, GROUP>(a, a.desc[item], tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
@@ -281,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
 // dependent ones: blocks [0, narrow_blocks) are k_fitch_up's (a wave per (node, tile) over
 // a.desc), the rest k_fitch_up_wide's (a workgroup per (wide node, tile) over wdesc).
 static_assert(PM_TILE_FAST, "k_fitch_up_mixed numbers its blocks on one grid axis");
-template <bool AP, bool SUB>
+template <bool AP, bool SUB, bool GROUP = false>
 __global__ __launch_bounds__(kBlock) void k_fitch_up_mixed(UpArgs a, const NodeDesc* wdesc, int32_t narrow_blocks) {
     __shared__ uint32_t part[kWavesPerBlock - 1][33][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -289,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_mixed(UpArgs a, const NodeD
         int32_t item;
         int tile;
         wave_item(wave, a.tiles, item, tile);
-        if (item < a.count) fitch_up_node<AP, false, SUB>(a, a.desc[item], tile, lane);
+        if (item < a.count) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[item], tile, lane);
         return;
     }
     const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
@@ -305,7 +357,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_mixed(UpArgs a, const NodeD
 // tile's records and masks are only touched by the waves of its own workgroup, so the
 // barrier's workgroup-scope release / acquire is all the synchronisation the hand-off needs;
 // what earlier launches wrote is visible at kernel start.
-template <bool AP, bool SUB>
+template <bool AP, bool SUB, bool GROUP = false>
 __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const int32_t* class_off, int32_t h0, int32_t h1) {
     __shared__ uint32_t acc[33][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -314,7 +366,7 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
     for (int32_t h = h0; h < h1; ++h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
                       e = class_off[(h + 1) * kDegreeClasses];
-        for (int32_t i = b + wave; i < m; i += kBandWaves) fitch_up_node<AP, false, SUB>(a, a.desc[i], tile, lane);
+        for (int32_t i = b + wave; i < m; i += kBandWaves) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[i], tile, lane);
         for (int32_t i = m; i < e; ++i) {   // out-degree > 3
             if (wave == 0) {
 #pragma unroll
@@ -397,9 +449,11 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const bool virt = !block && c->virtual_leaf_parents;
     const bool sub = virt && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
     const int32_t* child_enc = sub ? dt.child_enc_k : virt ? dt.child_enc_v : dt.child_enc;
-    const NodeDesc* up_desc = sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
+    // subtree form: grouped post-order launches (PM_OPT_UP_GROUP) or one launch per height
+    const bool grp = sub && c->up_group;
+    const NodeDesc* up_desc = grp ? dt.up_desc_g : sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
     const NodeDesc* down_desc = sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
-    const std::vector<int32_t>& up_off = sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off;
+    const std::vector<int32_t>& up_off = grp ? ht.up_level_off_g : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
 
     const bool ap = c->leaves_all_present;
@@ -419,8 +473,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
-    const std::vector<int32_t>& class_off = sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
-    const int form = sub ? 2 : virt ? 1 : 0;
+    const std::vector<int32_t>& class_off = grp ? ht.up_class_off_g : sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
+    const int form = sub ? 2 : virt ? 1 : 0;   // pre-order level tables (lvl_down)
+    const int up_form = grp ? 3 : form;        // post-order ones (lvl_up)
+    up.desc_all = up_desc;
     const int H = (int)up_off.size() - 1;
     // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
     auto narrow_up = [&](int h) {
@@ -434,9 +490,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             while (h1 < H && narrow_up(h1)) ++h1;
             if (h1 - h >= 2) {
                 up.desc = up_desc;
-                const int32_t* tab = dt.lvl + ht.lvl_up[form];
+                const int32_t* tab = dt.lvl + ht.lvl_up[up_form];
                 timer_begin(c, 0);
-                if (sub) hipLaunchKernelGGL((k_fitch_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                if (grp) hipLaunchKernelGGL((k_fitch_up_band<true, true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else if (sub) hipLaunchKernelGGL((k_fitch_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 else if (ap) hipLaunchKernelGGL((k_fitch_up_band<true, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 else hipLaunchKernelGGL((k_fitch_up_band<false, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 timer_end(c, 0);
@@ -453,7 +510,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             const int32_t nb = (int32_t)wave_grid(up.count, tiles).x;
             const dim3 grid((unsigned)(nb + (int64_t)(e - m) * tiles));
             timer_begin(c, 0);
-            if (sub) hipLaunchKernelGGL((k_fitch_up_mixed<true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+            if (grp) hipLaunchKernelGGL((k_fitch_up_mixed<true, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+            else if (sub) hipLaunchKernelGGL((k_fitch_up_mixed<true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
             else if (ap) hipLaunchKernelGGL((k_fitch_up_mixed<true, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
             else hipLaunchKernelGGL((k_fitch_up_mixed<false, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
             timer_end(c, 0);
@@ -463,9 +521,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             up.desc = up_desc + b;
             up.count = m - b;
             const dim3 grid = wave_grid(up.count, tiles);
-            const bool leafy = sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
+            const bool leafy = grp ? ht.up_leafy_g[h] : sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
             timer_begin(c, 0);
             if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (grp) hipLaunchKernelGGL((k_fitch_up<true, false, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);

@@ -74,6 +74,7 @@ void free_tree(DevTree& t) {
     dev_free(t.part_desc_v);
     dev_free(t.child_enc_k);
     dev_free(t.up_desc_k);
+    dev_free(t.up_desc_g);
     dev_free(t.down_desc_k);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
@@ -199,7 +200,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
-                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels,
+                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -386,6 +387,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_NARROW) {
         if (value < 0 || value > 1024) return fail(c, PM_ERR_ARG, "PM_OPT_NARROW: 0..1024 items per level");
         c->narrow_max = (int32_t)value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_UP_GROUP) {
+        c->up_group = value != 0;
         return PM_OK;
     }
     if (option == PM_OPT_GROUP_WAVES) {
@@ -769,6 +774,72 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const std::vector<NodeDesc> up_desc = make_desc(up_order, ht.child_enc);
     const std::vector<NodeDesc> up_desc_v = make_desc(up_order_v, child_enc_v);
     const std::vector<NodeDesc> up_desc_k = make_desc(up_order_k, child_enc_k);
+    // Grouped post-order launches of the subtree form (PM_OPT_UP_GROUP): a node of
+    // out-degree <= 3 joins the launch of its latest materialised children when each of
+    // those is of out-degree <= 3, computed from earlier launches only, and among its first
+    // two children -- its wave recomputes them in registers (k_fitch_up<.., GROUP>, the
+    // descriptor's pad0 / pad1 = their descriptor indices) -- otherwise the launch after.
+    // Children come before parents in up_order_k (height order).  Only nodes of heights
+    // with at most kUpGroupNodes nodes join a child's launch: big levels fill the chip by
+    // themselves and pay for the recomputation (measured at N*).
+    std::vector<NodeDesc> up_desc_g;
+    {
+        auto is_mat = [](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
+        auto narrow = [&](int32_t d) { return degree_class(ht.child_off[d + 1] - ht.child_off[d]) == 0; };
+        std::vector<int32_t> lv(I, -1), inl((size_t)I * 2, -1), hsize(I, 0);
+        for (size_t h = 0; h + 1 < ht.up_level_off_k.size(); ++h)
+            for (int32_t i = ht.up_level_off_k[h]; i < ht.up_level_off_k[h + 1]; ++i)
+                hsize[up_order_k[i]] = ht.up_level_off_k[h + 1] - ht.up_level_off_k[h];
+        std::vector<uint8_t> gen(I, 0);
+        int32_t G = 0;
+        for (int32_t d : up_order_k) {
+            int32_t M = -1;
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e)
+                if (is_mat(child_enc_k[e])) M = std::max(M, lv[child_enc_k[e]]);
+            if (M < 0) {
+                lv[d] = 0;
+            } else {
+                bool ok = narrow(d) && hsize[d] <= kUpGroupNodes;
+                for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1] && ok; ++e) {
+                    const int32_t x = child_enc_k[e];
+                    if (is_mat(x) && lv[x] == M) ok = !gen[x] && narrow(x) && e - ht.child_off[d] < 2;
+                }
+                lv[d] = ok ? M : M + 1;
+                gen[d] = ok;
+                if (ok)
+                    for (int32_t e = ht.child_off[d]; e < ht.child_off[d] + 2 && e < ht.child_off[d + 1]; ++e)
+                        if (is_mat(child_enc_k[e]) && lv[child_enc_k[e]] == M) inl[(size_t)d * 2 + (e - ht.child_off[d])] = child_enc_k[e];
+            }
+            G = std::max(G, lv[d] + 1);
+        }
+        // bucket by (launch, degree class), children-first order kept inside a bucket
+        ht.up_class_off_g.assign((size_t)G * kDegreeClasses + 1, 0);
+        auto key = [&](int32_t d) { return lv[d] * kDegreeClasses + degree_class(ht.child_off[d + 1] - ht.child_off[d]); };
+        for (int32_t d : up_order_k) ++ht.up_class_off_g[key(d) + 1];
+        for (size_t k = 0; k + 1 < ht.up_class_off_g.size(); ++k) ht.up_class_off_g[k + 1] += ht.up_class_off_g[k];
+        std::vector<int32_t> up_order_g(up_order_k.size()), cur(ht.up_class_off_g.begin(), ht.up_class_off_g.end() - 1),
+            pos(I, -1);
+        for (int32_t d : up_order_k) {
+            pos[d] = cur[key(d)]++;
+            up_order_g[pos[d]] = d;
+        }
+        ht.up_level_off_g.assign(G + 1, 0);
+        for (int32_t l = 0; l <= G; ++l) ht.up_level_off_g[l] = ht.up_class_off_g[(size_t)l * kDegreeClasses];
+        ht.up_leafy_g.assign(G, 0);
+        for (int32_t l = 0; l < G; ++l) {
+            bool leafy = true;
+            for (int32_t i = ht.up_class_off_g[(size_t)l * kDegreeClasses]; i < ht.up_class_off_g[(size_t)l * kDegreeClasses + 1] && leafy; ++i)
+                for (int32_t e = ht.child_off[up_order_g[i]]; e < ht.child_off[up_order_g[i] + 1]; ++e)
+                    leafy &= !is_mat(child_enc_k[e]);
+            ht.up_leafy_g[l] = leafy;
+        }
+        up_desc_g = make_desc(up_order_g, child_enc_k);
+        for (size_t k = 0; k < up_order_g.size(); ++k) {
+            const int32_t d = up_order_g[k];
+            up_desc_g[k].pad0 = inl[(size_t)d * 2] >= 0 ? pos[inl[(size_t)d * 2]] : -1;
+            up_desc_g[k].pad1 = inl[(size_t)d * 2 + 1] >= 0 ? pos[inl[(size_t)d * 2 + 1]] : -1;
+        }
+    }
     // subtree-form pre-order descriptors list only the children the level kernel handles:
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)
@@ -852,11 +923,12 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     upload_phase("parts");
     std::vector<int32_t> lvl;
     {
-        const std::vector<int32_t>* up[3] = {&ht.up_class_off, &ht.up_class_off_v, &ht.up_class_off_k};
+        const std::vector<int32_t>* up[4] = {&ht.up_class_off, &ht.up_class_off_v, &ht.up_class_off_k, &ht.up_class_off_g};
         const std::vector<int32_t>* dn[3] = {&ht.down_level_off, &ht.down_level_off_v, &ht.down_level_off_k};
-        for (int f = 0; f < 3; ++f) {
+        for (int f = 0; f < 4; ++f) {
             ht.lvl_up[f] = (int64_t)lvl.size();
             lvl.insert(lvl.end(), up[f]->begin(), up[f]->end());
+            if (f == 3) break;
             ht.lvl_down[f] = (int64_t)lvl.size();
             lvl.insert(lvl.end(), dn[f]->begin(), dn[f]->end());
         }
@@ -895,6 +967,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.child_enc_k, child_enc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.up_desc_k, up_desc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_g, up_desc_g, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess ||

@@ -33,6 +33,11 @@ constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole gra
 constexpr int kDegreeClasses = 4;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
                                   // complex, parent's simple, 3 pad (one 64-B scalar load)
+// Grouped post-order launches (PM_OPT_UP_GROUP): heights of at most this many nodes group.
+#ifndef PM_UP_GROUP_NODES
+#define PM_UP_GROUP_NODES 2048
+#endif
+constexpr int32_t kUpGroupNodes = PM_UP_GROUP_NODES;
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
@@ -102,6 +107,7 @@ struct DevTree {
     // subtree form (Fitch, all leaves present): S2 / S3 nodes inline in their parent too
     int32_t* child_enc_k = nullptr;   // [E] shapes in bits 28-29
     NodeDesc* up_desc_k = nullptr;
+    NodeDesc* up_desc_g = nullptr;     // grouped post-order launches of the subtree form
     NodeDesc* down_desc_k = nullptr;
     int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
@@ -143,12 +149,15 @@ struct HostTree {
     // subtree form: levels without the S2 / S3 nodes, each pre-order level's first dense index
     std::vector<int32_t> up_level_off_k, up_class_off_k, down_level_off_k, down_dense_base_k;
     std::vector<uint8_t> up_leafy_k;
+    // subtree form, grouped post-order launches (PM_OPT_UP_GROUP): launch l's nodes by class
+    std::vector<int32_t> up_level_off_g, up_class_off_g;
+    std::vector<uint8_t> up_leafy_g;
     bool down_dense_k = false;
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form
-    int64_t lvl_up[3] = {0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
+    int64_t lvl_up[4] = {0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
 };
 
 struct Timer {
@@ -174,6 +183,7 @@ struct pm_ctx {
     int32_t narrow_max = 16;          // Fitch: runs of levels this narrow go to one band launch (PM_OPT_NARROW)
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
     int32_t group_levels = 3;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
+    bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
 
     // column shard
     int64_t num_sites = 0;

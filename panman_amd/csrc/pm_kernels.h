@@ -67,6 +67,7 @@ constexpr int kBandBlock = kBandWaves * kWave;
 struct UpArgs {
     const int32_t* order;  // Sankoff: level items
     const NodeDesc* desc;  // level items
+    const NodeDesc* desc_all;  // grouped post-order launches: the whole descriptor array (pad0 / pad1 index it)
     const int4* vleaf;     // virtual node -> its (one or two) leaves, -1 padded
     int32_t count;
     const int32_t* child_off;

@@ -83,3 +83,32 @@ def test_group_option_range(engine):
     with pytest.raises(panman_amd.PanmanError):
         engine.set_group(32768, 4)
     engine.set_group(32768, 3)
+
+
+@pytest.mark.parametrize("narrow", [0, 16, 1024])
+@pytest.mark.parametrize("tree", ["sars-like", "random-join", "polytomy"])
+def test_up_groups_equal_heights(engine, narrow, tree):
+    """PM_OPT_UP_GROUP: post-order launches where nodes of out-degree <= 3 recompute their
+    same-launch children (subtree form) -- identical records to one launch per height, with
+    and without narrow bands over the grouped launches."""
+    if tree == "sars-like":
+        off, idx, root = panman_amd.sars_like_tree(6000, seed=31)
+    elif tree == "random-join":
+        off, idx, root = panman_amd.random_join_tree(6000, seed=32)
+    else:
+        off, idx, root = random_tree(3000, np.random.default_rng(33), max_children=4, unary=0.0)
+    _variant(engine, "virtual")
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, 4500, seed=6)
+    res = []
+    try:
+        for grp in (False, True):
+            engine.set_up_group(grp)
+            res.append(_run(engine, 32768, narrow))
+    finally:
+        engine.set_up_group(True)
+        engine.set_narrow(16)
+    (w, ws, wr), (g, gs, gr) = res
+    assert w.shape[0] > 0
+    assert g.shape == w.shape and (g == w).all()
+    assert (gs == ws).all() and (gr == wr).all()
