@@ -586,7 +586,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
                 // (subtree form: the lean body as in the level kernels, S2 / S3 records in k_tail)
                 if (block && ap) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (block) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                // (level groups inside the band when PM_OPT_GROUP_WAVES is on)
+                else if (ap && c->group_waves > 0) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (ap) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (c->group_waves > 0) hipLaunchKernelGGL((k_down_band<Mode::kFitch, false, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else hipLaunchKernelGGL((k_down_band<Mode::kFitch, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 timer_end(c, 1);
                 d = d1 - 1;

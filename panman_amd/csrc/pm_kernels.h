@@ -1291,18 +1291,24 @@ __global__ __launch_bounds__(kBlock, GROUP ? 8 : SUB ? PM_SUB_DOWN_WAVES : (M ==
 // level table `level_off` (descriptor ranges) walked by one launch, one 1024-thread workgroup
 // per tile, a workgroup barrier between levels.  `dense_base` (nullable): each level's first
 // dense index when the level is one dense range.
-template <Mode M, bool AP, bool SUB = false>
+// GROUP: kGroupLevels levels between barriers, the lower ones recomputing their ancestors'
+// finals (down_node's level groups).
+template <Mode M, bool AP, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBandBlock) void k_down_band(DownArgs a, const int32_t* level_off, const int32_t* dense_base,
                                                           int32_t d0, int32_t d1) {
     __shared__ pm_mut stage[kBandWaves][kStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
-    for (int32_t l = d0; l < d1; ++l) {
-        const int32_t b = level_off[l], e = level_off[l + 1];
-        const int32_t base = dense_base ? dense_base[l] : -1;
-        for (int32_t i = b + wave; i < e; i += kBandWaves) {
+    constexpr int G = GROUP ? kGroupLevels : 1;
+    for (int32_t l0 = d0; l0 < d1; l0 += G) {
+        const int32_t l1 = min(l0 + G, d1);
+        for (int32_t i = level_off[l0] + wave; i < level_off[l1]; i += kBandWaves) {
+            int32_t l = l0;
+            while (l + 1 < l1 && i >= level_off[l + 1]) ++l;
             const NodeDesc& d = a.desc[i];
-            down_node<M, AP, SUB>(a, d, base >= 0 ? base + (i - b) : d.node, (uint32_t)i, tile, lane, stage[wave]);
+            const int32_t base = dense_base ? dense_base[l] : -1;
+            down_node<M, AP, SUB, GROUP>(a, d, base >= 0 ? base + (i - level_off[l]) : d.node, (uint32_t)i, tile, lane,
+                                         stage[wave], l - l0);
         }
         __syncthreads();
     }
