@@ -1147,7 +1147,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
 #endif
 // One pre-order wave: node `n` (its descriptor d) x tile; `salt` spreads the waves over the
 // record shards; `stage` is the wave's LDS record stage (kStage records).
-// GROUP (Fitch modes): the launch holds up to kGroupLevels consecutive levels; a wave of
+// GROUP: the launch holds up to kGroupLevels consecutive levels; a wave of
 // the group's level g > 0 does not wait for its ancestors' finals to be stored -- it
 // recomputes them top down, each from the ancestor's set (intact: final_slot) and the final
 // above it, starting from the last final stored before the launch (descriptor: pad0 =
@@ -1156,7 +1156,6 @@ constexpr int kGroupLevels = 3;
 template <Mode M, bool AP, bool SUB, bool GROUP = false>
 __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, int32_t n, uint32_t salt, int tile,
                                           int lane, pm_mut* stage, int gen = 0) {
-    static_assert(!GROUP || M != Mode::kSankoff, "level groups: Fitch modes only");
     const int32_t parent = d.parent, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
@@ -1178,10 +1177,14 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
             const RecMask mv = rec_mask(a.cmask, vrec);   // its (x, s) and the final above's (px, ps)
             const bool vroot = k == 0 && above < 0;
             if (k == 0) q = vroot ? a.cons[word] : parent_final<REC>(a, above, mv, tile, lane, word);
-            SetFetch f;
-            fetch_fitch_set(a.sets + vrec * REC, mv, a.cons, lane, word, f);
             uint32_t vown[16], vz1[16], gc[4] = {q.x, q.y, q.z, q.w}, VF[4], vpres;
-            expand_fitch_set(f, vown);
+            if constexpr (M == Mode::kSankoff) {
+                load_sankoff(a.sets + vrec * REC, mv, a.cons, lane, word, vown, vz1, !vroot);
+            } else {
+                SetFetch f;
+                fetch_fitch_set(a.sets + vrec * REC, mv, a.cons, lane, word, f);
+                expand_fitch_set(f, vown);
+            }
             resolve_final<M>(a, vroot, word, vown, vz1, gc, VF, vpres);
             q = make_uint4(VF[0], VF[1], VF[2], VF[3]);
         }
@@ -1273,7 +1276,10 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
 // GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, split[2] =
 // count), dense from dense_g[g].
 template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
-__global__ __launch_bounds__(kBlock, GROUP ? 8 : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
+#ifndef PM_SK_GROUP_WAVES
+#define PM_SK_GROUP_WAVES 7
+#endif
+__global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;

@@ -561,7 +561,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
                 const int32_t* tab = dt.lvl + ht.lvl_down[virt ? 1 : 0];
                 const int32_t* base = dense_all ? tab : nullptr;
                 timer_begin(c, 1);
-                if (c->leaves_all_present) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                const bool grp = c->group_waves > 0;   // level groups inside the band
+                if (c->leaves_all_present && grp) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, true, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (c->leaves_all_present) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (grp) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, false, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else hipLaunchKernelGGL((k_down_band<Mode::kSankoff, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 timer_end(c, 1);
                 d = d1 - 1;
@@ -571,10 +574,37 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
-        const dim3 grid = wave_grid(dn.count, tiles);
-        timer_begin(c, 1);
         const bool dense = virt && ht.down_dense_v;   // level d = dense indices [down_off[d], down_off[d+1])
         dn.dense_base = dense ? down_off[d] : -1;
+        // levels d .. d + g - 1 in one launch (PM_OPT_GROUP_*; see launch_fitch)
+        auto narrow_down = [&](int l) { return c->narrow_max > 0 && down_off[l + 1] - down_off[l] <= c->narrow_max; };
+        auto band_at = [&](int l) { return narrow_down(l) && l + 1 < D && narrow_down(l + 1); };
+        int g = 1;
+        int64_t items = dn.count;
+        while (c->group_waves > 0 && g < std::min(c->group_levels, kGroupLevels) && d + g < D) {
+            const int32_t ng = down_off[d + g + 1] - down_off[d + g];
+            if (ng == 0 || (items + ng) * tiles > c->group_waves || band_at(d + g)) break;
+            items += ng;
+            ++g;
+        }
+        if (g > 1) {
+            for (int k = 0; k < kGroupLevels; ++k) {
+                const int l = std::min(d + k, d + g - 1);
+                if (k > 0) dn.split[k - 1] = k < g ? down_off[d + k] - down_off[d] : (int32_t)items;
+                dn.dense_g[k] = dense ? down_off[l] : -1;
+            }
+            dn.count = (int32_t)items;
+            const dim3 grid = wave_grid(dn.count, tiles);
+            timer_begin(c, 1);
+            if (c->leaves_all_present && dense) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, true, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else hipLaunchKernelGGL((k_down<Mode::kSankoff, false, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            timer_end(c, 1);
+            d += g - 1;
+            continue;
+        }
+        const dim3 grid = wave_grid(dn.count, tiles);
+        timer_begin(c, 1);
         if (c->leaves_all_present && dense) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (c->leaves_all_present) hipLaunchKernelGGL((k_down<Mode::kSankoff, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else hipLaunchKernelGGL((k_down<Mode::kSankoff, false, false>), grid, dim3(kBlock), 0, c->stream, dn);

@@ -112,3 +112,41 @@ def test_up_groups_equal_heights(engine, narrow, tree):
     assert w.shape[0] > 0
     assert g.shape == w.shape and (g == w).all()
     assert (gs == ws).all() and (gr == wr).all()
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_SANKOFF, panman_amd.MODE_BLOCK_SANKOFF])
+@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("narrow", [0, 16])
+def test_sankoff_groups_equal_levels(engine, mode, levels, narrow):
+    """Sankoff pre-order level groups (Z0 / Z1 of the ancestors recomputed), in level launches
+    and inside bands: identical records to one launch per level."""
+    rng = np.random.default_rng(90 + levels)
+    off, idx, root = panman_amd.sars_like_tree(4000, seed=41) if mode == panman_amd.MODE_SANKOFF else \
+        random_tree(600, rng, max_children=5, unary=0.1)
+    engine.tree_upload(off, idx, root)
+    if mode == panman_amd.MODE_SANKOFF:
+        engine.synth_columns(0, 3000, seed=7)
+    else:
+        n = off.shape[0] - 1
+        leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
+        node_row = np.full(n, -1, np.int32)
+        for r, lid in enumerate(leaf_ids):
+            if rng.random() > 0.2:
+                node_row[lid] = r
+        engine.leaves_upload(rng.choice(np.array([0, 1, 1, 1, 2], np.uint8), size=(len(leaf_ids), 400)), node_row)
+        engine.sites_upload(np.zeros(400, np.uint8), rng.integers(0, 3, size=400).astype(np.uint8))
+    res = []
+    try:
+        for waves in (0, ALL):
+            engine.set_group(waves, levels)
+            engine.set_narrow(narrow)
+            engine.run(mode)
+            recs = engine.mutations() if mode == panman_amd.MODE_SANKOFF else engine.block_mutations()
+            res.append((recs,) + tuple(engine.site_results()))
+    finally:
+        engine.set_group(32768, 3)
+        engine.set_narrow(16)
+    (w, ws, wr), (g, gs, gr) = res
+    assert w.shape[0] > 0
+    assert g.shape == w.shape and (g == w).all()
+    assert (gs == ws).all() and (gr == wr).all()
