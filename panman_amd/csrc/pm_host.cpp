@@ -800,12 +800,18 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 lv[d] = 0;
             } else {
                 bool ok = narrow(d) && hsize[d] <= kUpGroupNodes;
+                int top = 0, g = 0;   // children in launch M, the deepest recomputation below them
                 for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1] && ok; ++e) {
                     const int32_t x = child_enc_k[e];
-                    if (is_mat(x) && lv[x] == M) ok = !gen[x] && narrow(x) && e - ht.child_off[d] < 2;
+                    if (is_mat(x) && lv[x] == M) {
+                        ok = narrow(x) && e - ht.child_off[d] < 2 && gen[x] < kUpGroupDepth;
+                        ++top;
+                        g = std::max(g, (int)gen[x]);
+                    }
                 }
+                ok = ok && (g == 0 || top == 1);   // a chain below: one recomputed child only
                 lv[d] = ok ? M : M + 1;
-                gen[d] = ok;
+                gen[d] = ok ? (uint8_t)(g + 1) : 0;
                 if (ok)
                     for (int32_t e = ht.child_off[d]; e < ht.child_off[d] + 2 && e < ht.child_off[d + 1]; ++e)
                         if (is_mat(child_enc_k[e]) && lv[child_enc_k[e]] == M) inl[(size_t)d * 2 + (e - ht.child_off[d])] = child_enc_k[e];

@@ -38,6 +38,12 @@ constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, sim
 #define PM_UP_GROUP_NODES 2048
 #endif
 constexpr int32_t kUpGroupNodes = PM_UP_GROUP_NODES;
+// ... and a node recomputes same-launch descendants at most this many levels down (a node
+// recomputing a child that itself recomputes one: depth 2; such a chain holds one child per level).
+#ifndef PM_UP_GROUP_DEPTH
+#define PM_UP_GROUP_DEPTH 2
+#endif
+constexpr int kUpGroupDepth = PM_UP_GROUP_DEPTH;
 inline int degree_class(int32_t deg) { return deg <= 3 ? 0 : deg <= 15 ? 1 : deg <= 255 ? 2 : 3; }
 
 enum LeafFlag : uint8_t { kLeafAbsent = 0, kLeafPresent = 1, kLeafPartial = 2 };
