@@ -99,7 +99,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_GROUP_WAVES (default 32768): Fitch -- up to PM_OPT_GROUP_LEVELS consecutive
  *                  pre-order levels of at most this many (node, tile) waves together go to one
  *                  launch, the lower levels' waves recomputing their ancestors' finals; 0 = off.
- *   PM_OPT_GROUP_LEVELS (default 3): 2 or 3 levels per such launch.
+ *   PM_OPT_GROUP_LEVELS (default 4): 2 to 4 levels per such launch.
  *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
  *                  latest children have out-degree <= 3 runs in their post-order launch,
  *                  recomputing them, instead of one launch per height; 0 = by height.

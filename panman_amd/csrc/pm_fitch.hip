@@ -631,7 +631,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             ++g;
         }
         if (g > 1) {
-            for (int k = 0; k < kGroupLevels; ++k) {
+            for (int k = 0; k < 4; ++k) {
                 const int l = std::min(d + k, d + g - 1);
                 if (k > 0) dn.split[k - 1] = k < g ? down_off[d + k] - down_off[d] : (int32_t)items;
                 dn.dense_g[k] = !dense ? -1 : sub ? ht.down_dense_base_k[l] : down_off[l];

@@ -399,7 +399,7 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         return PM_OK;
     }
     if (option == PM_OPT_GROUP_LEVELS) {
-        if (value < 2 || value > 3) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_LEVELS: 2 or 3");
+        if (value < 2 || value > 4) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_LEVELS: 2 to 4");
         c->group_levels = (int32_t)value;
         return PM_OK;
     }

@@ -188,7 +188,7 @@ struct pm_ctx {
     bool subtree_form = true;         // Fitch, all leaves present: S2 / S3 inline too (PM_OPT_SUBTREE)
     int32_t narrow_max = 16;          // Fitch: runs of levels this narrow go to one band launch (PM_OPT_NARROW)
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
-    int32_t group_levels = 3;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
+    int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
 
     // column shard

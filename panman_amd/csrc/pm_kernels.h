@@ -614,8 +614,8 @@ struct DownArgs {
     const uint64_t* cmask;
     uint4* root_final;     // [W] the root's final codes (a forced root's differ from its set)
     int32_t dense_base;    // k_down<.., DENSE>: the level's first dense index (item k = dense base + k)
-    int32_t split[2];      // k_down<.., GROUP>: the first items of the group's levels 1 and 2
-    int32_t dense_g[3];    // k_down<.., DENSE, .., GROUP>: each level's first dense index
+    int32_t split[3];      // k_down<.., GROUP>: the first items of the group's levels 1, 2, 3
+    int32_t dense_g[4];    // k_down<.., DENSE, .., GROUP>: each level's first dense index
     const uint4* cons;
     int32_t root_dense;
     int32_t tiles;
@@ -1151,8 +1151,13 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
 // the group's level g > 0 does not wait for its ancestors' finals to be stored -- it
 // recomputes them top down, each from the ancestor's set (intact: final_slot) and the final
 // above it, starting from the last final stored before the launch (descriptor: pad0 =
-// grandparent, pad1 = great-grandparent), so g + 1 levels cost one launch.
-constexpr int kGroupLevels = 3;
+// grandparent, pad1 = great-grandparent; the fourth level's top ancestor's parent is one
+// scalar load beside the mask loads), so g + 1 levels cost one launch.
+#ifndef PM_GROUP_LEVELS
+#define PM_GROUP_LEVELS 4
+#endif
+constexpr int kGroupLevels = PM_GROUP_LEVELS;
+static_assert(kGroupLevels >= 2 && kGroupLevels <= 4, "level groups: 2 to 4 levels");
 template <Mode M, bool AP, bool SUB, bool GROUP = false>
 __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, int32_t n, uint32_t salt, int tile,
                                           int lane, pm_mut* stage, int gen = 0) {
@@ -1167,12 +1172,13 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     uint4* const p = a.sets + rec * REC;
     uint32_t own[16], pc[4], F[4];
     if (GROUP && gen > 0) {
-        // ancestors inside the group, top first: chain[0 .. gen-1], chain[gen-1] = parent
-        const int32_t chain[2] = {gen == 2 ? d.pad0 : parent, parent};
-        const int32_t above = gen == 2 ? d.pad1 : d.pad0;   // its final is stored (-1: chain[0] is the root)
+        // ancestors inside the group, top first: chain[3 - gen .. 2], chain[2] = parent
+        const int32_t chain[3] = {d.pad1, d.pad0, parent};
+        // the top one's parent, whose final is stored (-1: the top one is the root)
+        const int32_t above = gen == 1 ? d.pad0 : gen == 2 ? d.pad1 : d.pad1 >= 0 ? a.parent_dense[d.pad1] : -1;
         uint4 q;
         for (int k = 0; k < gen; ++k) {
-            const int32_t v = chain[k + 2 - gen];
+            const int32_t v = chain[k + 3 - gen];
             const size_t vrec = (size_t)v * a.tiles + tile;
             const RecMask mv = rec_mask(a.cmask, vrec);   // its (x, s) and the final above's (px, ps)
             const bool vroot = k == 0 && above < 0;
@@ -1273,8 +1279,8 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
 }
 
-// GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, split[2] =
-// count), dense from dense_g[g].
+// GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, unused
+// splits = count), dense from dense_g[g].
 template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
 #ifndef PM_SK_GROUP_WAVES
 #define PM_SK_GROUP_WAVES 7
@@ -1287,7 +1293,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;   // whole wave leaves together
     const NodeDesc& d = a.desc[item];
-    const int gen = !GROUP ? 0 : item >= a.split[1] ? 2 : item >= a.split[0] ? 1 : 0;
+    const int gen = !GROUP ? 0 : (item >= a.split[0]) + (item >= a.split[1]) + (item >= a.split[2]);
     const int32_t first = gen == 0 ? 0 : a.split[gen - 1];
     const int32_t n = !DENSE ? d.node : (GROUP ? a.dense_g[gen] : a.dense_base) + (item - first);
     down_node<M, AP, SUB, GROUP>(a, d, n, (uint32_t)item, tile, lane, stage[wave], gen);

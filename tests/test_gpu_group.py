@@ -1,4 +1,4 @@
-"""PM_OPT_GROUP_*: two or three consecutive pre-order levels in one k_down launch, the lower
+"""PM_OPT_GROUP_*: two to four consecutive pre-order levels in one k_down launch, the lower
 levels' waves recomputing their ancestors' finals from the ancestors' intact sets and the
 last stored final, give exactly the records, scores and root codes of one launch per level
 -- and of the oracle."""
@@ -21,7 +21,7 @@ def engine():
     e.close()
 
 
-def _run(engine, waves, narrow, levels=3):
+def _run(engine, waves, narrow, levels=4):
     engine.set_group(waves, levels)
     engine.set_narrow(narrow)
     engine.run(panman_amd.MODE_FITCH)
@@ -32,7 +32,7 @@ def _run(engine, waves, narrow, levels=3):
 
 @pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
 @pytest.mark.parametrize("narrow", [0, 16])
-@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("levels", [2, 3, 4])
 @pytest.mark.parametrize("tree", ["sars-like", "random-join"])
 def test_groups_equal_levels(engine, variant, narrow, levels, tree):
     """T2 (deep ladder, polytomies) and T1 trees, with and without narrow bands between
@@ -48,7 +48,7 @@ def test_groups_equal_levels(engine, variant, narrow, levels, tree):
         want = _run(engine, 0, 0)
         got = _run(engine, ALL, narrow, levels)
     finally:
-        engine.set_group(32768, 3)
+        engine.set_group(32768, 4)
         engine.set_narrow(16)
     assert want[0].shape[0] > 0
     assert got[0].shape == want[0].shape and (got[0] == want[0]).all()
@@ -57,7 +57,7 @@ def test_groups_equal_levels(engine, variant, narrow, levels, tree):
 
 @pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
 @pytest.mark.parametrize("seed", range(4))
-@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("levels", [2, 3, 4])
 def test_groups_vs_oracle_absent_and_polytomies(engine, oracle, variant, seed, levels):
     """Absent leaves (the non-AP kernels), unary nodes, polytomies, forced root; every
     level grouped, no bands."""
@@ -73,7 +73,7 @@ def test_groups_vs_oracle_absent_and_polytomies(engine, oracle, variant, seed, l
     try:
         _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant)
     finally:
-        engine.set_group(32768, 3)
+        engine.set_group(32768, 4)
         engine.set_narrow(16)
 
 
@@ -81,8 +81,8 @@ def test_group_option_range(engine):
     with pytest.raises(panman_amd.PanmanError):
         engine.set_group(-1)
     with pytest.raises(panman_amd.PanmanError):
-        engine.set_group(32768, 4)
-    engine.set_group(32768, 3)
+        engine.set_group(32768, 5)
+    engine.set_group(32768, 4)
 
 
 @pytest.mark.parametrize("narrow", [0, 16, 1024])
@@ -115,7 +115,7 @@ def test_up_groups_equal_heights(engine, narrow, tree):
 
 
 @pytest.mark.parametrize("mode", [panman_amd.MODE_SANKOFF, panman_amd.MODE_BLOCK_SANKOFF])
-@pytest.mark.parametrize("levels", [2, 3])
+@pytest.mark.parametrize("levels", [2, 3, 4])
 @pytest.mark.parametrize("narrow", [0, 16])
 def test_sankoff_groups_equal_levels(engine, mode, levels, narrow):
     """Sankoff pre-order level groups (Z0 / Z1 of the ancestors recomputed), in level launches
@@ -144,7 +144,7 @@ def test_sankoff_groups_equal_levels(engine, mode, levels, narrow):
             recs = engine.mutations() if mode == panman_amd.MODE_SANKOFF else engine.block_mutations()
             res.append((recs,) + tuple(engine.site_results()))
     finally:
-        engine.set_group(32768, 3)
+        engine.set_group(32768, 4)
         engine.set_narrow(16)
     (w, ws, wr), (g, gs, gr) = res
     assert w.shape[0] > 0
