@@ -533,6 +533,28 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             timer_end(c, 0);
             continue;
         }
+        // a level's narrow and wide nodes are independent: the wide launch runs beside the
+        // narrow one on the side stream (parallel graph branches) instead of after it
+#ifdef PM_NO_SIDE
+        const bool fork = false;
+#else
+        const bool fork = m > b && e > m;
+#endif
+        if (fork) {
+            const hipError_t fe = side_fork(c);
+            if (fe != hipSuccess) return fe;
+        }
+        if (e > m) {
+            UpArgs w = up;
+            w.desc = up_desc + m;
+            w.count = e - m;
+            const dim3 grid = block_grid(w.count, tiles);
+            hipStream_t s = fork ? c->side : c->stream;
+            if (!fork) timer_begin(c, 0);
+            if (ap) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, s, w);
+            else hipLaunchKernelGGL(k_fitch_up_wide<false>, grid, dim3(kBlock), 0, s, w);
+            if (!fork) timer_end(c, 0);
+        }
         if (m > b) {
             up.desc = up_desc + b;
             up.count = m - b;
@@ -545,15 +567,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             else if (ap && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL((k_fitch_up<false, false>), grid, dim3(kBlock), 0, c->stream, up);
-            timer_end(c, 0);
-        }
-        if (e > m) {
-            up.desc = up_desc + m;
-            up.count = e - m;
-            const dim3 grid = block_grid(up.count, tiles);
-            timer_begin(c, 0);
-            if (ap) hipLaunchKernelGGL(k_fitch_up_wide<true>, grid, dim3(kBlock), 0, c->stream, up);
-            else hipLaunchKernelGGL(k_fitch_up_wide<false>, grid, dim3(kBlock), 0, c->stream, up);
+            if (fork) {
+                const hipError_t je = side_join(c);
+                if (je != hipSuccess) return je;
+            }
             timer_end(c, 0);
         }
     }

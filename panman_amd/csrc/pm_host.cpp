@@ -275,6 +275,16 @@ int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
 
 }  // namespace
 
+hipError_t side_fork(pm_ctx* c) {
+    hipError_t e = hipEventRecord(c->ev_fork, c->stream);
+    return e == hipSuccess ? hipStreamWaitEvent(c->side, c->ev_fork, 0) : e;
+}
+
+hipError_t side_join(pm_ctx* c) {
+    hipError_t e = hipEventRecord(c->ev_join, c->side);
+    return e == hipSuccess ? hipStreamWaitEvent(c->stream, c->ev_join, 0) : e;
+}
+
 void timer_begin(pm_ctx* c, int cls) {
     if (!c->profiling) return;
     auto& v = c->timers[cls];
@@ -339,7 +349,13 @@ int pm_create(int device, pm_ctx** out) {
     if ((e = hipSetDevice(device)) != hipSuccess) return PM_ERR_HIP;
     pm_ctx* c = new pm_ctx();
     c->device = device;
-    if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) {
+        if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+        if (c->side) (void)hipStreamDestroy(c->side);
+        if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
         delete c;
         return PM_ERR_HIP;
     }
@@ -362,6 +378,10 @@ void pm_destroy(pm_ctx* c) {
             (void)hipEventDestroy(t.a);
             (void)hipEventDestroy(t.b);
         }
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -178,6 +178,9 @@ struct pm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    // a second stream for independent launches of one level (side_fork / side_join)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
 
     pm::HostTree ht;
@@ -248,6 +251,10 @@ namespace pm {
 int fail(pm_ctx* c, int code, const std::string& msg);
 int hip_fail(pm_ctx* c, hipError_t e, const char* what);
 
+// Work queued on c->side between side_fork and side_join runs concurrently with the work
+// queued on c->stream meanwhile (in a captured graph: parallel branches).
+hipError_t side_fork(pm_ctx* c);
+hipError_t side_join(pm_ctx* c);
 void timer_begin(pm_ctx* c, int cls);
 void timer_end(pm_ctx* c, int cls);
 
