@@ -441,7 +441,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.tiles = tiles;
     up.wpad = wpad;
     // nodes [b, e) of one level with more than 255 children: parts, then the merge
-    auto launch_parts = [&](int32_t b, int32_t e) {
+    auto launch_parts = [&](int32_t b, int32_t e, hipStream_t s) {
         const int32_t p0 = part_off[b], np = part_off[e] - p0;
         int32_t widest = 0;
         for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[virt][i]);
@@ -452,9 +452,9 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         mg.count = e - b;
         const dim3 grid = wave_grid(mg.count, tiles);
         timer_begin(c, 0);
-        hipLaunchKernelGGL(k_sankoff_part, wave_grid(np, tiles), dim3(kBlock), 0, c->stream, pa, parts + p0, np, c->sk_parts);
-        if (widest < (1 << 16)) hipLaunchKernelGGL(k_sankoff_merge<16>, grid, dim3(kBlock), 0, c->stream, mg, c->sk_parts);
-        else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, c->stream, mg, c->sk_parts);
+        hipLaunchKernelGGL(k_sankoff_part, wave_grid(np, tiles), dim3(kBlock), 0, s, pa, parts + p0, np, c->sk_parts);
+        if (widest < (1 << 16)) hipLaunchKernelGGL(k_sankoff_merge<16>, grid, dim3(kBlock), 0, s, mg, c->sk_parts);
+        else hipLaunchKernelGGL(k_sankoff_merge<32>, grid, dim3(kBlock), 0, s, mg, c->sk_parts);
         timer_end(c, 0);
     };
     // runs of >= 2 narrow levels with only out-degree <= 3 nodes (PM_OPT_NARROW): one band each
@@ -495,29 +495,43 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
                 // the level's nodes above 255 children (if any) still go to the parts below
                 for (int k = 3; k < kDegreeClasses; ++k) {
                     const int32_t pb = class_off[h * kDegreeClasses + k], pe = class_off[h * kDegreeClasses + k + 1];
-                    if (pe > pb) launch_parts(pb, pe);
+                    if (pe > pb) launch_parts(pb, pe, c->stream);
                 }
                 continue;
             }
         }
-        for (int k = 0; k < kDegreeClasses; ++k) {
+        // the level's degree classes are independent: the wide ones run on the side stream,
+        // beside the narrow launch (parallel graph branches), when both kinds are present
+        const int32_t lb = class_off[h * kDegreeClasses], lm = class_off[h * kDegreeClasses + 1],
+                      le = class_off[(h + 1) * kDegreeClasses];
+        const bool fork = lm > lb && le > lm;
+        if (fork) {
+            const hipError_t fe = side_fork(c);
+            if (fe != hipSuccess) return fe;
+        }
+        for (int k = kDegreeClasses - 1; k >= 0; --k) {   // wide classes first: they go to the side
             const int32_t b = class_off[h * kDegreeClasses + k];
             const int32_t e = class_off[h * kDegreeClasses + k + 1];
             if (e == b) continue;
+            hipStream_t s = fork && k > 0 ? c->side : c->stream;
             up.desc = up_desc + b;
             up.count = e - b;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, c->stream, up);
-            else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, c->stream, up);
+            if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, s, up);
+            else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, s, up);
+            else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, s, up);
+            else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, s, up);
             else {   // more than 255 children: parts, then the merge
                 timer_end(c, 0);
-                launch_parts(b, e);
+                launch_parts(b, e, s);
                 continue;
             }
             timer_end(c, 0);
+        }
+        if (fork) {
+            const hipError_t je = side_join(c);
+            if (je != hipSuccess) return je;
         }
     }
 
