@@ -60,6 +60,9 @@ def parse():
                    help="Fitch: PM_OPT_GROUP_WAVES, most waves of grouped pre-order levels in one launch "
                         "(-1: library default, 0: off)")
     p.add_argument("--group-levels", type=int, default=4, help="PM_OPT_GROUP_LEVELS (2 to 4)")
+    p.add_argument("--tail-chunk", type=int, default=-1,
+                   help="PM_OPT_TAIL_OVERLAP: tail chunks of >= this many waves beside the pre-order "
+                        "levels (-1: library default, 0: after the last level)")
     p.add_argument("--no-up-group", action="store_true",
                    help="Fitch: post-order launches by height (PM_OPT_UP_GROUP off)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
@@ -119,6 +122,8 @@ def main():
         eng.set_subtree(False)
     if args.narrow >= 0:
         eng.set_narrow(args.narrow)
+    if args.tail_chunk >= 0:
+        eng.set_tail_overlap(args.tail_chunk)
     if args.no_up_group:
         eng.set_up_group(False)
     if args.group >= 0 or args.group_levels != 4:

@@ -103,6 +103,11 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
  *                  latest children have out-degree <= 3 runs in their post-order launch,
  *                  recomputing them, instead of one launch per height; 0 = by height.
+ *   PM_OPT_TAIL_OVERLAP (default 0): the records of children beyond a node's second (and
+ *                  of inline subtrees) start on a second stream, in chunks of at least this
+ *                  many (item, tile) waves, as soon as their parents' pre-order level is
+ *                  done, beside the remaining levels; 0 = after the last level (measured: no gain
+ *                  at N*, C2 or C3 -- the levels already occupy the chip).
  * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
  * were measured slower than the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
@@ -112,6 +117,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_GROUP_WAVES 8
 #define PM_OPT_GROUP_LEVELS 9
 #define PM_OPT_UP_GROUP 10
+#define PM_OPT_TAIL_OVERLAP 11
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

@@ -606,7 +606,49 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
+    // The tail (children beyond the second, S2 / S3 subtrees) needs only its parents' finals:
+    // items whose parent's level is done start on the side stream, beside the remaining
+    // levels, in chunks of >= tail_chunk waves (not when profiling: the class timers time the
+    // main stream).
+    const TailDesc* tail_desc = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
+    int32_t tail_total = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
+#ifdef PM_EXP_NOTAIL   // timing experiment: no tail launch
+    tail_total = 0;
+#endif
+    const std::vector<int32_t>& tail_off = ht.tail_lvl_off[form];
+    const bool tail_side = !c->profiling && c->tail_chunk > 0;
+    int32_t tail_done = 0;
+    bool tail_forked = false;
+    auto tail_flush = [&](int level_end, bool last) -> hipError_t {
+        const int32_t upto = last ? tail_total : std::min(tail_total, tail_off[level_end]);
+        if (upto <= tail_done || (!last && (!tail_side || (int64_t)(upto - tail_done) * tiles < c->tail_chunk)))
+            return hipSuccess;
+        hipStream_t s = c->stream;
+        if (tail_side) {
+            const hipError_t fe = side_fork(c);
+            if (fe != hipSuccess) return fe;
+            s = c->side;
+            tail_forked = true;
+        }
+        DownArgs t = dn;
+        t.tail = tail_desc + tail_done;
+        t.count = upto - tail_done;
+        tail_done = upto;
+        const dim3 grid = wave_grid(t.count, tiles);
+        if (!tail_side) timer_begin(c, 1);
+        if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, s, t);
+        else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, s, t);
+        else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, s, t);
+        else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, s, t);
+        else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, s, t);
+        if (!tail_side) timer_end(c, 1);
+        return hipSuccess;
+    };
     for (int d = 0; d < D; ++d) {
+        {
+            const hipError_t te = tail_flush(d, false);
+            if (te != hipSuccess) return te;
+        }
         if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {
             int d1 = d + 1;
             while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
@@ -674,21 +716,9 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
-    dn.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
-    dn.count = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
-#ifdef PM_EXP_NOTAIL   // timing experiment: no tail launch
-    dn.count = 0;
-#endif
-    if (dn.count > 0) {
-        const dim3 grid = wave_grid(dn.count, tiles);
-        timer_begin(c, 1);
-        if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
-        else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, dn);
-        else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, dn);
-        timer_end(c, 1);
-    }
+    hipError_t te = tail_flush(D, true);
+    if (te == hipSuccess && tail_forked) te = side_join(c);
+    if (te != hipSuccess) return te;
     return hipGetLastError();
 }
 

@@ -200,7 +200,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
-                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
+                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group, (uint64_t)c->tail_chunk,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -407,6 +407,11 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_NARROW) {
         if (value < 0 || value > 1024) return fail(c, PM_ERR_ARG, "PM_OPT_NARROW: 0..1024 items per level");
         c->narrow_max = (int32_t)value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_TAIL_OVERLAP) {
+        if (value < 0) return fail(c, PM_ERR_ARG, "PM_OPT_TAIL_OVERLAP: >= 0 waves");
+        c->tail_chunk = value;
         return PM_OK;
     }
     if (option == PM_OPT_UP_GROUP) {
@@ -909,8 +914,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         return tail;
     };
     upload_phase("descriptors");
-    const std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
-    const std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
+    std::vector<TailDesc> tail_desc = make_tail(down_order, ht.child_enc);
+    std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
     ht.num_tail_v = (int32_t)tail_desc_v.size();
     std::vector<TailDesc> tail_desc_k = tail_desc_v;   // + every S2 / S3 node, its parent's final read back
@@ -927,6 +932,25 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         tail_desc_k.push_back(t);
     }
     ht.num_tail_k = (int32_t)tail_desc_k.size();
+    // tail items by their parent's pre-order level (the subtree form's levels are the leaf-
+    // parent form's, S2 / S3 nodes removed), with per-level offsets: the launcher starts the
+    // items of finished levels beside the remaining levels (side stream)
+    {
+        auto by_level = [&](std::vector<TailDesc>& tail, const std::vector<int32_t>& order,
+                            const std::vector<int32_t>& offs, std::vector<int32_t>& tail_off) {
+            std::vector<int32_t> lvl_of(I, 0);
+            for (size_t l = 0; l + 1 < offs.size(); ++l)
+                for (int32_t i = offs[l]; i < offs[l + 1]; ++i) lvl_of[order[i]] = (int32_t)l;
+            std::stable_sort(tail.begin(), tail.end(),
+                             [&](const TailDesc& x, const TailDesc& y) { return lvl_of[x.parent] < lvl_of[y.parent]; });
+            tail_off.assign(offs.size(), 0);
+            for (const TailDesc& t : tail) ++tail_off[lvl_of[t.parent] + 1];
+            for (size_t l = 0; l + 1 < tail_off.size(); ++l) tail_off[l + 1] += tail_off[l];
+        };
+        by_level(tail_desc, down_order, ht.down_level_off, ht.tail_lvl_off[0]);
+        by_level(tail_desc_v, down_order_v, ht.down_level_off_v, ht.tail_lvl_off[1]);
+        by_level(tail_desc_k, down_order_v, ht.down_level_off_v, ht.tail_lvl_off[2]);
+    }
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
     std::vector<PartDesc> part_desc[2];

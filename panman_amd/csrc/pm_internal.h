@@ -38,6 +38,7 @@ constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, sim
 #define PM_UP_GROUP_NODES 2048
 #endif
 constexpr int32_t kUpGroupNodes = PM_UP_GROUP_NODES;
+
 // ... and a node recomputes same-launch descendants at most this many levels down (a node
 // recomputing a child that itself recomputes one: depth 2; such a chain holds one child per level).
 #ifndef PM_UP_GROUP_DEPTH
@@ -162,6 +163,7 @@ struct HostTree {
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
+    std::vector<int32_t> tail_lvl_off[3];   // per form: tail items whose parent's pre-order level is < l
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form
     int64_t lvl_up[4] = {0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
 };
@@ -193,6 +195,7 @@ struct pm_ctx {
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
+    int64_t tail_chunk = 0;           // tail chunks of >= this many waves beside the remaining pre-order levels, 0 = off (PM_OPT_TAIL_OVERLAP)
 
     // column shard
     int64_t num_sites = 0;
