@@ -1352,8 +1352,11 @@ __device__ __forceinline__ void tail_put(const TailDesc& t, const Sink& sink, ui
     if (k.vl.y >= 0) put_records(sink, p, (uint32_t)t.id[2], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
 }
 
+#ifndef PM_TAIL_WAVES
+#define PM_TAIL_WAVES 6
+#endif
 template <Mode M, bool AP, bool SUB = false>
-__global__ __launch_bounds__(kBlock) void k_tail(DownArgs a) {
+__global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;

@@ -126,8 +126,11 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
+#ifndef PM_SK_UP_WAVES
+#define PM_SK_UP_WAVES 1
+#endif
 template <int B, bool AP>
-__global__ __launch_bounds__(kBlock) void k_sankoff_up(UpArgs a) {
+__global__ __launch_bounds__(kBlock, PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
