@@ -1285,7 +1285,13 @@ template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
 #ifndef PM_SK_GROUP_WAVES
 #define PM_SK_GROUP_WAVES 7
 #endif
-__global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? 8 : (M == Mode::kSankoff && AP) ? 7 : 1) void k_down(DownArgs a) {
+#ifndef PM_DOWN_WAVES
+#define PM_DOWN_WAVES 8
+#endif
+#ifndef PM_SK_DOWN_WAVES
+#define PM_SK_DOWN_WAVES 7
+#endif
+__global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? PM_DOWN_WAVES : (M == Mode::kSankoff && AP) ? PM_SK_DOWN_WAVES : 1) void k_down(DownArgs a) {
     __shared__ pm_mut stage[kWavesPerBlock][kStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
