@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import panman_amd  # noqa: E402  (after torch: one HIP runtime per process)
-from panman_amd.shard import gather_site_results, shard_range  # noqa: E402
+from panman_amd.shard import gather_site_results_device, shard_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md chip-level table)
 
@@ -60,9 +60,6 @@ def parse():
                    help="Fitch: PM_OPT_GROUP_WAVES, most waves of grouped pre-order levels in one launch "
                         "(-1: library default, 0: off)")
     p.add_argument("--group-levels", type=int, default=4, help="PM_OPT_GROUP_LEVELS (2 to 4)")
-    p.add_argument("--tail-chunk", type=int, default=-1,
-                   help="PM_OPT_TAIL_OVERLAP: tail chunks of >= this many waves beside the pre-order "
-                        "levels (-1: library default, 0: after the last level)")
     p.add_argument("--no-up-group", action="store_true",
                    help="Fitch: post-order launches by height (PM_OPT_UP_GROUP off)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
@@ -72,9 +69,11 @@ def parse():
     p.add_argument("--replay-blocks", type=int, default=500)
     p.add_argument("--replay-block-len", type=int, default=10_000)
     p.add_argument("--cpu-leaves", type=int, default=128, help="leaves replayed on the CPU baseline (~10 s)")
-    p.add_argument("--with", dest="with_", default="sankoff,replay,e2e",
+    p.add_argument("--with", dest="with_", default="sankoff,replay,e2e,commands",
                    help="secondary blocks in the default run's line: comma list of sankoff (N* Sankoff "
-                        "line), replay (C5 FASTA replay line), e2e (PCIe-inclusive rate), or none")
+                        "line), replay (C5 FASTA replay line), e2e (PCIe-inclusive rate), commands "
+                        "(panmanUtils -M / --low-mem-mode / -I --fasta-aligned wall times beside the "
+                        "oracle's restated drivers), or none")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_fitch.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     a = p.parse_args()
@@ -122,8 +121,6 @@ def main():
         eng.set_subtree(False)
     if args.narrow >= 0:
         eng.set_narrow(args.narrow)
-    if args.tail_chunk >= 0:
-        eng.set_tail_overlap(args.tail_chunk)
     if args.no_up_group:
         eng.set_up_group(False)
     if args.group >= 0 or args.group_levels != 4:
@@ -173,6 +170,11 @@ def main():
         log(rank, f"[bench] secondary: C5 replay ({time.time() - t0:.1f}s)")
         secondary["replay"] = replay_block(args, world, rank, local)
 
+    commands = None
+    if world == 1 and "commands" in extra and rank == 0:
+        log(rank, f"[bench] command-level block ({time.time() - t0:.1f}s)")
+        commands = commands_block(args)
+
     if rank == 0:
         out = {
             "metric": f"Fitch-Sankoff site*node updates/sec ({args.mode} mode)",
@@ -188,6 +190,7 @@ def main():
             "dtype": "u32 bit-planes (16-bit one-hot state sets)" if mode == panman_amd.MODE_FITCH
             else "u32 bit-planes (Z0/Z1 optimal-code sets, exact unit-cost Sankoff)",
             "data": f"synthetic (seeded on-device tree-evolved columns, {args.tree} tree)",
+            "build_id": panman_amd.build_id(),
             "config": {
                 "workload": (f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)"
                              if args.tree == "random-join" else
@@ -203,6 +206,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "end_to_end": e2e,
+            "commands": commands,
             "secondary": {k: {kk: v[kk] for kk in ("value", "unit", "ms_per_step", "metric", "roofline",
                                                    "config", "cpu_baseline", "parity_sample")
                               if kk in v}
@@ -220,19 +224,15 @@ def parsimony_block(args, eng, mode, ctx):
     # per-site (score, root code) of every site of the job, on every rank
     score_all = torch.zeros(S, dtype=torch.int32, device="cuda")
     root_all = torch.zeros(S, dtype=torch.uint8, device="cuda")
-    score_loc = torch.zeros(s_local, dtype=torch.int32, device="cuda")
-    root_loc = torch.zeros(s_local, dtype=torch.uint8, device="cuda")
 
     def step():
         if world > 1 and ctx["lib_gather"]:   # shard run + ONE RCCL all-gather inside the library
             eng.run_gather(mode, S, ctx["lo"], score_all.data_ptr(), root_all.data_ptr())
-        elif world > 1:
+        elif world > 1:   # the same chunks through a torch.distributed all-gather
             eng.run(mode)
-            eng.site_results_device(score_loc.data_ptr(), root_loc.data_ptr())
-            gather_site_results(score_loc, root_loc, S)
-        else:
+            gather_site_results_device(eng, ctx["lo"], S, score_all, root_all)
+        else:   # (score, root code) of every site stay in the context's device buffers
             eng.run(mode)
-            eng.site_results_device(score_all.data_ptr(), root_all.data_ptr())
 
     eng.set_graph(False)
     for _ in range(max(1, args.warmup)):
@@ -254,6 +254,8 @@ def parsimony_block(args, eng, mode, ctx):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    if world == 1:   # untimed: the last step's (score, root code), record buffers checked
+        eng.site_results_device(score_all.data_ptr(), root_all.data_ptr())
     if args.graph:   # per-kernel durations for the roofline: same steps, eager, untimed
         eng.set_graph(False)
         eng.set_profiling(True)
@@ -311,15 +313,24 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
     dms, dl, dbytes = classes[dom]
     achieved = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
     traffic_all, score_traffic = {}, None   # HBM bytes per run of each pass (PMC)
+    build = panman_amd.build_id()
+    traffic_note = f"no PMC traffic for this workload in {os.path.relpath(args.traffic, ROOT)}"
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            wk = f"{key}:{L}x{s_local}:step"
-            for k, kernels in prof_names.items():
-                got = [tj[n][wk] for n in kernels if wk in tj.get(n, {})]
-                traffic_all[k] = sum(got) if got else None
-            score_traffic = tj.get("k_site_score", {}).get(wk)
-        except (OSError, ValueError):
+            wk = f"{key}:{L}x{s_local}"
+            # PMC bytes count only for the library build they were measured on
+            stamps = {tj[n].get(wk + ":build") for kk in prof_names.values() for n in kk if wk in tj.get(n, {})}
+            if stamps and stamps != {build}:
+                traffic_note = (f"PMC traffic in {os.path.relpath(args.traffic, ROOT)} was measured on build(s) "
+                                f"{sorted(str(x) for x in stamps)}, the loaded library is {build}: re-profile")
+            elif stamps:
+                traffic_note = f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes on this build ({build})"
+                for k, kernels in prof_names.items():
+                    got = [tj[n][wk + ":step"] for n in kernels if wk + ":step" in tj.get(n, {})]
+                    traffic_all[k] = sum(got) if got else None
+                score_traffic = tj.get("k_site_score", {}).get(wk + ":step")
+        except (OSError, ValueError, KeyError):
             traffic_all = {}
     traffic = traffic_all[dom] / dl if traffic_all.get(dom) and dl else None   # per launch of the pass
     if fitch:   # SURVEY.md §8d contract: 2-B sets through memory
@@ -338,6 +349,8 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        "traffic_note": traffic_note,
+        "build_id": build,
         "bytes_model": "pm_design_bytes: bytes this record layout must move (16-B lane granularity)",
         "design_bytes_per_launch": dbytes / dl if dl else None,
         "traffic_over_design": round(traffic / (dbytes / dl), 3) if traffic and dl and dbytes else None,
@@ -417,19 +430,23 @@ def cgroup_cpus():
         return None
 
 
+def host_threads(args):
+    """Every CPU this process may run on: the affinity set, capped by the cgroup's CPU quota
+    (the GPU box exposes 256 CPUs but grants a 16-CPU quota; more threads than that only
+    time-slice the same 16 CPUs).  Returns (threads, usable, quota, effective)."""
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpus()
+    effective = max(1, min(usable, int(quota))) if quota else usable
+    return args.cpu_threads or effective, usable, quota, effective
+
+
 def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     """Reference-faithful CPU path (oracle: per-column unordered_map<string,int> +
     recursion, src/fitchSankoff.cpp:30-171) on a bounded column sample, plus a bit-exact
     check of the GPU kernels on the same sample at full tree size."""
     sys.path.insert(0, ROOT)
     import oracle as orc
-    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    quota = cgroup_cpus()
-    # every CPU this process may run on: the affinity set, capped by the cgroup's CPU quota
-    # (the GPU box exposes 256 CPUs but grants a 16-CPU quota; more threads than that only
-    # time-slice the same 16 CPUs)
-    effective = max(1, min(usable, int(quota))) if quota else usable
-    threads = args.cpu_threads or effective
+    threads, usable, quota, effective = host_threads(args)
     ns = args.cpu_sites or 3 * threads   # ~15 s of CPU work at 1M leaves
     codes = eng.leaf_codes(0, ns, L)
     cons = eng.consensus(0, ns)
@@ -472,6 +489,123 @@ def cpu_baseline(args, eng, off, idx, root, L, n_nodes, mode):
     parity = {"sites": ns, "records": int(want.shape[0]),
               "bit_exact": bool(got.shape == want.shape and (got == want).all())}
     return cpu, parity
+
+
+def evolved_msa(leaves: int, sites: int, seed: int, mu: float = 1e-3, gap: float = 1e-4):
+    """Random-join tree (T1) and a tree-evolved alignment: uniform ACGT root, per edge and
+    site a substitution (mu) or a one-site gap (gap); no all-gap column.
+    Returns (newick with leaves s<i>, MSA FASTA text)."""
+    off, idx, root = panman_amd.random_join_tree(leaves, seed=seed)
+    n = off.shape[0] - 1
+    rng = np.random.default_rng(seed + 1)
+    alphabet = np.frombuffer(b"-ACGT", np.uint8)
+    seq = np.zeros((n, sites), np.uint8)   # 1..4 = ACGT, 0 = gap
+    seq[root] = rng.integers(1, 5, size=sites)
+    order = [root]
+    for v in order:
+        kids = idx[off[v]:off[v + 1]]
+        order.extend(int(c) for c in kids)
+        for c in kids:
+            s = seq[v].copy()
+            r = rng.random(sites)
+            sub = r < mu
+            s[sub] = (s[sub] + rng.integers(0, 3, size=int(sub.sum()))) % 4 + 1   # another base (gap -> a base)
+            s[(r >= mu) & (r < mu + gap)] = 0
+            seq[c] = s
+    leaf = [v for v in range(n) if off[v] == off[v + 1]]
+    all_gap = (seq[leaf] == 0).all(axis=0)
+    seq[leaf[0], all_gap] = 1
+    names = {v: f"s{v}" for v in leaf}
+
+    def nwk(v):
+        kids = idx[off[v]:off[v + 1]]
+        return names[v] if len(kids) == 0 else "(" + ",".join(nwk(int(c)) for c in kids) + ")"
+    sys.setrecursionlimit(max(10000, 4 * n))
+    text = "".join(f">{names[v]}\n{alphabet[seq[v]].tobytes().decode()}\n" for v in leaf)
+    return nwk(root) + ";\n", text
+
+
+def commands_block(args):
+    """Command-level wall times of the drop-in CLI (bin/panmanUtils over the C-ABI: input
+    parsing, grouping, the GPU kernels, the PanMAN writer / FASTA text) beside the oracle's
+    restatement of the reference's drivers on the same host and inputs:
+      -M (M1, src/panman.cpp:1274-1466, a sequential per-column loop: 1 thread),
+      --low-mem-mode (M2, :1467-1649, tbb::parallel_for over columns: every quota thread),
+      -I <C5 .panman> --fasta-aligned (R1, src/fasta.cpp:1981-2099, parallel_for_each over
+      leaves: every quota thread).
+    The survey's compiled-reference probe of M1 on 2 000 x 2 000 took 2.63 s."""
+    import subprocess
+    import tempfile
+    sys.path.insert(0, ROOT)
+    import oracle as orc
+    cli = os.path.join(ROOT, "bin", "panmanUtils")
+    if not os.path.exists(cli):
+        return {"error": "bin/panmanUtils not built"}
+    threads = host_threads(args)[0]
+    o = orc.load()
+    out = {"threads": threads, "cli": "bin/panmanUtils (C++ over libpanman_amd.so, 1 GPU)",
+           "oracle": "oracle/pm_oracle.cpp restated drivers (reference unbuildable here)",
+           "survey_reference_probe": {"M1 2000x2000": "2.63 s", "M1 20000x300": "6.78 s",
+                                      "M2 2000x2000 (serial TBB stand-in)": "9.52 s",
+                                      "M2 20000x300 (serial TBB stand-in)": "19.47 s"},
+           "runs": []}
+
+    def run_cli(argv, cwd, stdout=None):
+        t = time.perf_counter()
+        r = subprocess.run([cli] + argv, cwd=cwd, stdout=stdout or subprocess.PIPE, stderr=subprocess.PIPE,
+                           timeout=600)
+        dt = time.perf_counter() - t
+        if r.returncode != 0:
+            raise RuntimeError(f"panmanUtils {' '.join(argv)}: {r.stderr.decode(errors='replace')[-400:]}")
+        return dt
+
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+        for leaves, sites in ((2000, 2000), (20000, 300)):
+            nwk, msa = evolved_msa(leaves, sites, seed=11)
+            with open(os.path.join(tmp, "t.nwk"), "w") as f:
+                f.write(nwk)
+            with open(os.path.join(tmp, "a.fa"), "w") as f:
+                f.write(msa)
+            for low_mem in (False, True):
+                flag = ["--low-mem-mode"] if low_mem else []
+                try:
+                    gpu_s = run_cli(["-M", "a.fa", "-N", "t.nwk", "-o", "cmd"] + flag, tmp)
+                except (RuntimeError, subprocess.TimeoutExpired) as exc:
+                    out["runs"].append({"command": f"-M {'--low-mem-mode ' if low_mem else ''}{leaves}x{sites}",
+                                        "error": str(exc)})
+                    continue
+                nt = threads if low_mem else 1
+                t = time.perf_counter()
+                dump = o.msa_build(nwk, msa, "", mode=1 if low_mem else 0, threads=nt)
+                cpu_s = time.perf_counter() - t
+                recs = sum(1 for line in dump.splitlines() if line and not line.startswith("#"))
+                out["runs"].append({
+                    "command": f"panmanUtils -M a.fa -N t.nwk -o cmd{' --low-mem-mode' if low_mem else ''}",
+                    "workload": f"{leaves} leaves x {sites} columns (random-join tree, tree-evolved MSA)",
+                    "gpu_cli_wall_s": round(gpu_s, 3),
+                    "oracle_driver_s": round(cpu_s, 3), "oracle_threads": nt,
+                    "oracle_scope": "construction only (the CLI also writes the .panman: Cap'n Proto + xz)",
+                    "speedup": round(cpu_s / gpu_s, 2), "oracle_nucmut_records": recs})
+        # C5: -I <file> --fasta-aligned, text to stdout (discarded)
+        from panman_amd.synth import c5_panmat
+        pm = c5_panmat(leaves=args.replay_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len)
+        path = os.path.join(tmp, "c5.panman")
+        try:
+            panman_amd.write_panman(path, [pm])
+            with open(os.devnull, "wb") as devnull:
+                gpu_s = run_cli(["-I", path, "-m"], tmp, stdout=devnull)
+            text, cpu_s = o.fasta(pm, True, timed=True, threads=threads)
+            out["runs"].append({
+                "command": "panmanUtils -I c5.panman --fasta-aligned (stdout)",
+                "workload": f"C5: {args.replay_leaves} leaves, {args.replay_blocks} blocks, aligned text "
+                            f"{len(text) / 1e9:.2f} GB",
+                "gpu_cli_wall_s": round(gpu_s, 3), "oracle_driver_s": round(cpu_s, 3), "oracle_threads": threads,
+                "oracle_scope": "replay + text in memory (the CLI also loads the file and writes the text)",
+                "speedup": round(cpu_s / gpu_s, 2)})
+            del text
+        except (RuntimeError, subprocess.TimeoutExpired, OSError) as exc:
+            out["runs"].append({"command": "-I c5.panman --fasta-aligned", "error": str(exc)})
+    return out
 
 
 def replay_main(args):
@@ -567,8 +701,9 @@ def replay_block(args, world, rank, local):
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle as orc
-        k = args.cpu_leaves
-        want, secs = orc.load().fasta(pm, True, leaf_limit=k, timed=True)
+        threads = host_threads(args)[0]
+        k = max(args.cpu_leaves, 32 * threads)   # every thread replays many leaves (~2-3 s wall)
+        want, secs = orc.load().fasta(pm, True, leaf_limit=k, timed=True, threads=threads)
         names = sorted(nm for nm, i in zip(pm.names, range(pm.num_nodes)) if off[i] == off[i + 1])[:k]
         got = []
         for nm in names:
@@ -576,9 +711,10 @@ def replay_block(args, world, rank, local):
             end = text.find(b">", at + 1)
             got.append(text[at: end if end >= 0 else len(text)].decode())
         parity = {"leaves": k, "bit_exact": "".join(got) == want}
-        cpu = {"value": k * cols / secs, "unit": "leaf*column/s", "cores": 1, "kind": "port",
+        cpu = {"value": k * cols / secs, "unit": "leaf*column/s", "cores": threads, "kind": "port",
                "sample": f"first {k} leaves by name, aligned FASTA, oracle printFASTAUltraFast restatement "
-                         f"({secs:.1f}s, 1 thread; the reference's tbb::parallel_for_each body)"}
+                         f"({secs:.1f}s on {threads} threads, leaves in parallel as the reference's "
+                         f"tbb::parallel_for_each over leaves, src/fasta.cpp:1993)"}
     # PMC-measured HBM bytes per k_replay_tile launch (tools/pmc_traffic.py, key replay:LxC)
     traffic = None
     if os.path.exists(args.traffic):

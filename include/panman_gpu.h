@@ -103,13 +103,13 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
  *                  latest children have out-degree <= 3 runs in their post-order launch,
  *                  recomputing them, instead of one launch per height; 0 = by height.
- *   PM_OPT_TAIL_OVERLAP (default 0): the records of children beyond a node's second (and
- *                  of inline subtrees) start on a second stream, in chunks of at least this
- *                  many (item, tile) waves, as soon as their parents' pre-order level is
- *                  done, beside the remaining levels; 0 = after the last level (measured: no gain
- *                  at N*, C2 or C3 -- the levels already occupy the chip).
- * (Option ids 1, 4 and 5 -- subtree-region, heavy-path-chain and level-band schedules --
- * were measured slower than the level kernels on MI355X and removed.) */
+ *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the
+ *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
+ *                  re-run with a larger buffer when its results are read (pm_mutation_count,
+ *                  pm_site_results*, pm_run_gather), so results never depend on it.
+ * (Option ids 1, 4, 5 and 11 -- subtree-region, heavy-path-chain and level-band schedules,
+ * tail records overlapped with the pre-order levels -- were measured slower than, or no
+ * faster than, the level kernels on MI355X and removed.) */
 #define PM_OPT_VIRTUAL 2
 #define PM_OPT_GRAPH 3
 #define PM_OPT_SUBTREE 6
@@ -117,7 +117,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_GROUP_WAVES 8
 #define PM_OPT_GROUP_LEVELS 9
 #define PM_OPT_UP_GROUP 10
-#define PM_OPT_TAIL_OVERLAP 11
+#define PM_OPT_RECORD_CAP 12
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);
@@ -154,8 +154,9 @@ int pm_mutations_fetch(pm_ctx* ctx, pm_mut* out, int64_t cap, int64_t* count);
 /* Per site: number of mutated edges below the root (parsimony score of the assignment)
  * and the root's final code (255 = unresolved).  Either pointer may be NULL. */
 int pm_site_results(pm_ctx* ctx, int32_t* score, uint8_t* root_code);
-/* Same, copied device-to-device into caller buffers on the ctx stream (async), so that a
- * collective can gather them without a host round trip. */
+/* Same, copied device-to-device into caller buffers on the ctx stream (async after the
+ * record-buffer check, which synchronises), so that a collective can gather them without a
+ * host copy. */
 int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_device);
 /* Accumulated device milliseconds and launch counts per kernel class since the last
  * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram, 3 replay,
@@ -176,11 +177,22 @@ int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
  *   pm_run_gather       pm_run on this rank's shard [site_begin, site_begin + uploaded
  *                       sites) of `total_sites`, then the all-gather: score_device
  *                       [total_sites] int32 and root_device [total_sites] u8 (device
- *                       memory) receive every rank's sites.  Async on the ctx stream;
- *                       every rank must call it.  Shards hold at most ceil(total/ranks)+2.
+ *                       memory) receive every rank's sites.  Every rank must call it; it
+ *                       returns when the gathered vectors are complete.  A rank whose shard
+ *                       fails (bad range, run error) still joins the collective with a
+ *                       failed chunk head, so every rank returns an error instead of one
+ *                       rank leaving the others blocked.  Shards hold at most
+ *                       ceil(total/ranks)+2 sites.
  *   pm_multi_run        the same for pm_comm_init_all contexts from one thread (RCCL group
  *                       call); site_begin[i] per ctx; results to host (nullable).
- *   pm_shard_range      the balanced rule [r*S/n, (r+1)*S/n) bench.py and shard.py use. */
+ *   pm_shard_range      the balanced rule [r*S/n, (r+1)*S/n) bench.py and shard.py use.
+ * The gathered unit is one chunk per rank of `per` = ceil(S/ranks)+3 u64 entries: entry 0 =
+ * site_begin << 32 | count (count 0xffffffff: that rank failed), then one entry per site =
+ * score (int32) | root code << 32.  The same layout moves through any other collective:
+ *   pm_pack_site_results    the ctx's last run into a chunk in device memory (async);
+ *   pm_unpack_site_results  ranks x per gathered entries (device) into score / root device
+ *                           vectors; checks the heads (failed rank, overlaps, gaps); syncs.
+ *   pm_chunk_entries / pm_chunk_pack / pm_chunk_unpack  the same on host memory, no GPU. */
 #define PM_COMM_ID_BYTES 128
 int pm_comm_unique_id(uint8_t* id, int64_t len);
 int pm_comm_init_rank(pm_ctx* ctx, const uint8_t* id, int nranks, int rank);
@@ -190,6 +202,14 @@ int pm_run_gather(pm_ctx* ctx, int mode, int64_t total_sites, int64_t site_begin
 int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin, int64_t total_sites,
                  int32_t* score, uint8_t* root_code);
 int pm_shard_range(int rank, int ranks, int64_t total_sites, int64_t* begin, int64_t* end);
+int pm_pack_site_results(pm_ctx* ctx, int64_t site_begin, int64_t per, void* chunk_device);
+int pm_unpack_site_results(pm_ctx* ctx, const void* all_device, int64_t per, int ranks, int64_t total_sites,
+                           void* score_device, void* root_device);
+int pm_chunk_entries(int64_t total_sites, int ranks, int64_t* per);
+int pm_chunk_pack(int64_t site_begin, int64_t count, const int32_t* score, const uint8_t* root, int64_t per,
+                  uint64_t* chunk);
+int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_sites, int32_t* score,
+                    uint8_t* root);
 
 /* ---- measurement (bench.py roofline; not part of the reference interface) ------------ */
 /* Bytes this design must move in the last pm_run (nucleotide modes), counted from the run's
@@ -201,6 +221,8 @@ int pm_shard_range(int rank, int ranks, int64_t total_sites, int64_t* begin, int
  * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
  * words, finals written, tail items.  `n` >= 5.  Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
+/* Hash of the library's sources (16 hex digits): profiled PMC traffic is tied to it. */
+const char* pm_build_id(void);
 /* Achievable HBM rate on `device`: a 16-B-per-lane streaming copy of `bytes` bytes, `reps`
  * times; *gbs = (read + write bytes) / s / 1e9. */
 int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs);

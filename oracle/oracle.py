@@ -35,9 +35,11 @@ def load() -> "Oracle":
             C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
             C.c_int, C.c_int, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int64), C.c_void_p]
         lib.oracle_fasta.restype = C.c_void_p
-        lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
+        lib.oracle_fasta.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
         lib.oracle_pangraph.restype = C.c_void_p
         lib.oracle_pangraph.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+        lib.oracle_pangraph_fasta.restype = C.c_void_p
+        lib.oracle_pangraph_fasta.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]
         lib.oracle_summary.restype = C.c_void_p
         lib.oracle_summary.argtypes = [C.c_void_p]
         lib.oracle_reroot.restype = C.c_void_p
@@ -66,12 +68,13 @@ class Oracle:
                                       mode, threads)
         return _take_string(self.lib, p)
 
-    def fasta(self, panmat, aligned: bool, leaf_limit: int = 0, timed: bool = False):
+    def fasta(self, panmat, aligned: bool, leaf_limit: int = 0, timed: bool = False, threads: int = 1):
         """printFASTAUltraFast records of every leaf (or the first `leaf_limit` by name),
-        sorted by name (panman_amd.panmat.PanMAT).  timed=True -> (text, seconds)."""
+        sorted by name (panman_amd.panmat.PanMAT).  timed=True -> (text, seconds).
+        threads > 1: leaves replayed in parallel (the reference's parallel_for_each)."""
         st, keep = panmat.as_struct()
         secs = C.c_double(0.0)
-        p = self.lib.oracle_fasta(C.byref(st), int(aligned), int(leaf_limit), C.byref(secs))
+        p = self.lib.oracle_fasta(C.byref(st), int(aligned), int(leaf_limit), int(threads), C.byref(secs))
         del keep
         text = _take_string(self.lib, p)
         return (text, secs.value) if timed else text
@@ -80,6 +83,13 @@ class Oracle:
         """Tree(PanGraph) dump (M3): blocks, then per node its block mutations and NucMuts.
         tbb_order=False iterates individualSequences as a std::unordered_map instead."""
         p = self.lib.oracle_pangraph(flat.encode(), newick.encode(), reference.encode(), int(tbb_order))
+        return _take_string(self.lib, p)
+
+    def pangraph_fasta(self, flat: str, newick: str, reference: str = "", tbb_order: bool = True,
+                       aligned: bool = False) -> str:
+        """M3 then printFASTAUltraFast on the built Tree: every leaf's record, by name."""
+        p = self.lib.oracle_pangraph_fasta(flat.encode(), newick.encode(), reference.encode(), int(tbb_order),
+                                           int(aligned))
         return _take_string(self.lib, p)
 
     def reroot(self, panmat, leaf: str) -> str:

@@ -1466,19 +1466,31 @@ std::string reroot_dump(RTree& t, const std::string& name) {
 
 // FASTA records of every leaf (printFASTAUltraFast), sorted by leaf name; at most
 // `leaf_limit` leaves (<= 0: all) and, when `seconds` is set, the replay wall time.
-char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, double* seconds) {
+// `threads` > 1: the leaves are replayed in parallel, as the reference's
+// tbb::parallel_for_each over leaves does (src/fasta.cpp:1993), then joined in name order.
+char* oracle_fasta(const OraclePanmat* p, int aligned, int leaf_limit, int threads, double* seconds) {
     RTree t;
     build_rtree(p, t);
-    std::string out;
-    int done = 0;
-    auto t0 = std::chrono::steady_clock::now();
+    std::vector<RNode*> leaves;
     for (auto& kv : t.all) {
         if (!kv.second->children.empty()) continue;
-        if (leaf_limit > 0 && done >= leaf_limit) break;
-        out += leaf_record(t, kv.second, aligned != 0);
-        ++done;
+        if (leaf_limit > 0 && (int)leaves.size() >= leaf_limit) break;
+        leaves.push_back(kv.second);
     }
+    std::vector<std::string> rec(leaves.size());
+    auto t0 = std::chrono::steady_clock::now();
+    const int nt = std::max(1, std::min(threads, (int)leaves.size()));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i = next++; i < leaves.size(); i = next++) rec[i] = leaf_record(t, leaves[i], aligned != 0);
+    };
+    std::vector<std::thread> pool;
+    for (int k = 1; k < nt; ++k) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::string out;
+    for (auto& r : rec) out += r;
     return dup_string(out);
 }
 
@@ -1730,7 +1742,11 @@ std::vector<std::string> split_tabs(const std::string& line) {
 
 using Item = std::pair<char, std::vector<char>>;
 
-std::string build_dump(const std::string& flat, const std::string& newick, const std::string& reference, bool tbb_order) {
+// `rt` (nullable) receives the built Tree in the R1 replay's form (blocks packed 8 codes per
+// u32, gap slots, per-node mutations, rotation / inversion / circular offsets), so the
+// oracle's printFASTAUltraFast restatement can replay what this driver built.
+std::string build_dump(const std::string& flat, const std::string& newick, const std::string& reference, bool tbb_order,
+                       RTree* rt = nullptr) {
     // --- Pangraph (:6200-6425) ---
     std::unordered_map<std::string, std::vector<std::string>> paths;
     std::unordered_map<std::string, std::vector<int>> strand_paths;
@@ -2035,6 +2051,44 @@ std::string build_dump(const std::string& flat, const std::string& newick, const
     std::map<std::string, std::vector<RNucMut>> nuc;
     for (auto& kv : non_gap) group6(kv.second, false, nuc[kv.first]);
     for (auto& kv : gap_m) group6(kv.second, true, nuc[kv.first]);
+    if (rt) {
+        std::unordered_map<const ONode*, RNode*> of;
+        for (ONode* o : t.owned) {
+            auto n = std::make_unique<RNode>();
+            n->id = o->id;
+            of[o] = n.get();
+            rt->nodes.push_back(std::move(n));
+        }
+        for (ONode* o : t.owned) {
+            RNode* n = of[o];
+            if (o->parent) n->parent = of[o->parent];
+            for (ONode* ch : o->children) n->children.push_back(of[ch]);
+            rt->all[n->id] = n;
+        }
+        rt->root = of[t.root];
+        rt->internal_counter = t.internal_counter;
+        for (size_t i = 0; i < topo.size(); ++i) {
+            const std::string& seq = consensus[id_of[topo[i]]];
+            RBlock b{(int32_t)i, std::vector<uint32_t>((seq.size() + 8) / 8, 0u)};   // a 0 code ends the block
+            for (size_t k = 0; k < seq.size(); ++k) b.seq[k / 8] |= (uint32_t)code_of(seq[k]) << (4 * (7 - k % 8));
+            rt->blocks.push_back(std::move(b));
+            RGap g{(int32_t)i, {}, {}};
+            for (auto& gp : gaps[id_of[topo[i]]]) {
+                g.pos.push_back((uint32_t)gp.first);
+                g.len.push_back((uint32_t)gp.second);
+            }
+            rt->gaps.push_back(std::move(g));
+        }
+        for (auto& kv : block_muts)
+            if (rt->all.count(kv.first)) rt->all[kv.first]->bmuts = kv.second;
+        for (auto& kv : nuc)
+            if (rt->all.count(kv.first)) rt->all[kv.first]->nmuts = kv.second;
+        for (auto& kv : circular) rt->circular[kv.first] = kv.second;
+        for (auto& kv : rotation)
+            if (kv.second != 0) rt->rotation[kv.first] = kv.second;
+        for (auto& kv : inverted)
+            if (kv.second) rt->inverted[kv.first] = true;
+    }
     // dump: blocks, then per node (name order) block and nucleotide mutations
     std::string out;
     char buf[200];
@@ -2060,6 +2114,22 @@ std::string build_dump(const std::string& flat, const std::string& newick, const
 }
 
 }  // namespace pgo
+
+// M3 then R1 (src/panman.cpp:820-1273, src/fasta.cpp:1981-2099): the FASTA records of every
+// leaf of the Tree the PanGraph driver builds, sorted by leaf name -- the round trip that
+// test/sars_20.fa pins (the input genomes come back).
+char* oracle_pangraph_fasta(const char* flat, const char* newick, const char* reference, int tbb_order, int aligned) {
+    std::string nwk(newick);
+    const size_t nl = nwk.find('\n');
+    if (nl != std::string::npos) nwk.resize(nl);
+    RTree t;
+    const std::string dump = pgo::build_dump(flat, nwk, reference ? reference : "", tbb_order != 0, &t);
+    if (dump.rfind("#error", 0) == 0 || !t.root) return dup_string(dump);
+    std::string out;
+    for (auto& kv : t.all)
+        if (kv.second->children.empty()) out += leaf_record(t, kv.second, aligned != 0);
+    return dup_string(out);
+}
 
 char* oracle_pangraph(const char* flat, const char* newick, const char* reference, int tbb_order) {
     std::string nwk(newick);

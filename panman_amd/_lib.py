@@ -93,11 +93,24 @@ _SIGS = {
     "pm_run_gather": (C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]),
     "pm_multi_run": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
     "pm_shard_range": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "pm_pack_site_results": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]),
+    "pm_unpack_site_results": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p,
+                                         C.c_void_p]),
+    "pm_chunk_entries": (C.c_int, [C.c_int64, C.c_int, C.POINTER(C.c_int64)]),
+    "pm_chunk_pack": (C.c_int, [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "pm_chunk_unpack": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]),
     "pm_summary_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Summary)]),
     "pm_design_bytes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "pm_build_id": (C.c_char_p, []),
     "pm_stream_copy_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
+
+
+def build_id() -> str:
+    """Hash of the loaded library's sources (pm_build_id)."""
+    lib = load()
+    return lib.pm_build_id().decode() if hasattr(lib, "pm_build_id") else "unknown"
 
 
 def header_symbols() -> list[str]:

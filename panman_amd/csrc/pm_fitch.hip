@@ -15,9 +15,6 @@
 #include "pm_kernels.h"
 
 namespace pm {
-#ifdef PM_EXP_COUNT_COMPLEX
-__device__ unsigned long long g_exp_words[4];
-#endif
 namespace {
 
 // One wave = (node, tile).  Children are folded straight into the AND / OR accumulators
@@ -154,23 +151,6 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     uint64_t mx, ms;
     store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
-#ifdef PM_EXP_COUNT_COMPLEX
-    {
-        uint32_t one = 0, two = 0;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) { two |= one & both[v]; one |= both[v]; }
-        const bool complex_word = (one != ~0u) || two;
-        const unsigned long long m = __ballot(complex_word);
-        const bool acgt = ((ms >> lane) & 1ull) && (both[1] | both[2] | both[4] | both[8]) == ~0u;
-        const unsigned long long ma = __ballot(acgt);
-        if (lane == 0) {
-            atomicAdd(&g_exp_words[0], (unsigned long long)__popcll(m));
-            atomicAdd(&g_exp_words[1], 64ull);
-            atomicAdd(&g_exp_words[2], (unsigned long long)__popcll(ms));
-            atomicAdd(&g_exp_words[3], (unsigned long long)__popcll(ma));
-        }
-    }
-#endif
 }
 
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
@@ -606,49 +586,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
-    // The tail (children beyond the second, S2 / S3 subtrees) needs only its parents' finals:
-    // items whose parent's level is done start on the side stream, beside the remaining
-    // levels, in chunks of >= tail_chunk waves (not when profiling: the class timers time the
-    // main stream).
-    const TailDesc* tail_desc = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
-    int32_t tail_total = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
-#ifdef PM_EXP_NOTAIL   // timing experiment: no tail launch
-    tail_total = 0;
-#endif
-    const std::vector<int32_t>& tail_off = ht.tail_lvl_off[form];
-    const bool tail_side = !c->profiling && c->tail_chunk > 0;
-    int32_t tail_done = 0;
-    bool tail_forked = false;
-    auto tail_flush = [&](int level_end, bool last) -> hipError_t {
-        const int32_t upto = last ? tail_total : std::min(tail_total, tail_off[level_end]);
-        if (upto <= tail_done || (!last && (!tail_side || (int64_t)(upto - tail_done) * tiles < c->tail_chunk)))
-            return hipSuccess;
-        hipStream_t s = c->stream;
-        if (tail_side) {
-            const hipError_t fe = side_fork(c);
-            if (fe != hipSuccess) return fe;
-            s = c->side;
-            tail_forked = true;
-        }
-        DownArgs t = dn;
-        t.tail = tail_desc + tail_done;
-        t.count = upto - tail_done;
-        tail_done = upto;
-        const dim3 grid = wave_grid(t.count, tiles);
-        if (!tail_side) timer_begin(c, 1);
-        if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, s, t);
-        else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, s, t);
-        else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, s, t);
-        else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, s, t);
-        else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, s, t);
-        if (!tail_side) timer_end(c, 1);
-        return hipSuccess;
-    };
     for (int d = 0; d < D; ++d) {
-        {
-            const hipError_t te = tail_flush(d, false);
-            if (te != hipSuccess) return te;
-        }
         if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {
             int d1 = d + 1;
             while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
@@ -716,9 +654,22 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
-    hipError_t te = tail_flush(D, true);
-    if (te == hipSuccess && tail_forked) te = side_join(c);
-    if (te != hipSuccess) return te;
+    // The tail (children beyond the second, S2 / S3 subtrees) needs only its parents'
+    // finals: one flat launch after the levels.
+    const int32_t tail_total = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
+    if (tail_total > 0) {
+        DownArgs t = dn;
+        t.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
+        t.count = tail_total;
+        const dim3 grid = wave_grid(t.count, tiles);
+        timer_begin(c, 1);
+        if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, t);
+        else if (block && ap) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, true>), grid, dim3(kBlock), 0, c->stream, t);
+        else if (block) hipLaunchKernelGGL((k_tail<Mode::kBlockFitch, false>), grid, dim3(kBlock), 0, c->stream, t);
+        else if (ap) hipLaunchKernelGGL((k_tail<Mode::kFitch, true>), grid, dim3(kBlock), 0, c->stream, t);
+        else hipLaunchKernelGGL((k_tail<Mode::kFitch, false>), grid, dim3(kBlock), 0, c->stream, t);
+        timer_end(c, 1);
+    }
     return hipGetLastError();
 }
 
@@ -737,10 +688,4 @@ hipError_t launch_score(pm_ctx* c) {
 }
 
 }  // namespace pm
-
-#ifdef PM_EXP_COUNT_COMPLEX
-extern "C" int pm_exp_counters(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pm::g_exp_words), 32) == hipSuccess ? 0 : -1;
-}
-#endif
 

@@ -181,7 +181,7 @@ int alloc_work(pm_ctx* c, int mode) {
     if (c->shard_cap == 0) {
         const double nodes = (double)c->dt.num_internal + c->dt.num_leaves;
         const double guess = std::max(65536.0, 0.01 * nodes * (double)c->num_sites);
-        const int64_t cap = (int64_t)(guess * 1.5 / kShards) + 256;
+        const int64_t cap = c->record_cap > 0 ? c->record_cap : (int64_t)(guess * 1.5 / kShards) + 256;
         if ((e = dev_alloc(&c->recs, (size_t)cap * kShards)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("mutation records: ") + hipGetErrorString(e));
         c->shard_cap = cap;
@@ -200,7 +200,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
-                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group, (uint64_t)c->tail_chunk,
+                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -274,6 +274,11 @@ int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
 }
 
 }  // namespace
+
+int settle_run(pm_ctx* c) {
+    std::vector<uint32_t> counts;
+    return settle(c, counts);
+}
 
 hipError_t side_fork(pm_ctx* c) {
     hipError_t e = hipEventRecord(c->ev_fork, c->stream);
@@ -409,11 +414,6 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->narrow_max = (int32_t)value;
         return PM_OK;
     }
-    if (option == PM_OPT_TAIL_OVERLAP) {
-        if (value < 0) return fail(c, PM_ERR_ARG, "PM_OPT_TAIL_OVERLAP: >= 0 waves");
-        c->tail_chunk = value;
-        return PM_OK;
-    }
     if (option == PM_OPT_UP_GROUP) {
         c->up_group = value != 0;
         return PM_OK;
@@ -426,6 +426,16 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_GROUP_LEVELS) {
         if (value < 2 || value > 4) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_LEVELS: 2 to 4");
         c->group_levels = (int32_t)value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_RECORD_CAP) {
+        if (value < 1 || value > ((int64_t)1 << 31)) return fail(c, PM_ERR_ARG, "PM_OPT_RECORD_CAP: 1 .. 2^31 records per shard");
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        drop_graph(c);
+        dev_free(c->recs);
+        c->shard_cap = 0;   // the next run allocates record_cap per shard
+        c->record_cap = value;
+        c->ran = false;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
@@ -578,6 +588,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
     const int32_t I = (int32_t)ht.internal_id.size();
     const int32_t L = (int32_t)ht.leaf_id.size();
+    // child encodings keep the dense index in the low kShapeShift bits (shape and virtual
+    // flags above it)
+    if (I >= (1 << kShapeShift)) return fail(c, PM_ERR_ARG, "trees of 2^28 or more internal nodes are not supported");
     ht.child_off.assign(I + 1, 0);
     ht.child_enc.reserve(E);
     std::vector<int32_t> parent_dense(I, -1), leaf_parent(L, -1);
@@ -933,23 +946,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
     ht.num_tail_k = (int32_t)tail_desc_k.size();
     // tail items by their parent's pre-order level (the subtree form's levels are the leaf-
-    // parent form's, S2 / S3 nodes removed), with per-level offsets: the launcher starts the
-    // items of finished levels beside the remaining levels (side stream)
+    // parent form's, S2 / S3 nodes removed): neighbouring waves read neighbouring parents
     {
         auto by_level = [&](std::vector<TailDesc>& tail, const std::vector<int32_t>& order,
-                            const std::vector<int32_t>& offs, std::vector<int32_t>& tail_off) {
+                            const std::vector<int32_t>& offs) {
             std::vector<int32_t> lvl_of(I, 0);
             for (size_t l = 0; l + 1 < offs.size(); ++l)
                 for (int32_t i = offs[l]; i < offs[l + 1]; ++i) lvl_of[order[i]] = (int32_t)l;
             std::stable_sort(tail.begin(), tail.end(),
                              [&](const TailDesc& x, const TailDesc& y) { return lvl_of[x.parent] < lvl_of[y.parent]; });
-            tail_off.assign(offs.size(), 0);
-            for (const TailDesc& t : tail) ++tail_off[lvl_of[t.parent] + 1];
-            for (size_t l = 0; l + 1 < tail_off.size(); ++l) tail_off[l + 1] += tail_off[l];
         };
-        by_level(tail_desc, down_order, ht.down_level_off, ht.tail_lvl_off[0]);
-        by_level(tail_desc_v, down_order_v, ht.down_level_off_v, ht.tail_lvl_off[1]);
-        by_level(tail_desc_k, down_order_v, ht.down_level_off_v, ht.tail_lvl_off[2]);
+        by_level(tail_desc, down_order, ht.down_level_off);
+        by_level(tail_desc_v, down_order_v, ht.down_level_off_v);
+        by_level(tail_desc_k, down_order_v, ht.down_level_off_v);
     }
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
@@ -1175,6 +1184,8 @@ int pm_site_results(pm_ctx* c, int32_t* score, uint8_t* root_code) {
 int pm_site_results_device(pm_ctx* c, void* score_device, void* root_device) {
     if (!c) return PM_ERR_ARG;
     if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    const int rc = settle_run(c);
+    if (rc != PM_OK) return rc;
     hipError_t e = hipSuccess;
     if (score_device)
         e = hipMemcpyAsync(score_device, c->score, sizeof(int32_t) * c->num_sites, hipMemcpyDeviceToDevice, c->stream);

@@ -163,7 +163,6 @@ struct HostTree {
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
-    std::vector<int32_t> tail_lvl_off[3];   // per form: tail items whose parent's pre-order level is < l
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form
     int64_t lvl_up[4] = {0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
 };
@@ -195,7 +194,6 @@ struct pm_ctx {
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
-    int64_t tail_chunk = 0;           // tail chunks of >= this many waves beside the remaining pre-order levels, 0 = off (PM_OPT_TAIL_OVERLAP)
 
     // column shard
     int64_t num_sites = 0;
@@ -222,6 +220,7 @@ struct pm_ctx {
     uint4* root_final = nullptr;      // [W] the root's final codes (other finals live in the records)
     pm_mut* recs = nullptr;           // [kShards][shard_cap]
     int64_t shard_cap = 0;
+    int64_t record_cap = 0;           // PM_OPT_RECORD_CAP: first allocation per shard (0 = a guess)
     uint32_t* shard_cnt = nullptr;    // [kShards]
     int32_t* score = nullptr;         // [S]
     uint8_t* root_code = nullptr;     // [S]
@@ -252,6 +251,9 @@ struct pm_ctx {
 namespace pm {
 
 int fail(pm_ctx* c, int code, const std::string& msg);
+// Synchronise after a run; if a record shard overflowed, grow the buffer and run again (the
+// per-site score only counts stored records).  pm_host.cpp.
+int settle_run(pm_ctx* c);
 int hip_fail(pm_ctx* c, hipError_t e, const char* what);
 
 // Work queued on c->side between side_fork and side_join runs concurrently with the work

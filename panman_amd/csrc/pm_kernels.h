@@ -1011,12 +1011,8 @@ __device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink
 __device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* stage, uint32_t total, uint32_t shard,
                                             int lane, int item, int tile, uint32_t& base, pm_mut*& out) {
     base = 0;
-#ifdef PM_EXP_NOATOMIC
-    base = (uint32_t)((item * 64 + tile) % 1024) * 16;
-#else
     if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
     base = __shfl(base, 0, 64);
-#endif
     out = a.recs + (size_t)shard * a.shard_cap;
     if (total > kStage) return false;
     for (uint32_t i = lane; i < total; i += kWave)
@@ -1199,11 +1195,7 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
         const uint4 q = is_root ? a.cons[word] : parent_final<REC>(a, parent, m, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
-#ifdef PM_EXP_NODIRTY   // timing experiment: no leaf-ish child loads in the pre-order pass
-    const bool dirty = false;
-#else
     const bool dirty = is_root || ((m.d >> lane) & 1ull);
-#endif
     Kid kids[2];
     kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
     if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
@@ -1229,14 +1221,6 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     }
 
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-#ifdef PM_EXP_NORECORDS   // timing experiment: loads and finals only, no records
-    {
-        uint32_t x = self_diff;
-        for (int k = 0; k < 2; ++k) x ^= kids[k].L0.x ^ kids[k].L0.y ^ kids[k].L0.z ^ kids[k].L0.w ^ kids[k].L1.x ^ kids[k].L1.y ^ kids[k].L1.z ^ kids[k].L1.w;
-        if (x == 0x9E3779B9u) a.shard_cnt[0] = x;
-        return;
-    }
-#endif
     // Records: every lane's count first, positions by a wave prefix sum (no LDS counter),
     // and the shard reservation's global atomic issued before the records are built, so
     // its round trip overlaps the staging.

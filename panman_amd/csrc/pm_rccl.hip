@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "pm_chunk.h"
 #include "pm_internal.h"
 
 namespace pm {
@@ -75,29 +76,18 @@ int rccl_fail(pm_ctx* c, ncclResult_t e, const char* what) {
     return fail(c, PM_ERR_HIP, std::string(what) + ": " + rccl().error_string(e));
 }
 
-// Gather chunk: entry 0 = (site_begin << 32 | count), then count packed sites.  Shards of
-// every rule in use (balanced r*S/n, the MSA driver's even-aligned one) hold at most
-// ceil(S/n) + 2 sites.
-int64_t chunk_entries(int64_t total, int n) { return (total + n - 1) / n + 3; }
-
-__global__ void k_pack_results(const int32_t* score, const uint8_t* root, int64_t begin, int64_t count,
+__global__ void k_pack_results(const int32_t* score, const uint8_t* root, int64_t begin, int64_t count, bool ok,
                                uint64_t* chunk) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) chunk[0] = ((uint64_t)begin << 32) | (uint64_t)count;
-    if (i < count) chunk[1 + i] = (uint64_t)(uint32_t)score[i] | ((uint64_t)root[i] << 32);
+    if (i == 0) chunk[0] = ok ? chunk_head(begin, count) : chunk_failed_head();
+    if (ok && i < count) chunk[1 + i] = chunk_entry(score[i], root[i]);
 }
 
 __global__ void k_unpack_results(const uint64_t* all, int64_t per, int n, int64_t total, int32_t* score,
-                                 uint8_t* root) {
+                                 uint8_t* root, int32_t* status) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= per * n) return;
-    const int64_t r = g / per, i = g - r * per;
-    const uint64_t head = all[r * per];
-    const int64_t begin = (int64_t)(head >> 32), count = (int64_t)(head & 0xffffffffu);
-    if (i >= count || begin + i >= total) return;
-    const uint64_t e = all[r * per + 1 + i];
-    score[begin + i] = (int32_t)(uint32_t)e;
-    root[begin + i] = (uint8_t)(e >> 32);
+    if (g == 0) *status = chunk_check(all, per, n, total);
+    if (g < per * n) chunk_unpack_one(all, per, g, total, score, root);
 }
 
 }  // namespace
@@ -116,39 +106,63 @@ using namespace pm;
 
 namespace {
 
-// pm_run on the ctx's shard, then the packed chunk into the gather send buffer (async).
+// The gather buffers: [send chunk | ranks x chunk | status].
+int ensure_gather(pm_ctx* c, int64_t per) {
+    const size_t need = sizeof(uint64_t) * ((size_t)per * (size_t)(c->comm_size + 1) + 1);
+    if (need <= c->gather_bytes) return PM_OK;
+    if (c->gather_buf) (void)hipFree(c->gather_buf);
+    c->gather_buf = nullptr;
+    c->gather_bytes = 0;
+    const hipError_t e = hipMalloc(&c->gather_buf, need);
+    if (e != hipSuccess) return hip_fail(c, e, "gather buffers");
+    c->gather_bytes = need;
+    return PM_OK;
+}
+
+int32_t* gather_status(pm_ctx* c, int64_t per) {
+    return reinterpret_cast<int32_t*>(static_cast<uint64_t*>(c->gather_buf) + (size_t)per * (c->comm_size + 1));
+}
+
+// pm_run on the ctx's shard, record-buffer overflow settled (a re-run with a bigger buffer:
+// the score counts only stored records), then the packed chunk into the send buffer.  On a
+// local failure the chunk carries the failed head instead, so the caller still joins the
+// collective and every rank learns of it from the heads.
 int enqueue_shard(pm_ctx* c, int mode, int64_t total_sites, int64_t site_begin, int64_t per) {
-    if (!c->comm) return fail(c, PM_ERR_STATE, "no communicator: pm_comm_init_rank / pm_comm_init_all first");
-    if (site_begin < 0 || site_begin > UINT32_MAX || c->num_sites > per - 1 ||
-        site_begin + c->num_sites > total_sites)
-        return fail(c, PM_ERR_ARG, "shard outside [0, total_sites) or wider than ceil(total / ranks) + 2");
-    int rc = pm_run(c, mode);
-    if (rc != PM_OK) return rc;
-    const size_t need = sizeof(uint64_t) * (size_t)per * (size_t)(c->comm_size + 1);
-    if (need > c->gather_bytes) {
-        if (c->gather_buf) (void)hipFree(c->gather_buf);
-        c->gather_buf = nullptr;
-        c->gather_bytes = 0;
-        const hipError_t e = hipMalloc(&c->gather_buf, need);
-        if (e != hipSuccess) return hip_fail(c, e, "gather buffers");
-        c->gather_bytes = need;
-    }
-    uint64_t* send = static_cast<uint64_t*>(c->gather_buf);
-    const unsigned blocks = (unsigned)((c->num_sites + kBlock) / kBlock);
-    hipLaunchKernelGGL(k_pack_results, dim3(blocks), dim3(kBlock), 0, c->stream, c->score, c->root_code, site_begin,
-                       c->num_sites, send);
+    int rc = PM_OK;
+    if (site_begin < 0 || site_begin > UINT32_MAX || c->num_sites > per - 1 || site_begin + c->num_sites > total_sites)
+        rc = fail(c, PM_ERR_ARG, "shard outside [0, total_sites) or wider than ceil(total / ranks) + 2");
+    if (rc == PM_OK) rc = pm_run(c, mode);
+    if (rc == PM_OK) rc = settle_run(c);
+    const bool ok = rc == PM_OK;
+    const int64_t count = ok ? c->num_sites : 0;
+    hipLaunchKernelGGL(k_pack_results, dim3((unsigned)((count + kBlock) / kBlock)), dim3(kBlock), 0, c->stream,
+                       ok ? c->score : nullptr, ok ? c->root_code : nullptr, site_begin, count, ok,
+                       static_cast<uint64_t*>(c->gather_buf));
     const hipError_t e = hipGetLastError();
+    if (rc != PM_OK) return rc;
     return e == hipSuccess ? PM_OK : hip_fail(c, e, "pack site results");
 }
 
-int enqueue_unpack(pm_ctx* c, int64_t total_sites, int64_t per, void* score_device, void* root_device) {
-    const uint64_t* recv = static_cast<const uint64_t*>(c->gather_buf) + per;
+int enqueue_unpack(pm_ctx* c, const uint64_t* recv, int64_t total_sites, int64_t per, void* score_device,
+                   void* root_device) {
     const int64_t n = per * c->comm_size;
     hipLaunchKernelGGL(k_unpack_results, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, recv,
                        per, c->comm_size, total_sites, static_cast<int32_t*>(score_device),
-                       static_cast<uint8_t*>(root_device));
+                       static_cast<uint8_t*>(root_device), gather_status(c, per));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PM_OK : hip_fail(c, e, "unpack site results");
+}
+
+// Wait for the unpack and turn its head check into a status (every rank sees the same heads,
+// so every rank returns the same verdict).
+int gathered_status(pm_ctx* c, int64_t per) {
+    int32_t st = 0;
+    hipError_t e = hipMemcpyAsync(&st, gather_status(c, per), sizeof st, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "gather status");
+    if (st > 0) return fail(c, PM_ERR_STATE, "rank " + std::to_string(st - 1) + "'s shard failed");
+    if (st < 0) return fail(c, PM_ERR_ARG, "gathered shards do not tile [0, total_sites) (shard rules differ between ranks)");
+    return PM_OK;
 }
 
 int gather_call(pm_ctx* c, int64_t per) {
@@ -213,13 +227,85 @@ int pm_comm_init_all(pm_ctx* const* ctxs, int n) {
 
 int pm_run_gather(pm_ctx* c, int mode, int64_t total_sites, int64_t site_begin, void* score_device,
                   void* root_device) {
+    // arguments every rank passes alike: a failure here fails every rank the same way
     if (!c || total_sites < 1 || !score_device || !root_device) return PM_ERR_ARG;
+    if (!c->comm) return fail(c, PM_ERR_STATE, "no communicator: pm_comm_init_rank / pm_comm_init_all first");
     (void)hipSetDevice(c->device);
-    const int64_t per = chunk_entries(total_sites, c->comm ? c->comm_size : 1);
-    int rc = enqueue_shard(c, mode, total_sites, site_begin, per);
-    if (rc == PM_OK) rc = gather_call(c, per);
-    if (rc == PM_OK) rc = enqueue_unpack(c, total_sites, per, score_device, root_device);
-    return rc;
+    const int64_t per = chunk_entries(total_sites, c->comm_size);
+    int rc = ensure_gather(c, per);   // (a rank that cannot allocate a few KiB cannot join)
+    if (rc != PM_OK) return rc;
+    // rank-specific work: a failure is carried in this rank's chunk head, the collective joined
+    const int local = enqueue_shard(c, mode, total_sites, site_begin, per);
+    rc = gather_call(c, per);
+    if (rc == PM_OK) rc = enqueue_unpack(c, static_cast<const uint64_t*>(c->gather_buf) + per, total_sites, per,
+                                         score_device, root_device);
+    if (rc == PM_OK) rc = gathered_status(c, per);
+    return local != PM_OK ? local : rc;
+}
+
+int pm_pack_site_results(pm_ctx* c, int64_t site_begin, int64_t per, void* chunk_device) {
+    if (!c || !chunk_device || per < 2) return PM_ERR_ARG;
+    if (!c->ran) return fail(c, PM_ERR_STATE, "nothing ran");
+    (void)hipSetDevice(c->device);
+    int rc = settle_run(c);
+    if (rc != PM_OK) return rc;
+    if (site_begin < 0 || site_begin > UINT32_MAX || c->num_sites > per - 1)
+        return fail(c, PM_ERR_ARG, "shard wider than the chunk (per - 1 sites)");
+    hipLaunchKernelGGL(k_pack_results, dim3((unsigned)((c->num_sites + kBlock) / kBlock)), dim3(kBlock), 0, c->stream,
+                       c->score, c->root_code, site_begin, c->num_sites, true, static_cast<uint64_t*>(chunk_device));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PM_OK : hip_fail(c, e, "pack site results");
+}
+
+int pm_unpack_site_results(pm_ctx* c, const void* all_device, int64_t per, int ranks, int64_t total_sites,
+                           void* score_device, void* root_device) {
+    if (!c || !all_device || per < 2 || ranks < 1 || total_sites < 1 || !score_device || !root_device) return PM_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    int32_t* st = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&st), sizeof(int32_t), c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "unpack status");
+    const int64_t n = per * ranks;
+    hipLaunchKernelGGL(k_unpack_results, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       static_cast<const uint64_t*>(all_device), per, ranks, total_sites,
+                       static_cast<int32_t*>(score_device), static_cast<uint8_t*>(root_device), st);
+    int32_t v = 0;
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(&v, st, sizeof v, hipMemcpyDeviceToHost, c->stream);
+    (void)hipFreeAsync(st, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "unpack site results");
+    if (v > 0) return fail(c, PM_ERR_STATE, "rank " + std::to_string(v - 1) + "'s shard failed");
+    if (v < 0) return fail(c, PM_ERR_ARG, "gathered shards do not tile [0, total_sites)");
+    return PM_OK;
+}
+
+int pm_chunk_entries(int64_t total_sites, int ranks, int64_t* per) {
+    if (total_sites < 1 || ranks < 1 || !per) return PM_ERR_ARG;
+    *per = chunk_entries(total_sites, ranks);
+    return PM_OK;
+}
+
+int pm_chunk_pack(int64_t site_begin, int64_t count, const int32_t* score, const uint8_t* root, int64_t per,
+                  uint64_t* chunk) {
+    if (!chunk || per < 2 || count < 0) return PM_ERR_ARG;
+    if (!score || !root) {   // a failed shard: the head alone
+        chunk[0] = chunk_failed_head();
+        return PM_OK;
+    }
+    if (site_begin < 0 || site_begin > UINT32_MAX || count > per - 1) return PM_ERR_ARG;
+    chunk[0] = chunk_head(site_begin, count);
+    for (int64_t i = 0; i < count; ++i) chunk[1 + i] = chunk_entry(score[i], root[i]);
+    for (int64_t i = count + 1; i < per; ++i) chunk[i] = 0;
+    return PM_OK;
+}
+
+int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_sites, int32_t* score, uint8_t* root) {
+    if (!all || per < 2 || ranks < 1 || total_sites < 1 || !score || !root) return PM_ERR_ARG;
+    const int st = chunk_check(all, per, ranks, total_sites);
+    if (st > 0) return PM_ERR_STATE;
+    if (st < 0) return PM_ERR_ARG;
+    for (int64_t g = 0; g < per * ranks; ++g) chunk_unpack_one(all, per, g, total_sites, score, root);
+    return PM_OK;
 }
 
 int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin, int64_t total_sites,
@@ -237,6 +323,7 @@ int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin
         if (hipMalloc(&out_s[i], sizeof(int32_t) * total_sites) != hipSuccess ||
             hipMalloc(&out_r[i], (size_t)total_sites) != hipSuccess)
             rc = fail(ctxs[i], PM_ERR_OOM, "gathered results");
+        if (rc == PM_OK) rc = ensure_gather(ctxs[i], per);
         if (rc == PM_OK) rc = enqueue_shard(ctxs[i], mode, total_sites, site_begin[i], per);
     }
     if (rc == PM_OK) {   // one process drives every rank: the collective is one RCCL group
@@ -250,7 +337,12 @@ int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin
     }
     for (int i = 0; i < n && rc == PM_OK; ++i) {
         (void)hipSetDevice(ctxs[i]->device);
-        rc = enqueue_unpack(ctxs[i], total_sites, per, out_s[i], out_r[i]);
+        rc = enqueue_unpack(ctxs[i], static_cast<const uint64_t*>(ctxs[i]->gather_buf) + per, total_sites, per,
+                            out_s[i], out_r[i]);
+    }
+    for (int i = 0; i < n && rc == PM_OK; ++i) {
+        (void)hipSetDevice(ctxs[i]->device);
+        rc = gathered_status(ctxs[i], per);
     }
     if (rc == PM_OK) {   // every rank holds the full vectors; hand back rank 0's
         (void)hipSetDevice(ctxs[0]->device);

@@ -105,12 +105,6 @@ __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& 
 }
 
 __device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_t c0) {
-#ifdef PM_EXP_NOWRITE   // timing experiment: edits loaded, not written
-    uint32_t x = 0;
-    for (int j = 0; j < kEditsPerLane; ++j) x ^= r.col[j] ^ r.chr[j] ^ r.node8[j];
-    if (x == 0x9E3779B9u) buf[0] = 1;
-    return;
-#endif
     const int lane = (int)threadIdx.x & (kWave - 1);
     uint64_t pend[kEditsPerLane];
     bool any = false;
@@ -256,11 +250,7 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
     const bool editor = tid < kWave;
     const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
     constexpr bool piped = PIPED;
-#ifdef PM_EXP_NOEDITS   // timing experiment: no edits
-    const int cnt = 0;
-#else
     const int cnt = (int)min((int64_t)kWave, p1 - p0);
-#endif
     // wave 0, piped: this lane's path node's slice bounds for the current tile and ahead
     const int64_t* te = nullptr;
     int64_t te_next = 0, te_next2 = 0;   // this lane's node: slice starts of tiles t+1, t+2
@@ -319,9 +309,6 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
             ch = edit_chunk_from(cnt, te_next, te_next2, tid);
             te_next = te_next2;
             if (t + 3 <= d.tiles) te_next2 = te[t + 3];
-#ifdef PM_EXP_NOROUND   // timing experiment: slice bounds and scan only, no edit gather
-            if (ch.total == 0x7fffffff)
-#endif
             if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
         }
         __syncthreads();

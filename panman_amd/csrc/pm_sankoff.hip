@@ -569,40 +569,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     const int D = (int)down_off.size() - 1;
     const bool dense_all = virt && ht.down_dense_v;
-    // tail chunks beside the remaining levels (PM_OPT_TAIL_OVERLAP; see launch_fitch)
-    const TailDesc* tail_desc = virt ? dt.tail_desc_v : dt.tail_desc;
-    const int32_t tail_total = virt ? ht.num_tail_v : ht.num_tail;
-    const std::vector<int32_t>& tail_off = ht.tail_lvl_off[virt ? 1 : 0];
-    const bool tail_side = !c->profiling && c->tail_chunk > 0;
-    int32_t tail_done = 0;
-    bool tail_forked = false;
-    auto tail_flush = [&](int level_end, bool last) -> hipError_t {
-        const int32_t upto = last ? tail_total : std::min(tail_total, tail_off[level_end]);
-        if (upto <= tail_done || (!last && (!tail_side || (int64_t)(upto - tail_done) * tiles < c->tail_chunk)))
-            return hipSuccess;
-        hipStream_t s = c->stream;
-        if (tail_side) {
-            const hipError_t fe = side_fork(c);
-            if (fe != hipSuccess) return fe;
-            s = c->side;
-            tail_forked = true;
-        }
-        DownArgs t = dn;
-        t.tail = tail_desc + tail_done;
-        t.count = upto - tail_done;
-        tail_done = upto;
-        const dim3 grid = wave_grid(t.count, tiles);
-        if (!tail_side) timer_begin(c, 1);
-        if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, s, t);
-        else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, s, t);
-        if (!tail_side) timer_end(c, 1);
-        return hipSuccess;
-    };
     for (int d = 0; d < D; ++d) {
-        {
-            const hipError_t te = tail_flush(d, false);
-            if (te != hipSuccess) return te;
-        }
         if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {   // PM_OPT_NARROW
             int d1 = d + 1;
             while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
@@ -660,9 +627,18 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         else hipLaunchKernelGGL((k_down<Mode::kSankoff, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
         timer_end(c, 1);
     }
-    hipError_t te = tail_flush(D, true);
-    if (te == hipSuccess && tail_forked) te = side_join(c);
-    if (te != hipSuccess) return te;
+    // children beyond a node's second: one flat launch after the levels (k_tail)
+    const int32_t tail_total = virt ? ht.num_tail_v : ht.num_tail;
+    if (tail_total > 0) {
+        DownArgs t = dn;
+        t.tail = virt ? dt.tail_desc_v : dt.tail_desc;
+        t.count = tail_total;
+        const dim3 grid = wave_grid(t.count, tiles);
+        timer_begin(c, 1);
+        if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, t);
+        else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, t);
+        timer_end(c, 1);
+    }
     return hipGetLastError();
 }
 

@@ -134,6 +134,10 @@ extern "C" int pm_summary_compute(pm_ctx* c, const pm_panmat* p, pm_summary* out
     int64_t dup = 0, trans = 0;
     if (bm_n > 0) {
         std::vector<uint8_t> exists(B, 0), strand(B, 1);
+        // a block's presence before the current node's mutations: `prior` for the blocks
+        // this node touches (first old value), `exists` for the others -- no O(B) copy per node
+        constexpr uint8_t kUntouched = 0xff;
+        std::vector<uint8_t> prior(B, kUntouched);
         struct Frame {
             int32_t v;
             int32_t next_child;
@@ -142,10 +146,10 @@ extern "C" int pm_summary_compute(pm_ctx* c, const pm_panmat* p, pm_summary* out
         std::vector<Frame> st;
         auto enter = [&](int32_t v) {
             Frame f{v, p->child_offsets[v], {}};
-            const std::vector<uint8_t> before = exists;
             for (int64_t k = p->block_mut_offsets[v]; k < p->block_mut_offsets[v + 1]; ++k) {
                 const int32_t b = p->block_mut_primary[k];
                 if (b < 0 || b >= B) continue;
+                if (prior[b] == kUntouched) prior[b] = exists[b];
                 f.undo.emplace_back(b, exists[b], strand[b]);
                 const bool inv = p->block_mut_inversion[k] != 0;
                 if (p->block_mut_info[k]) {
@@ -163,10 +167,12 @@ extern "C" int pm_summary_compute(pm_ctx* c, const pm_panmat* p, pm_summary* out
                 if (!p->block_mut_info[k] || b < 0 || b >= B) continue;
                 for (int32_t d : groups[group_of[b]]) {
                     if (d == b || d < 0 || d >= B) continue;
-                    if (exists[d] && before[d]) { ++dup; break; }
-                    if (!exists[d] && before[d]) { ++trans; break; }
+                    const bool before = prior[d] != kUntouched ? prior[d] != 0 : exists[d] != 0;
+                    if (exists[d] && before) { ++dup; break; }
+                    if (!exists[d] && before) { ++trans; break; }
                 }
             }
+            for (const auto& u : f.undo) prior[std::get<0>(u)] = kUntouched;
             st.push_back(std::move(f));
         };
         enter(p->root);

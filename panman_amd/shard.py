@@ -1,7 +1,8 @@
 """Column sharding across ranks: alignment columns are independent, so
 rank r of W owns sites [r*S//W, (r+1)*S//W); the tree is replicated.  The only exchange
-is one all-gather of the per-site (score, root code) pair; over RCCL (backend "nccl")
-on GPUs, gloo on CPU tensors in the tests.  Mutation records stay per rank and are
+is one all-gather of the per-site (score, root code) pair in the library's chunk layout
+(include/panman_gpu.h, pm_chunk.h); over RCCL inside the library (pm_run_gather) on GPUs,
+or through torch.distributed (gloo on CPU tensors in the tests).  Mutation records stay per rank and are
 merged on the host by (node, site)."""
 from __future__ import annotations
 
@@ -14,23 +15,40 @@ def shard_range(rank: int, world: int, sites: int) -> tuple[int, int]:
     return rank * sites // world, (rank + 1) * sites // world
 
 
-def gather_site_results(score_local: torch.Tensor, root_local: torch.Tensor, sites: int,
-                        group=None) -> tuple[torch.Tensor, torch.Tensor]:
-    """All-gather every rank's (score, root code) shard into full-length vectors."""
+def gather_chunks(chunk: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather one fixed-size chunk (int64 / u64 entries) per rank, rank order."""
     world = dist.get_world_size(group)
-    per = (sites + world - 1) // world
-    dev = score_local.device
-    s_pad = torch.zeros(per, dtype=torch.int32, device=dev)
-    r_pad = torch.full((per,), 255, dtype=torch.uint8, device=dev)
-    s_pad[: score_local.numel()] = score_local
-    r_pad[: root_local.numel()] = root_local
-    s_all = torch.empty(per * world, dtype=torch.int32, device=dev)
-    r_all = torch.empty(per * world, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(s_all, s_pad, group=group)
-    dist.all_gather_into_tensor(r_all, r_pad.view(torch.uint8), group=group)
-    keep = torch.cat([torch.arange(r * per, r * per + (shard_range(r, world, sites)[1] - shard_range(r, world, sites)[0]))
-                      for r in range(world)]).to(dev)
-    return s_all[keep], r_all[keep]
+    out = torch.empty(world * chunk.numel(), dtype=chunk.dtype, device=chunk.device)
+    dist.all_gather_into_tensor(out, chunk.contiguous(), group=group)
+    return out
+
+
+def gather_site_results(score_local, root_local, site_begin: int, sites: int, group=None):
+    """Host tensors (gloo): this rank's (score, root code) shard packed into the library's
+    gather chunk (pm_chunk_pack: head site_begin << 32 | count, one score | root << 32 entry
+    per site), every rank's chunk all-gathered, and unpacked into full-length vectors
+    (pm_chunk_unpack) -- the layout pm_run_gather moves over RCCL."""
+    from .engine import chunk_entries, chunk_pack, chunk_unpack
+    world = dist.get_world_size(group)
+    per = chunk_entries(sites, world)
+    chunk = chunk_pack(site_begin, np.asarray(score_local), np.asarray(root_local), per)
+    allc = gather_chunks(torch.from_numpy(chunk.view(np.int64)), group)
+    s, r = chunk_unpack(allc.numpy().view(np.uint64), per, world, sites)
+    return torch.from_numpy(s), torch.from_numpy(r)
+
+
+def gather_site_results_device(engine, site_begin: int, sites: int, score_all: torch.Tensor,
+                               root_all: torch.Tensor, group=None):
+    """GPU tensors through a torch.distributed collective: the engine's last run packed on the
+    device (pm_pack_site_results), the chunks all-gathered, unpacked on the device
+    (pm_unpack_site_results) into score_all [sites] int32 / root_all [sites] u8."""
+    from .engine import chunk_entries
+    world = dist.get_world_size(group)
+    per = chunk_entries(sites, world)
+    chunk = torch.empty(per, dtype=torch.int64, device=score_all.device)
+    engine.pack_site_results(site_begin, per, chunk.data_ptr())
+    allc = gather_chunks(chunk, group)
+    engine.unpack_site_results(allc.data_ptr(), per, world, sites, score_all.data_ptr(), root_all.data_ptr())
 
 
 def merge_mut_records(parts: list[np.ndarray], site_offsets: list[int]) -> np.ndarray:

@@ -1,8 +1,10 @@
-"""N>1 path on CPU: column shards on 2 / 3 gloo ranks, one all-gather of (score, root code),
-host merge of the records in the C-ABI layout (pm_mut: node, site << 8 | type << 4 | code,
-sites local to the rank's shard, as pm_mutations_fetch returns them) -- must equal the
-single-shard result.  The oracle is the per-shard engine, since this host has no GPU; the
-GPU side of the same path (pm_run_gather over RCCL) is tests/test_gpu_multi.py."""
+"""N>1 path on CPU: column shards on 2 / 3 / 8 gloo ranks, one all-gather of (score, root code)
+carried in the library's gather chunks (pm_chunk_pack -> all_gather -> pm_chunk_unpack, the
+layout pm_run_gather moves over RCCL), host merge of the records in the C-ABI layout (pm_mut:
+node, site << 8 | type << 4 | code, sites local to the rank's shard, as pm_mutations_fetch
+returns them) -- must equal the single-shard result, under both shard rules in use (balanced
+and the MSA driver's even-aligned split).  The oracle is the per-shard engine, since this host
+has no GPU; the GPU side of the same path (pm_run_gather over RCCL) is tests/test_gpu_multi.py."""
 import os
 import socket
 
@@ -30,19 +32,26 @@ def _problem():
     return off, idx, root, codes, cons, node_row, names
 
 
-def _worker(rank, world, port, q):
+def _ranges(rule, world, sites):
+    if rule == "balanced":
+        return [(r * sites // world, (r + 1) * sites // world) for r in range(world)]
+    lo = [min(sites, (sites * g // world + 1) // 2 * 2) for g in range(world)] + [sites]   # pm_msa.cpp
+    return [(lo[g], lo[g + 1]) for g in range(world)]
+
+
+def _worker(rank, world, port, q, rule):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle as orc
-    from panman_amd.shard import gather_site_results, shard_range, to_pm_mut
+    from panman_amd.shard import gather_site_results, to_pm_mut
     off, idx, root, codes, cons, node_row, names = _problem()
-    lo, hi = shard_range(rank, world, codes.shape[1])
+    lo, hi = _ranges(rule, world, codes.shape[1])[rank]
     _, recs, rootc = orc.load().csr_columns(off, idx, root, names, codes[:, lo:hi], node_row, cons[lo:hi],
                                            None, algo=0, threads=2, with_root=True)
     score = np.bincount(recs[recs[:, 0] != root][:, 1], minlength=hi - lo).astype(np.int32)
-    s_all, r_all = gather_site_results(torch.from_numpy(score), torch.from_numpy(rootc), codes.shape[1])
+    s_all, r_all = gather_site_results(score, rootc, lo, codes.shape[1])
     objs = [None] * world
     dist.all_gather_object(objs, (lo, to_pm_mut(recs)))
     if rank == 0:
@@ -59,8 +68,8 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_columns_match_single_shard(world):
+@pytest.mark.parametrize("world,rule", [(2, "balanced"), (3, "balanced"), (3, "even"), (8, "even")])
+def test_sharded_columns_match_single_shard(world, rule):
     import sys
     sys.path.insert(0, ROOT)
     import oracle as orc
@@ -68,7 +77,7 @@ def test_sharded_columns_match_single_shard(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, rule)) for r in range(world)]
     for p in procs:
         p.start()
     s_all, r_all, parts = q.get(timeout=120)

@@ -150,28 +150,3 @@ def test_sankoff_groups_equal_levels(engine, mode, levels, narrow):
     assert w.shape[0] > 0
     assert g.shape == w.shape and (g == w).all()
     assert (gs == ws).all() and (gr == wr).all()
-
-
-@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
-@pytest.mark.parametrize("variant", ["virtual", "leafparent", "plain"])
-@pytest.mark.parametrize("tree", ["sars-like", "random-join"])
-def test_tail_overlap_equal(engine, mode, variant, tree):
-    """PM_OPT_TAIL_OVERLAP: tail chunks on the side stream after every level (chunk 1)
-    give the records of one tail launch after the last level."""
-    off, idx, root = panman_amd.sars_like_tree(4000, seed=51) if tree == "sars-like" else \
-        panman_amd.random_join_tree(5000, seed=52)
-    _variant(engine, variant)
-    engine.tree_upload(off, idx, root)
-    engine.synth_columns(0, 3000, seed=8)
-    res = []
-    try:
-        for chunk in (0, 1):
-            engine.set_tail_overlap(chunk)
-            engine.run(mode)
-            res.append((engine.mutations(),) + tuple(engine.site_results()))
-    finally:
-        engine.set_tail_overlap(0)
-    (w, ws, wr), (g, gs, gr) = res
-    assert w.shape[0] > 0
-    assert g.shape == w.shape and (g == w).all()
-    assert (gs == ws).all() and (gr == wr).all()

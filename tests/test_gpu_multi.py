@@ -1,7 +1,11 @@
 """Multi-GPU column-shard path through the C-ABI (pm_rccl.hip): a
-single-rank RCCL communicator must reproduce pm_run's per-site results exactly, and the
-measurement helpers behind bench.py's roofline must be self-consistent.  (Two or more
-ranks need two GPUs; the gloo tests in test_distributed.py cover the host-side merge.)"""
+single-rank RCCL communicator must reproduce pm_run's per-site results exactly; n = 2, 3, 8
+shards run as separate contexts on this one GPU, packed by the device kernel into the gather
+chunk (pm_pack_site_results), laid side by side as an all-gather leaves them and unpacked on
+the device (pm_unpack_site_results), must reproduce the unsharded run; a record buffer far too
+small is settled before the gather; and the measurement helpers behind bench.py's roofline
+must be self-consistent.  (RCCL across two or more GPUs needs two GPUs; the gloo tests in
+test_distributed.py carry the same chunks through a real all-gather.)"""
 import numpy as np
 import pytest
 import torch
@@ -46,6 +50,76 @@ def test_init_rank_run_gather_equals_run():
     # a shard claiming sites outside the total is refused
     with pytest.raises(panman_amd.PanmanError):
         eng.run_gather(panman_amd.MODE_FITCH, eng.num_sites, 5, s.data_ptr(), r.data_ptr())
+    eng.close()
+
+
+def _ranges(rule, world, sites):
+    if rule == "balanced":
+        return [panman_amd.shard_range_c(r, world, sites) for r in range(world)]
+    lo = [min(sites, (sites * g // world + 1) // 2 * 2) for g in range(world)] + [sites]   # pm_msa.cpp
+    return [(lo[g], lo[g + 1]) for g in range(world)]
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+@pytest.mark.parametrize("world,rule", [(2, "balanced"), (3, "even"), (8, "balanced"), (8, "even")])
+def test_device_chunks_of_shards_equal_one_run(mode, world, rule):
+    leaves, sites, seed = 3000, 4099, 9
+    full = _engine(leaves, sites, seed)
+    full.run(mode)
+    want_score, want_root = full.site_results()
+    want_recs = full.mutations()
+    full.close()
+    per = panman_amd.chunk_entries(sites, world)
+    allc = torch.zeros(per * world, dtype=torch.int64, device="cuda")
+    off, idx, root = panman_amd.random_join_tree(leaves, seed=seed)
+    parts, offsets = [], []
+    for r, (lo, hi) in enumerate(_ranges(rule, world, sites)):
+        eng = panman_amd.Engine(0)
+        eng.tree_upload(off, idx, root)
+        eng.synth_columns(lo, hi - lo, seed=seed + 1)
+        eng.run(mode)
+        eng.pack_site_results(lo, per, allc[r * per:].data_ptr())
+        parts.append(eng.mutations_raw())
+        offsets.append(lo)
+        torch.cuda.synchronize()
+        eng.close()
+    s = torch.full((sites,), -7, dtype=torch.int32, device="cuda")
+    rt = torch.full((sites,), 77, dtype=torch.uint8, device="cuda")
+    helper = _engine(200, 64, 1)
+    helper.unpack_site_results(allc.data_ptr(), per, world, sites, s.data_ptr(), rt.data_ptr())
+    assert (s.cpu().numpy() == want_score).all() and (rt.cpu().numpy() == want_root).all()
+    # a rank whose chunk head says "failed" fails the unpack on every rank
+    allc[per] = 0xffffffff
+    with pytest.raises(panman_amd.PanmanError, match="failed"):
+        helper.unpack_site_results(allc.data_ptr(), per, world, sites, s.data_ptr(), rt.data_ptr())
+    helper.close()
+    from panman_amd.shard import merge_mut_records
+    merged = merge_mut_records(parts, offsets)
+    assert merged.shape[0] == want_recs.shape[0]
+    from panman_amd.shard import to_pm_mut
+    assert (merged == to_pm_mut(want_recs)).all()
+
+
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_tiny_record_buffer_settles_before_gather(mode):
+    eng = _engine(sites=3001)
+    eng.run(mode)
+    want_score, want_root = eng.site_results()
+    want_n = eng.mutation_count()
+    eng.set_record_cap(4)   # 4 records per shard: every run overflows first
+    uid = panman_amd.comm_unique_id()
+    eng.comm_init_rank(uid, 1, 0)
+    s = torch.zeros(eng.num_sites, dtype=torch.int32, device="cuda")
+    r = torch.zeros(eng.num_sites, dtype=torch.uint8, device="cuda")
+    eng.run_gather(mode, eng.num_sites, 0, s.data_ptr(), r.data_ptr())
+    assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()
+    assert eng.mutation_count() == want_n
+    eng.set_record_cap(4)
+    eng.run(mode)
+    s.zero_()
+    eng.site_results_device(s.data_ptr(), r.data_ptr())
+    torch.cuda.synchronize()
+    assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()
     eng.close()
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an experimental variant of the library with extra -D flags:
-#   tools/build_variant.sh NAME "-DPM_EXP_X=1 ..."  ->  build_var/NAME/libpanman_amd.so
+#   tools/build_variant.sh NAME "-DPM_DOWN_WAVES=7 ..."  ->  build_var/NAME/libpanman_amd.so
 # Use it with PANMAN_AMD_LIB=build_var/NAME/libpanman_amd.so python bench.py ...
 set -euo pipefail
 cd "$(dirname "$0")/.."

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into HBM bytes per launch.
 
-Usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON
+Usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON BUILD_ID
   FETCH_DIR / WRITE_DIR: rocprofv3 -d directories (…_counter_collection.csv inside)
-  WORKLOAD_KEY: e.g. 1000000x30000 (leaves x sites-per-GPU), the key bench.py looks up.
+  WORKLOAD_KEY: e.g. fitch:1000000x30000 (mode:leaves x sites-per-GPU), the key bench.py looks up.
+  BUILD_ID: pm_build_id() of the profiled library (bench.py's "build_id"); written beside every
+  entry as "<key>:build", and bench.py reports no traffic when the loaded library differs.
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half of the bytes
 of a wide coalesced 16-B-per-lane stream -> doubled; WRITE_SIZE (KiB) is exact for 16-B
@@ -37,7 +39,7 @@ def per_kernel(d, counter):
 
 
 def main():
-    fetch_dir, write_dir, key, out = sys.argv[1:5]
+    fetch_dir, write_dir, key, out, build = sys.argv[1:6]
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
     res = json.load(open(out)) if os.path.exists(out) else {}
@@ -49,6 +51,7 @@ def main():
         nw, bw = write[k]
         per_launch = 2.0 * bf / nf + bw / nw
         res.setdefault(k, {})[key] = per_launch
+        res[k][key + ":build"] = build
         step = ""
         if runs:
             res[k][key + ":step"] = (2.0 * bf + bw * nf / nw) / runs
