@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU box: every -m gpu test, then the default bench line (driver-style).
+#   tools/gpu_round_check.sh TAG  ->  gpurun_out/gputests_TAG.log, gpurun_out/bench_default_TAG.json
+set -o pipefail
+cd "$(dirname "$0")/.."
+tag=$1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_$tag.log 2>&1 \
+  || { echo "GPU TESTS FAILED"; tail -60 gpurun_out/gputests_$tag.log; exit 1; }
+tail -2 gpurun_out/gputests_$tag.log
+timeout -k 10 900 python bench.py > gpurun_out/bench_default_$tag.json 2> gpurun_out/bench_default_$tag.err \
+  || { echo "bench failed"; tail -20 gpurun_out/bench_default_$tag.err; exit 2; }
+python3 -c "
+import json;d=json.load(open('gpurun_out/bench_default_$tag.json'));r=d['roofline']
+print('N*', round(d['ms_per_step'],3), 'ms', r['kernel'], r['kernel_ms_per_step'], r['other_kernels_ms_per_step'], 'frac', r['frac'], 'traffic', r['traffic'])
+print('cmds', json.dumps(d.get('commands'))[:1500])
+print('replay cpu', json.dumps(d['secondary']['replay']['cpu_baseline'])[:400])
+"
