@@ -88,17 +88,31 @@ __device__ __forceinline__ uint32_t code_at(uint32_t b0, uint32_t b1, uint32_t b
            (((b3 >> bit) & 1u) << 3);
 }
 
-// 64-lane exclusive prefix sum; returns the wave total through `total`.
+// 64-lane inclusive prefix sum by DPP lane moves (no LDS round trips): shifts of 1, 2, 4, 8
+// inside each 16-lane row, then row 0's / rows 0-1's totals broadcast to the rows above
+// (row_bcast:15, row_bcast:31 -- the gfx9 family's DPP broadcasts).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    uint32_t t;
+    t = dpp_mov<0x111>(v); if (r >= 1) v += t;    // row_shr:1
+    t = dpp_mov<0x112>(v); if (r >= 2) v += t;    // row_shr:2
+    t = dpp_mov<0x114>(v); if (r >= 4) v += t;    // row_shr:4
+    t = dpp_mov<0x118>(v); if (r >= 8) v += t;    // row_shr:8
+    t = dpp_mov<0x142>(v); if (lane & 16) v += t; // row_bcast:15 -> rows 1, 3
+    t = dpp_mov<0x143>(v); if (lane >= 32) v += t; // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// 64-lane exclusive prefix sum; returns the wave total through `total`.  Every lane active.
 __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t& total) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    total = __shfl(x, 63, 64);
-    return x - v;
+    const uint32_t incl = wave_inclusive_scan(v);
+    total = __builtin_amdgcn_readlane(incl, 63);
+    return incl - v;
 }
 
 }  // namespace pm

@@ -72,6 +72,7 @@ void free_tree(DevTree& t) {
     dev_free(t.vleaf);
     dev_free(t.part_desc);
     dev_free(t.part_desc_v);
+    dev_free(t.part_desc_k);
     dev_free(t.child_enc_k);
     dev_free(t.up_desc_k);
     dev_free(t.up_desc_g);
@@ -167,7 +168,8 @@ int alloc_work(pm_ctx* c, int mode) {
     }
     if (!fitch) {   // Sankoff nodes of out-degree > 255: part counters
         const size_t parts = (size_t)std::max(c->ht.part_off.empty() ? 0 : c->ht.part_off.back(),
-                                              c->ht.part_off_v.empty() ? 0 : c->ht.part_off_v.back());
+                                              std::max(c->ht.part_off_v.empty() ? 0 : c->ht.part_off_v.back(),
+                                                       c->ht.part_off_k.empty() ? 0 : c->ht.part_off_k.back()));
         const size_t need = parts * kPartPlanes * wpad * sizeof(uint32_t);
         if (need > c->sk_parts_bytes) {
             dev_free(c->sk_parts);
@@ -962,10 +964,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
-    std::vector<PartDesc> part_desc[2];
-    for (int v = 0; v < 2; ++v) {
-        const std::vector<NodeDesc>& ud = v ? up_desc_v : up_desc;
-        std::vector<int32_t>& po = v ? ht.part_off_v : ht.part_off;
+    std::vector<PartDesc> part_desc[3];
+    for (int v = 0; v < 3; ++v) {
+        const std::vector<NodeDesc>& ud = v == 2 ? up_desc_k : v ? up_desc_v : up_desc;
+        std::vector<int32_t>& po = v == 2 ? ht.part_off_k : v ? ht.part_off_v : ht.part_off;
         po.assign(ud.size() + 1, 0);
         ht.up_degree[v].assign(ud.size(), 0);
         for (size_t k = 0; k < ud.size(); ++k) {
@@ -976,9 +978,11 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             po[k + 1] = po[k] + np;
         }
     }
-    std::vector<NodeDesc> up_desc_p = up_desc, up_desc_vp = up_desc_v;   // pad0 = first part
+    // pad0 = the first part (Sankoff up descriptors; the Fitch level kernels do not read it)
+    std::vector<NodeDesc> up_desc_p = up_desc, up_desc_vp = up_desc_v, up_desc_kp = up_desc_k;
     for (size_t k = 0; k < up_desc_p.size(); ++k) up_desc_p[k].pad0 = ht.part_off[k];
     for (size_t k = 0; k < up_desc_vp.size(); ++k) up_desc_vp[k].pad0 = ht.part_off_v[k];
+    for (size_t k = 0; k < up_desc_kp.size(); ++k) up_desc_kp[k].pad0 = ht.part_off_k[k];
     upload_phase("parts");
     std::vector<int32_t> lvl;
     {
@@ -1024,8 +1028,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
         (e = upload(&dt.part_desc, part_desc[0], c->stream)) != hipSuccess ||
         (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess ||
+        (e = upload(&dt.part_desc_k, part_desc[2], c->stream)) != hipSuccess ||
         (e = upload(&dt.child_enc_k, child_enc_k, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_k, up_desc_k, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_k, up_desc_kp, c->stream)) != hipSuccess ||
         (e = upload(&dt.up_desc_g, up_desc_g, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||

@@ -111,6 +111,7 @@ struct DevTree {
     // Sankoff parts of the nodes of out-degree > 255 ([0] over child_enc, [1] over child_enc_v)
     PartDesc* part_desc = nullptr;
     PartDesc* part_desc_v = nullptr;
+    PartDesc* part_desc_k = nullptr;   // subtree form (Sankoff)
     // subtree form (Fitch, all leaves present): S2 / S3 nodes inline in their parent too
     int32_t* child_enc_k = nullptr;   // [E] shapes in bits 28-29
     NodeDesc* up_desc_k = nullptr;
@@ -150,9 +151,9 @@ struct HostTree {
     bool down_dense_v = false;            // down_order_v[k] == k (dense order = pre-order levels)
     int32_t num_tail = 0, num_tail_v = 0;
     // Sankoff parts: prefix over the up-order descriptors ([I'+1]; nodes of out-degree <= 255
-    // have none) of each form, and every descriptor's out-degree ([0] plain, [1] virtual form)
-    std::vector<int32_t> part_off, part_off_v;
-    std::vector<int32_t> up_degree[2];
+    // have none) of each form, and every descriptor's out-degree
+    std::vector<int32_t> part_off, part_off_v, part_off_k;
+    std::vector<int32_t> up_degree[3];   // [0] plain, [1] leaf-parent form, [2] subtree form
     // subtree form: levels without the S2 / S3 nodes, each pre-order level's first dense index
     std::vector<int32_t> up_level_off_k, up_class_off_k, down_level_off_k, down_dense_base_k;
     std::vector<uint8_t> up_leafy_k;

@@ -661,82 +661,111 @@ __device__ __forceinline__ uint32_t leaf_diff(const Args& a, int32_t leaf, int64
     return m & ((L.x ^ F[0]) | (L.y ^ F[1]) | (L.z ^ F[2]) | (L.w ^ F[3]));
 }
 
-// Record sinks.  A wave's records are first staged in LDS (positions from an LDS counter,
-// so children are processed in one pass with no re-reads); the wave then reserves global
-// space with one atomic and copies them out.  If a wave has more than kStage records the
-// pass is redone writing straight to the reserved global range (rare).
-constexpr uint32_t kStage = 512;   // records per wave (4 KiB of LDS)
-
-struct LdsSink {
-    pm_mut* buf;
-    uint32_t* cnt;
-    __device__ __forceinline__ uint32_t reserve(uint32_t k) const { return atomicAdd(cnt, k); }
-    __device__ __forceinline__ void put(uint32_t p, pm_mut m) const {
-        if (p < kStage) buf[p] = m;
-    }
-};
-
-struct GlobalSink {
-    pm_mut* out;
-    int64_t base, cap;
-    uint32_t* cnt;   // the wave's LDS counter, reset to 0
-    __device__ __forceinline__ uint32_t reserve(uint32_t k) const { return atomicAdd(cnt, k); }
-    __device__ __forceinline__ void put(uint32_t p, pm_mut m) const {
-        if (base + p < cap) out[base + p] = m;
-    }
-};
-
-// One record per changed site (src/fitchSankoff.cpp:140-166): parent gap -> NI,
-// child gap -> ND (char '-', code 0), else NS; NI/NS carry the child's code.  Written at
-// positions p, p+1, ... of the sink (p advanced).
-// The record's low byte, (type << 4) | code, comes from six bit-planes computed for all 32
-// sites at once: the child's code planes (an ND child has code 0, the '-' record code),
-// ND = parent not gap & child gap, NI = parent gap (PM_MUT_ND = 1, PM_MUT_NI = 2).
+// Mutation records (src/fitchSankoff.cpp:140-166, :676-703): one per changed site --
+// parent gap -> NI, child gap -> ND (char '-', code 0), else NS; NI / NS carry the child's
+// code.  The record's low byte, (type << 4) | code, is the child's code with ND = parent not
+// gap & child gap, NI = parent gap (PM_MUT_ND = 1, PM_MUT_NI = 2).
+//
+// Emission by entries.  A record stream is one node's 32-site word: the mask D of sites where
+// its final differs from its parent's, its 4 code planes and its parent's gap plane.  Each
+// stream is staged in the wave's LDS area as a 32-B entry -- lanes with D != 0 packed by rank
+// (ballot + mbcnt), no per-lane loop while staging -- and a flush reserves the wave's records
+// in a shard with one global atomic, then expands the entries one per lane, every lane busy
+// whichever lanes the records came from, straight into the reserved range.
 static_assert(PM_MUT_NS == 0 && PM_MUT_ND == 1 && PM_MUT_NI == 2, "record type bits");
 __device__ __forceinline__ uint32_t bit_at(uint32_t plane, int b) { return __builtin_amdgcn_ubfe(plane, b, 1); }
 
-// A lane whose word holds more than kHeavyBits records (an N run at a leaf, a gap) is
-// expanded by 32 lanes at once; the others write theirs one per loop iteration, so the
-// wave's trip count is at most kHeavyBits plus one per heavy lane instead of the largest
-// per-lane count (up to 32).  Positions p .. p + popc(diff) - 1 were reserved by the lane.
-// Called with every lane of the wave active (lanes 0-31 write a heavy lane's records).
+constexpr uint32_t kEntryCap = 128;          // staged entries per wave (4 KiB of LDS)
+constexpr int kEntryQuads = 2 * kEntryCap;   // entry k = quads 2k {D, node, site0, parent gap}, 2k+1 {code planes}
+
+struct Emit {
+    uint4* lds;       // the wave's kEntryQuads
+    uint32_t shard;   // record shard this wave appends to
+    uint32_t n;       // staged entries (wave-uniform)
+    uint32_t cnt;     // records of this lane's staged entries
+};
+
+// low byte of the record at bit b of an entry
+__device__ __forceinline__ uint32_t rec_low(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t pz, int b) {
+    const uint32_t code = bit_at(c0, b) | (bit_at(c1, b) << 1) | (bit_at(c2, b) << 2) | (bit_at(c3, b) << 3);
+    const uint32_t z = bit_at(pz, b);
+    return code | ((uint32_t)(code == 0 && z == 0) << 4) | (z << 5);
+}
+
+// An entry whose word holds more than kHeavyBits records (an N run at a leaf, a gap) is
+// expanded by 32 lanes at once; the others write theirs one per loop iteration, so a round's
+// trip count is at most kHeavyBits plus one per heavy entry instead of the largest count (32).
 constexpr int kHeavyBits = 4;
 
-template <class Sink>
-__device__ __forceinline__ void put_records(const Sink& sink, uint32_t& p, uint32_t node, uint32_t diff, int64_t word,
-                                            const uint32_t* pc, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    if (__ballot(diff != 0) == 0) return;
-    const uint32_t pz = ~(pc[0] | pc[1] | pc[2] | pc[3]);
-    const uint32_t nd = ~pz & ~(c0 | c1 | c2 | c3);
-    const uint32_t site0 = (uint32_t)(word * 32);
-    const uint32_t nbits = (uint32_t)__builtin_popcount(diff);
-    const bool heavy = nbits > (uint32_t)kHeavyBits;
-    uint32_t d = heavy ? 0u : diff, q = p;
-    while (d) {
-        const int b = __builtin_ctz(d);
-        d &= d - 1;
-        const uint32_t low = bit_at(c0, b) | (bit_at(c1, b) << 1) | (bit_at(c2, b) << 2) | (bit_at(c3, b) << 3) |
-                             (bit_at(nd, b) << 4) | (bit_at(pz, b) << 5);
-        sink.put(q++, pm_mut{node, ((site0 + (uint32_t)b) << 8) | low});
-    }
-    uint64_t hv = __ballot(heavy);
-    const int lane = threadIdx.x & 63, j = lane & 31;
-    while (hv) {
-        const int l = __builtin_ctzll(hv);
-        hv &= hv - 1;
-        const uint32_t w = __builtin_amdgcn_readlane(diff, l);
-        const uint32_t h0 = __builtin_amdgcn_readlane(c0, l), h1 = __builtin_amdgcn_readlane(c1, l),
-                       h2 = __builtin_amdgcn_readlane(c2, l), h3 = __builtin_amdgcn_readlane(c3, l),
-                       hn = __builtin_amdgcn_readlane(nd, l), hz = __builtin_amdgcn_readlane(pz, l),
-                       hs = __builtin_amdgcn_readlane(site0, l), hp = __builtin_amdgcn_readlane(p, l);
-        if (lane < 32 && ((w >> j) & 1u)) {
-            const uint32_t low = bit_at(h0, j) | (bit_at(h1, j) << 1) | (bit_at(h2, j) << 2) | (bit_at(h3, j) << 3) |
-                                 (bit_at(hn, j) << 4) | (bit_at(hz, j) << 5);
-            sink.put(hp + __builtin_amdgcn_mbcnt_lo(w, 0u), pm_mut{node, ((hs + (uint32_t)j) << 8) | low});
+template <class Args>
+__device__ __forceinline__ void emit_flush(const Args& a, Emit& em, int lane) {
+    if (em.n == 0) return;
+    uint32_t total;
+    (void)wave_exclusive_scan(em.cnt, total);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.shard_cnt[em.shard], total);
+    base = __builtin_amdgcn_readfirstlane(base);
+    pm_mut* out = a.recs + (size_t)em.shard * a.shard_cap;
+    const int64_t cap = a.shard_cap;
+    for (uint32_t r0 = 0; r0 < em.n; r0 += kWave) {
+        const uint32_t j = r0 + (uint32_t)lane;
+        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
+        if (j < em.n) {
+            e0 = em.lds[2 * j];
+            e1 = em.lds[2 * j + 1];
         }
+        const uint32_t D = e0.x, node = e0.y, site0 = e0.z, pz = e0.w;
+        const uint32_t c = (uint32_t)__builtin_popcount(D);
+        uint32_t tot;
+        const uint32_t p0 = base + wave_exclusive_scan(c, tot);
+        const bool heavy = c > (uint32_t)kHeavyBits;
+        uint32_t d = heavy ? 0u : D, p = p0;
+        while (d) {
+            const int b = __builtin_ctz(d);
+            d &= d - 1;
+            if ((int64_t)p < cap) out[p] = pm_mut{node, ((site0 + (uint32_t)b) << 8) | rec_low(e1.x, e1.y, e1.z, e1.w, pz, b)};
+            ++p;
+        }
+        uint64_t hv = __ballot(heavy);
+        const int bit = lane & 31;
+        while (hv) {
+            const int l = __builtin_ctzll(hv);
+            hv &= hv - 1;
+            const uint32_t w = __builtin_amdgcn_readlane(D, l);
+            const uint32_t h0 = __builtin_amdgcn_readlane(e1.x, l), h1 = __builtin_amdgcn_readlane(e1.y, l),
+                           h2 = __builtin_amdgcn_readlane(e1.z, l), h3 = __builtin_amdgcn_readlane(e1.w, l),
+                           hz = __builtin_amdgcn_readlane(pz, l), hs = __builtin_amdgcn_readlane(site0, l),
+                           hn = __builtin_amdgcn_readlane(node, l), hp = __builtin_amdgcn_readlane(p0, l);
+            if (lane < 32 && ((w >> bit) & 1u)) {
+                const uint32_t q = hp + __builtin_amdgcn_mbcnt_lo(w, 0u);
+                if ((int64_t)q < cap) out[q] = pm_mut{hn, ((hs + (uint32_t)bit) << 8) | rec_low(h0, h1, h2, h3, hz, bit)};
+            }
+        }
+        base += tot;
     }
-    p += nbits;
+    em.n = 0;
+    em.cnt = 0;
 }
+
+// Stage one stream: node id (wave-uniform), diff mask D, the child's code planes c, the
+// parent's code planes pc.  Every lane of the wave calls it.
+template <class Args>
+__device__ __forceinline__ void emit_stream(const Args& a, Emit& em, int lane, uint32_t node, uint32_t D, uint32_t site0,
+                                            uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const uint32_t* pc) {
+    const uint64_t m = __ballot(D != 0);
+    if (m == 0) return;
+    const uint32_t k = (uint32_t)__builtin_popcountll(m);
+    if (em.n + k > kEntryCap) emit_flush(a, em, lane);
+    if (D) {
+        const uint32_t at = em.n + lanes_below(m);
+        em.lds[2 * at] = make_uint4(D, node, site0, ~(pc[0] | pc[1] | pc[2] | pc[3]));
+        em.lds[2 * at + 1] = make_uint4(c0, c1, c2, c3);
+        em.cnt += (uint32_t)__builtin_popcount(D);
+    }
+    em.n += k;
+}
+
+__device__ __forceinline__ uint32_t shard_of(uint32_t salt, int tile) { return (salt * 31u + (uint32_t)tile * 7919u) % kShards; }
 
 // A leaf word for emission: its code planes L and the mask of sites where it can carry a
 // mutation (leaf_diff's rules: absent leaves none -- or, block Sankoff, state 0 everywhere;
@@ -771,7 +800,8 @@ __device__ __forceinline__ uint32_t diff4(const uint4& L, const uint32_t* F) {
 }
 
 // One of the first two children of a node, fetched before the node's own state is known
-// (leaf: its word; virtual leaf-parent: its first two leaves' words).
+// (leaf: its word; virtual leaf-parent: its first two leaves' words), with the caller node
+// ids its records carry (id0: the child; id1, id2: a virtual child's leaves).
 struct Kid {
     int32_t enc = 0;
     int4 vl = make_int4(-1, -1, -1, -1);
@@ -780,6 +810,7 @@ struct Kid {
     // subtree form (S2 / S3 child): third and fourth leaf, node ids of its cherries
     uint4 L2 = make_uint4(0, 0, 0, 0), L3 = make_uint4(0, 0, 0, 0);
     int32_t ix = -1, iy = -1;
+    uint32_t id0 = 0, id1 = 0, id2 = 0;
 };
 
 __device__ __forceinline__ int kid_shape(int32_t enc) { return enc >= 0 && (enc & kVirtualBit) ? (enc >> kShapeShift) & 3 : 0; }
@@ -789,17 +820,24 @@ __device__ __forceinline__ int kid_shape(int32_t enc) { return enc >= 0 && (enc 
 // Loads are written as "initialise, then exec-masked load" with the leaf choice made on
 // uniform values first: zero-filling a load's registers on a sibling branch instead makes
 // the compiler drain every outstanding load (s_waitcnt vmcnt(0)) between the fetches.
-template <Mode M, bool AP, bool SUB = false>
+// IDS: load the records' node ids (uniform scalar loads, in flight with the words).
+template <Mode M, bool AP, bool SUB = false, bool IDS = true>
 __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 vl, int64_t word, bool dirty, Kid& k) {
     k.enc = enc;
     int32_t l0 = -1, l1 = -1;
     if (enc < 0) {
         l0 = -enc - 1;
+        if (IDS) k.id0 = (uint32_t)a.leaf_id[l0];
     } else if (M != Mode::kBlockFitch && (enc & kVirtualBit)) {
         k.vl = make_int4(__builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y),
                          __builtin_amdgcn_readfirstlane(vl.z), __builtin_amdgcn_readfirstlane(vl.w));
         l0 = k.vl.x;
         l1 = k.vl.y;
+        if (IDS) {
+            k.id0 = (uint32_t)a.internal_id[enc & kDenseMask];
+            k.id1 = (uint32_t)a.leaf_id[l0];
+            if (l1 >= 0) k.id2 = (uint32_t)a.leaf_id[l1];
+        }
     }
     k.L0 = k.L1 = make_uint4(0, 0, 0, 0);
     k.m0 = k.m1 = 0;
@@ -837,21 +875,6 @@ __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint
     have |= m;
 }
 
-// What a child of a node with final codes Fn records: a leaf its changed sites (d0); a
-// virtual child (one or two leaves, prefetched) its final F, its own changed sites
-// (self, against Fn) and its leaves' (d0, d1, against F).  A virtual child's final:
-//   Fitch   (src/fitchSankoff.cpp:115-123 on the union set): Fn if among the leaves'
-//           codes, else the lowest of them.
-//   Sankoff (:513-530): the optimal codes are the present leaves' codes; every other code
-//           is one above optimal unless both leaves are present with one code (then two
-//           above).  So Fn wins if among the leaves' codes, otherwise the lowest of them
-//           and -- when Fn is one above optimal -- Fn (ties go to the lowest index).
-struct KidOut {
-    uint32_t F[4];
-    uint32_t self, d0, d1;
-    uint32_t nsub;   // subtree form: records of an S2 / S3 child's subtree (rebuilt by kid_put)
-};
-
 __device__ __forceinline__ uint4 sel4(uint32_t t, const uint4& p, const uint4& q) {
     return make_uint4(bsel(t, p.x, q.x), bsel(t, p.y, q.y), bsel(t, p.z, q.z), bsel(t, p.w, q.w));
 }
@@ -865,8 +888,6 @@ __device__ __forceinline__ uint4 min4(const uint4& p, const uint4& q) {   // low
 //   S2 (x = (a, b), c): S_v = {c} if c in {a, b}, else {a, b, c};
 //   S3 (x = (a, b), y = (c, d)): S_v = X & Y if the cherries share a code, else X | Y.
 //   F_v = P if P in S_v else lowest(S_v);  F_x = F_v if F_v in {a, b} else min(a, b); F_y alike.
-// Nothing is kept between counting and writing the records: both recompute from the leaves
-// (VALU is cheaper here than the registers that would hold the finals and masks).
 struct SubFinals {
     uint4 F, G, H;
 };
@@ -893,60 +914,92 @@ __device__ __forceinline__ SubFinals subtree_finals(const Kid& k, int sh, const 
     return r;
 }
 
-// Records of an S2 / S3 subtree per lane: v, x, (y,) a, b, c, (d).
-__device__ __forceinline__ uint32_t subtree_count(const Kid& k, int sh, uint32_t valid, const uint4& P) {
-    const SubFinals f = subtree_finals(k, sh, P);
-    const uint32_t M = valid & k.m0;
-    uint32_t n = __builtin_popcount(M & code_ne(f.F, P)) + __builtin_popcount(M & code_ne(f.G, f.F)) +
-                 __builtin_popcount(M & code_ne(k.L0, f.G)) + __builtin_popcount(M & code_ne(k.L1, f.G)) +
-                 __builtin_popcount(M & code_ne(k.L2, f.H));
-    if (sh == 2) n += __builtin_popcount(M & code_ne(f.H, f.F)) + __builtin_popcount(M & code_ne(k.L3, f.H));
-    return n;
+// Sankoff finals inside an S2 / S3 child v given its parent's final P (src/fitchSankoff.cpp:
+// 487-531 at v, then at its cherries, unit costs; leaves keep their codes).  Z0 = codes of
+// the maximum child count, Z1 = one below it (see pm_sankoff.hip):
+//   cherry x = (a, b): a == b: Z0 = {a}, Z1 = {};  else Z0 = {a, b}, Z1 = every other code.
+//   v = (x, y): X & Y != {} ? Z0 = X & Y, Z1 = X ^ Y : Z0 = X | Y, Z1 = every other code
+//   (S2: y = {c}).  A node's final: P if P in Z0, else the lowest of Z0 -- or P when P is in
+//   Z1 and below that lowest code (ties go to the lowest index).
+__device__ __forceinline__ uint4 cherry_final_sankoff(const uint4& A, const uint4& B, const uint4& F) {
+    const uint4 mab = min4(A, B);
+    const uint4 open = sel4(~code_ne(F, A) | ~code_ne(F, B), F, min4(mab, F));   // a != b: Z1 = the rest
+    return sel4(~code_ne(A, B), A, open);
 }
 
-// One record stream per iteration (v, x, a, b, c[, y, d]): a single put_records body serves
-// them all, selected by the wave-uniform stream index.
-template <class Sink>
-__device__ __forceinline__ void subtree_put(const TailDesc& t, const Sink& sink, uint32_t& p, const Kid& k, int sh,
-                                            uint32_t valid, const uint32_t* Fn, int64_t word) {
+__device__ __forceinline__ SubFinals subtree_finals_sankoff(const Kid& k, int sh, const uint4& P) {
+    const uint4 A = k.L0, B = k.L1, Cc = k.L2;
+    const uint4 mab = min4(A, B);
+    const uint32_t pX = ~code_ne(P, A) | ~code_ne(P, B);
+    SubFinals r;
+    if (sh == 1) {
+        const uint32_t inx = ~code_ne(Cc, A) | ~code_ne(Cc, B);
+        // c in X: Z0 = {c}, Z1 = X \ {c};  else Z0 = {a, b, c}, Z1 = the rest
+        const uint4 f_in = sel4(pX & code_less(&P.x, &Cc.x), P, Cc);
+        const uint4 f_out = sel4(pX | ~code_ne(P, Cc), P, min4(min4(mab, Cc), P));
+        r.F = sel4(inx, f_in, f_out);
+        r.H = r.F;
+    } else {
+        const uint4 D = k.L3;
+        const uint4 mcd = min4(Cc, D);
+        const uint32_t ia = ~code_ne(A, Cc) | ~code_ne(A, D), ib = ~code_ne(B, Cc) | ~code_ne(B, D), nz = ia | ib;
+        const uint32_t pY = ~code_ne(P, Cc) | ~code_ne(P, D);
+        const uint32_t p_z0 = (~code_ne(P, A) & ia) | (~code_ne(P, B) & ib);
+        const uint4 low = sel4(ia & ib, mab, sel4(ia, A, B));
+        const uint4 f_nz = sel4(p_z0 | ((pX ^ pY) & code_less(&P.x, &low.x)), P, low);
+        const uint4 f_z = sel4(pX | pY, P, min4(min4(mab, mcd), P));
+        r.F = sel4(nz, f_nz, f_z);
+        r.H = cherry_final_sankoff(Cc, D, r.F);
+    }
+    r.G = cherry_final_sankoff(A, B, r.F);
+    return r;
+}
+
+template <class Args>
+__device__ __forceinline__ void emit_code(const Args& a, Emit& em, int lane, uint32_t node, uint32_t D, uint32_t site0,
+                                          const uint4& c, const uint4& pc) {
+    const uint32_t p4[4] = {pc.x, pc.y, pc.z, pc.w};
+    emit_stream(a, em, lane, node, D, site0, c.x, c.y, c.z, c.w, p4);
+}
+
+// Records of an S2 / S3 subtree: v, x, a, b, c (S2: c under v) [, y, d]; ids = the
+// child's node id, then its leaves' (id[1..4]), cherries ix / iy.
+template <Mode M, class Args>
+__device__ __forceinline__ void subtree_emit(const Args& a, Emit& em, int lane, const int32_t* id, int32_t ix, int32_t iy,
+                                             const Kid& k, int sh, uint32_t valid, const uint32_t* Fn, uint32_t site0) {
     const uint4 P = make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]);
-    const SubFinals f = subtree_finals(k, sh, P);
-    const uint32_t M = valid & k.m0;
-    const int streams = sh == 1 ? 5 : 7;
-#pragma unroll 1
-    for (int st = 0; st < streams; ++st) {
-        uint4 pc = P, cc = f.F;
-        int32_t node = t.id[0];
-        switch (st) {
-            case 1: node = t.ix; pc = f.F; cc = f.G; break;
-            case 2: node = t.id[1]; pc = f.G; cc = k.L0; break;
-            case 3: node = t.id[2]; pc = f.G; cc = k.L1; break;
-            case 4: node = t.id[3]; pc = sh == 1 ? f.F : f.H; cc = k.L2; break;
-            case 5: node = t.iy; pc = f.F; cc = f.H; break;
-            case 6: node = t.id[4]; pc = f.H; cc = k.L3; break;
-            default: break;
-        }
-        const uint32_t pcs[4] = {pc.x, pc.y, pc.z, pc.w};
-        put_records(sink, p, (uint32_t)node, M & code_ne(cc, pc), word, pcs, cc.x, cc.y, cc.z, cc.w);
+    const SubFinals f = M == Mode::kSankoff ? subtree_finals_sankoff(k, sh, P) : subtree_finals(k, sh, P);
+    const uint32_t msk = valid & k.m0;
+    emit_code(a, em, lane, (uint32_t)id[0], msk & code_ne(f.F, P), site0, f.F, P);
+    emit_code(a, em, lane, (uint32_t)ix, msk & code_ne(f.G, f.F), site0, f.G, f.F);
+    emit_code(a, em, lane, (uint32_t)id[1], msk & code_ne(k.L0, f.G), site0, k.L0, f.G);
+    emit_code(a, em, lane, (uint32_t)id[2], msk & code_ne(k.L1, f.G), site0, k.L1, f.G);
+    const uint4 pc = sh == 1 ? f.F : f.H;
+    emit_code(a, em, lane, (uint32_t)id[3], msk & code_ne(k.L2, pc), site0, k.L2, pc);
+    if (sh == 2) {
+        emit_code(a, em, lane, (uint32_t)iy, msk & code_ne(f.H, f.F), site0, f.H, f.F);
+        emit_code(a, em, lane, (uint32_t)id[4], msk & code_ne(k.L3, f.H), site0, k.L3, f.H);
     }
 }
 
-template <Mode M, bool SUB = false>
-__device__ __forceinline__ void kid_prepare(const Kid& k, uint32_t valid, const uint32_t* Fn, KidOut& o) {
-    o.self = o.d0 = o.d1 = 0;
-    if constexpr (SUB) o.nsub = 0;
+// What a child of a node with final codes Fn records: a leaf its changed sites; a virtual
+// child (one or two leaves, prefetched) its final F, its own changed sites (against Fn) and
+// its leaves' (against F).  A virtual child's final:
+//   Fitch   (src/fitchSankoff.cpp:115-123 on the union set): Fn if among the leaves'
+//           codes, else the lowest of them.
+//   Sankoff (:513-530): the optimal codes are the present leaves' codes; every other code
+//           is one above optimal unless both leaves are present with one code (then two
+//           above).  So Fn wins if among the leaves' codes, otherwise the lowest of them
+//           and -- when Fn is one above optimal -- Fn (ties go to the lowest index).
+// ids: the child's id, then its leaves'.
+template <Mode M, class Args>
+__device__ __forceinline__ void kid_emit(const Args& a, Emit& em, int lane, const Kid& k, uint32_t id0, uint32_t id1,
+                                         uint32_t id2, uint32_t valid, const uint32_t* Fn, uint32_t site0) {
     if (k.enc < 0) {
-        o.d0 = valid & k.m0 & diff4(k.L0, Fn);
+        emit_stream(a, em, lane, id0, valid & k.m0 & diff4(k.L0, Fn), site0, k.L0.x, k.L0.y, k.L0.z, k.L0.w, Fn);
         return;
     }
     if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
-    if constexpr (SUB) {
-        const int sh = kid_shape(k.enc);
-        if (sh) {
-            o.nsub = subtree_count(k, sh, valid, make_uint4(Fn[0], Fn[1], Fn[2], Fn[3]));
-            return;
-        }
-    }
     uint32_t low[4] = {0, 0, 0, 0}, have = 0, hit = 0;
     virt_fold(k.L0, k.m0, Fn, low, have, hit);
     virt_fold(k.L1, k.m1, Fn, low, have, hit);
@@ -959,65 +1012,14 @@ __device__ __forceinline__ void kid_prepare(const Kid& k, uint32_t valid, const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) low[j] = bsel(take, Fn[j], low[j]);
     }
+    uint32_t F[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o.F[j] = bsel(hit, Fn[j], low[j]);
-    o.self = have & valid & ((o.F[0] ^ Fn[0]) | (o.F[1] ^ Fn[1]) | (o.F[2] ^ Fn[2]) | (o.F[3] ^ Fn[3]));
-    o.d0 = valid & k.m0 & diff4(k.L0, o.F);
-    o.d1 = valid & k.m1 & diff4(k.L1, o.F);
-}
-
-template <bool SUB = false>
-__device__ __forceinline__ uint32_t kid_count(const KidOut& o) {
-    uint32_t n = (uint32_t)(__builtin_popcount(o.self) + __builtin_popcount(o.d0) + __builtin_popcount(o.d1));
-    if constexpr (SUB) n += o.nsub;
-    return n;
-}
-
-template <Mode M, class Sink>
-__device__ __forceinline__ void kid_put(const DownArgs& a, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
-                                        int64_t word, const uint32_t* Fn) {
-    if (k.enc < 0) {
-        put_records(sink, p, (uint32_t)a.leaf_id[-k.enc - 1], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
-        return;
-    }
-    if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
-    put_records(sink, p, (uint32_t)a.internal_id[k.enc & kDenseMask], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
-    put_records(sink, p, (uint32_t)a.leaf_id[k.vl.x], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
-    if (k.vl.y >= 0) put_records(sink, p, (uint32_t)a.leaf_id[k.vl.y], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
-}
-
-// Every record of node n's wave: the node itself and its first two children (prefetched
-// in registers), all counted first so each lane reserves its sink range once.  Leaf /
-// virtual children beyond the second are k_tail's items.
-template <Mode M, bool AP, class Sink>
-__device__ __forceinline__ void node_records(const DownArgs& a, const Sink& sink, int32_t n, int32_t e0, int32_t e1,
-                                             const Kid* kids, int64_t word, uint32_t valid, const uint32_t* pc,
-                                             const uint32_t* F, uint32_t self_diff) {
-    KidOut o0, o1;
-    kid_prepare<M>(kids[0], valid, F, o0);
-    const bool two = e1 - e0 > 1;
-    if (two) kid_prepare<M>(kids[1], valid, F, o1);
-    else o1.self = o1.d0 = o1.d1 = 0;
-    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count(o0) + kid_count(o1);
-    uint32_t p = cnt ? sink.reserve(cnt) : 0u;   // every lane stays active (put_records expands cooperatively)
-    put_records(sink, p, (uint32_t)a.internal_id[n], self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M>(a, sink, p, kids[0], o0, word, F);
-    if (two) kid_put<M>(a, sink, p, kids[1], o1, word, F);
-}
-
-// Move a wave's staged records to one of the kShards record shards (one global atomic);
-// returns false, with the reserved base in `base`, when the stage overflowed and the
-// caller must redo its records into global memory.
-__device__ __forceinline__ bool flush_stage(const DownArgs& a, const pm_mut* stage, uint32_t total, uint32_t shard,
-                                            int lane, int item, int tile, uint32_t& base, pm_mut*& out) {
-    base = 0;
-    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
-    base = __shfl(base, 0, 64);
-    out = a.recs + (size_t)shard * a.shard_cap;
-    if (total > kStage) return false;
-    for (uint32_t i = lane; i < total; i += kWave)
-        if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[i];
-    return true;
+    for (int j = 0; j < 4; ++j) F[j] = bsel(hit, Fn[j], low[j]);
+    const uint32_t self = have & valid & ((F[0] ^ Fn[0]) | (F[1] ^ Fn[1]) | (F[2] ^ Fn[2]) | (F[3] ^ Fn[3]));
+    emit_stream(a, em, lane, id0, self, site0, F[0], F[1], F[2], F[3], Fn);
+    emit_stream(a, em, lane, id1, valid & k.m0 & diff4(k.L0, F), site0, k.L0.x, k.L0.y, k.L0.z, k.L0.w, F);
+    if (k.vl.y >= 0)
+        emit_stream(a, em, lane, id2, valid & k.m1 & diff4(k.L1, F), site0, k.L1.x, k.L1.y, k.L1.z, k.L1.w, F);
 }
 
 // Where a complex lane's final goes: the record's simple area past the simple lanes' codes
@@ -1126,15 +1128,6 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 // two children's words) is issued before any of them is consumed.
 // DENSE: the level's nodes are the dense indices dense_base + item (DevTree down order),
 // so the record masks are fetched alongside the descriptor, not after it.
-// Inclusive prefix sum of v over the wave's lanes.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
 
 // SUB: subtree form (Fitch, every leaf present) -- the first two children may be S2 / S3
 // subtrees, whose inner finals and records this wave produces (subtree_prepare).
@@ -1142,7 +1135,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
 #define PM_SUB_DOWN_WAVES 4
 #endif
 // One pre-order wave: node `n` (its descriptor d) x tile; `salt` spreads the waves over the
-// record shards; `stage` is the wave's LDS record stage (kStage records).
+// record shards; `stage` is the wave's LDS entry area (kEntryQuads, see emit_stream).
 // GROUP: the launch holds up to kGroupLevels consecutive levels; a wave of
 // the group's level g > 0 does not wait for its ancestors' finals to be stored -- it
 // recomputes them top down, each from the ancestor's set (intact: final_slot) and the final
@@ -1156,8 +1149,9 @@ constexpr int kGroupLevels = PM_GROUP_LEVELS;
 static_assert(kGroupLevels >= 2 && kGroupLevels <= 4, "level groups: 2 to 4 levels");
 template <Mode M, bool AP, bool SUB, bool GROUP = false>
 __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, int32_t n, uint32_t salt, int tile,
-                                          int lane, pm_mut* stage, int gen = 0) {
+                                          int lane, uint4* stage, int gen = 0) {
     const int32_t parent = d.parent, e0 = d.e0, e1 = d.e1;
+    const uint32_t node_id = (uint32_t)a.internal_id[n];   // (scalar load, in flight with the rest)
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
     const bool is_root = parent < 0;
@@ -1221,46 +1215,13 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     }
 
     const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
-    // Records: every lane's count first, positions by a wave prefix sum (no LDS counter),
-    // and the shard reservation's global atomic issued before the records are built, so
-    // its round trip overlaps the staging.
-    KidOut o0, o1;
-    kid_prepare<M, SUB>(kids[0], valid, F, o0);
-    const bool two = e1 - e0 > 1;
-    if (two) kid_prepare<M, SUB>(kids[1], valid, F, o1);
-    else o1.self = o1.d0 = o1.d1 = o1.nsub = 0;
-    const uint32_t cnt = (uint32_t)__builtin_popcount(self_diff) + kid_count<SUB>(o0) + kid_count<SUB>(o1);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    if (total == 0) return;
-    const uint32_t p0 = incl - cnt;
-    const uint32_t shard = (salt * 31u + tile * 7919u) % kShards;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
-    const uint32_t node_id = (uint32_t)a.internal_id[n];
-    uint32_t rp = p0;
-    const LdsSink ls{stage, nullptr};
-    put_records(ls, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M>(a, ls, rp, kids[0], o0, word, F);
-    if (two) kid_put<M>(a, ls, rp, kids[1], o1, word, F);
-    base = __shfl(base, 0, 64);
-    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
-    if (total <= kStage) {
-        for (uint32_t i = lane; i < total; i += kWave)
-            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[i];
-        return;
-    }
-    // overflowed the stage: the same records at the same positions, straight into global
-    const GlobalSink gs{out, (int64_t)base, a.shard_cap, nullptr};
-    rp = p0;
-    put_records(gs, rp, node_id, self_diff, word, pc, F[0], F[1], F[2], F[3]);
-    kid_put<M>(a, gs, rp, kids[0], o0, word, F);
-    if (two) kid_put<M>(a, gs, rp, kids[1], o1, word, F);
+    // records: the node's and its first two children's streams, staged and expanded
+    Emit em{stage, shard_of(salt, tile), 0u, 0u};
+    const uint32_t site0 = (uint32_t)(word * 32);
+    emit_stream(a, em, lane, node_id, self_diff, site0, F[0], F[1], F[2], F[3], pc);
+    kid_emit<M>(a, em, lane, kids[0], kids[0].id0, kids[0].id1, kids[0].id2, valid, F, site0);
+    if (e1 - e0 > 1) kid_emit<M>(a, em, lane, kids[1], kids[1].id0, kids[1].id1, kids[1].id2, valid, F, site0);
+    emit_flush(a, em, lane);
 }
 
 // GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, unused
@@ -1276,7 +1237,7 @@ template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
 #define PM_SK_DOWN_WAVES 7
 #endif
 __global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? PM_DOWN_WAVES : (M == Mode::kSankoff && AP) ? PM_SK_DOWN_WAVES : 1) void k_down(DownArgs a) {
-    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    __shared__ uint4 stage[kWavesPerBlock][kEntryQuads];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
@@ -1284,7 +1245,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_
     if (item >= a.count) return;   // whole wave leaves together
     const NodeDesc& d = a.desc[item];
     const int gen = !GROUP ? 0 : (item >= a.split[0]) + (item >= a.split[1]) + (item >= a.split[2]);
-    const int32_t first = gen == 0 ? 0 : a.split[gen - 1];
+    const int32_t first = gen == 0 ? 0 : a.split[gen > 0 ? gen - 1 : 0];
     const int32_t n = !DENSE ? d.node : (GROUP ? a.dense_g[gen] : a.dense_base) + (item - first);
     down_node<M, AP, SUB, GROUP>(a, d, n, (uint32_t)item, tile, lane, stage[wave], gen);
 }
@@ -1298,7 +1259,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_
 template <Mode M, bool AP, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBandBlock) void k_down_band(DownArgs a, const int32_t* level_off, const int32_t* dense_base,
                                                           int32_t d0, int32_t d1) {
-    __shared__ pm_mut stage[kBandWaves][kStage];
+    __shared__ uint4 stage[kBandWaves][kEntryQuads];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
     constexpr int G = GROUP ? kGroupLevels : 1;
@@ -1321,33 +1282,12 @@ __global__ __launch_bounds__(kBandBlock) void k_down_band(DownArgs a, const int3
 // SUB: subtree form -- the S2 / S3 children are tail items too (their inner finals and
 // records from the parent's final and their leaves, subtree_put), so the level kernels stay
 // lean.
-// A tail child's records, node ids from its descriptor.
-template <Mode M, bool SUB, class Sink>
-__device__ __forceinline__ void tail_put(const TailDesc& t, const Sink& sink, uint32_t& p, const Kid& k, const KidOut& o,
-                                         int64_t word, uint32_t valid, const uint32_t* Fn) {
-    if (k.enc < 0) {
-        put_records(sink, p, (uint32_t)t.id[0], o.d0, word, Fn, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
-        return;
-    }
-    if (M == Mode::kBlockFitch || !(k.enc & kVirtualBit)) return;
-    if constexpr (SUB) {
-        const int sh = kid_shape(k.enc);
-        if (sh) {   // S2 / S3: v, its cherries and the leaves (subtree_put)
-            subtree_put(t, sink, p, k, sh, valid, Fn, word);
-            return;
-        }
-    }
-    put_records(sink, p, (uint32_t)t.id[0], o.self, word, Fn, o.F[0], o.F[1], o.F[2], o.F[3]);
-    put_records(sink, p, (uint32_t)t.id[1], o.d0, word, o.F, k.L0.x, k.L0.y, k.L0.z, k.L0.w);
-    if (k.vl.y >= 0) put_records(sink, p, (uint32_t)t.id[2], o.d1, word, o.F, k.L1.x, k.L1.y, k.L1.z, k.L1.w);
-}
-
 #ifndef PM_TAIL_WAVES
 #define PM_TAIL_WAVES 6
 #endif
 template <Mode M, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownArgs a) {
-    __shared__ pm_mut stage[kWavesPerBlock][kStage];
+    __shared__ uint4 stage[kWavesPerBlock][kEntryQuads];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
@@ -1363,7 +1303,7 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     if (!proot && pm.d == 0) return;   // no dirty lane: the child holds the parent's code everywhere
     const bool dirty = proot || ((pm.d >> lane) & 1ull);
     Kid k;
-    kid_fetch<M, AP, SUB>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
+    kid_fetch<M, AP, SUB, false>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
     // the parent's final, dirty lanes only (elsewhere the child emits nothing)
     const uint4* fsrc = proot ? a.root_final + word
                               : ((pm.x >> lane) & 1ull) ? a.sets + prec * REC + final_slot(pm)
@@ -1371,29 +1311,12 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     uint4 q = make_uint4(0, 0, 0, 0);
     if (dirty) q = *fsrc;
     const uint32_t F[4] = {q.x, q.y, q.z, q.w};
-    // records: counts, positions by a wave prefix sum, the shard reservation issued before
-    // the records are staged (as in down_node)
-    KidOut o;
-    kid_prepare<M, SUB>(k, valid, F, o);
-    const uint32_t cnt = kid_count<SUB>(o);
-    const uint32_t incl = wave_incl_sum(cnt, lane);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    if (total == 0) return;
-    const uint32_t p0 = incl - cnt;
-    const uint32_t shard = (uint32_t)(item * 31u + tile * 7919u) % kShards;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.shard_cnt[shard], total);
-    uint32_t rp = p0;
-    tail_put<M, SUB>(t, LdsSink{stage[wave], nullptr}, rp, k, o, word, valid, F);
-    base = __shfl(base, 0, 64);
-    pm_mut* out = a.recs + (size_t)shard * a.shard_cap;
-    if (total <= kStage) {
-        for (uint32_t i = lane; i < total; i += kWave)
-            if ((int64_t)base + i < a.shard_cap) out[base + i] = stage[wave][i];
-        return;
-    }
-    rp = p0;
-    tail_put<M, SUB>(t, GlobalSink{out, (int64_t)base, a.shard_cap, nullptr}, rp, k, o, word, valid, F);
+    // records: node ids from the descriptor
+    Emit em{stage[wave], shard_of((uint32_t)item, tile), 0u, 0u};
+    const uint32_t site0 = (uint32_t)(word * 32);
+    if (SUB && kid_shape(t.enc)) subtree_emit<M>(a, em, lane, t.id, t.ix, t.iy, k, kid_shape(t.enc), valid, F, site0);
+    else kid_emit<M>(a, em, lane, k, (uint32_t)t.id[0], (uint32_t)t.id[1], (uint32_t)t.id[2], valid, F, site0);
+    emit_flush(a, em, lane);
 }
 
 }  // namespace pm

@@ -97,7 +97,8 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "record masks");
     const bool virt = c->virtual_leaf_parents;
-    const bool sub = virt && mode == PM_MODE_FITCH && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
+    const bool sub = virt && (mode == PM_MODE_FITCH || mode == PM_MODE_SANKOFF) && c->subtree_form && c->leaves_all_present &&
+                     ht.num_sshape > 0;
     const int32_t root = c->dt.root_dense;
     // virtual nodes as pm_tree_upload forms them (leaf-parents: not the root, one or two
     // children, all leaves; subtree form: S2 / S3 too): vnode = the leaves their parent reads

@@ -12,6 +12,7 @@
 //                   host, so a per-(node, tile) offset table bounds each node's slice),
 //                   absent blocks restored, one coalesced write of the tile: 1 B per
 //                   leaf-column to HBM, the replay roofline of SURVEY.md §8d.
+#include "pm_bits.h"
 #include "pm_internal.h"
 
 namespace pm {
@@ -58,12 +59,7 @@ __device__ __forceinline__ EditChunk edit_chunk(const ReplayDev& d, int64_t q, i
         c.lo = te[0];
         c.len = (int32_t)(te[1] - c.lo);
     }
-    int32_t incl = c.len;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const int32_t v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)c.len);
     c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
     c.excl = incl - c.len;
     return c;
@@ -159,12 +155,7 @@ __device__ __forceinline__ EditChunk edit_chunk_from(int cnt, int64_t lo, int64_
     c.cnt = cnt;
     c.lo = lo;
     c.len = lane < cnt ? (int32_t)(hi - lo) : 0;
-    int32_t incl = c.len;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const int32_t v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)c.len);
     c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
     c.excl = incl - c.len;
     return c;

@@ -52,7 +52,11 @@ __device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& fi
 
 // AP: every leaf present -- the first two children's loads are issued together (see
 // fetch_child_ap), the third (if any) after.
-template <int B, bool AP>
+// SUB: subtree form (every leaf present) -- the first two children may be S2 / S3 subtrees
+// of three / four leaves, whose Z0 (= their Fitch set: binary unit-cost Sankoff keeps the
+// codes of maximum count, AND if non-empty else OR) comes from subtree_set_ap in registers.
+// Their records need the leaves wherever the subtree's leaves disagree (sd: dirty lanes).
+template <int B, bool AP, bool SUB = false>
 __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node;
     const int64_t word = (int64_t)tile * kWave + lane;
@@ -62,20 +66,24 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     for (int v = 0; v < 16; ++v)
 #pragma unroll
         for (int b = 0; b < B; ++b) cnt[v][b] = 0;
-    uint32_t finite = 0, z[16];
+    uint32_t finite = 0, z[16], sd = 0;
     const int32_t e0 = d.e0, e1 = d.e1;
     int32_t first = e0;
     if constexpr (AP) {
-        const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], -1, -1), vl1 = make_int4(d.vl1[0], d.vl1[1], -1, -1);
+        const int4 vl0 = SUB ? make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]) : make_int4(d.vl0[0], d.vl0[1], -1, -1);
+        const int4 vl1 = SUB ? make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]) : make_int4(d.vl1[0], d.vl1[1], -1, -1);
         ChildFetch f0, f1;
-        fetch_child_ap<kSankoffRec>(a, d.c0, vl0, tile, lane, word, f0);
-        if (e1 - e0 > 1) fetch_child_ap<kSankoffRec>(a, d.c1, vl1, tile, lane, word, f1);
+        fetch_child_ap<kSankoffRec, false, SUB>(a, d.c0, vl0, tile, lane, word, f0);
+        if (e1 - e0 > 1) fetch_child_ap<kSankoffRec, false, SUB>(a, d.c1, vl1, tile, lane, word, f1);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t vd = 0;
-        child_set_ap(d.c0, vl0, f0, z, vd);
+        child_set_ap<SUB>(d.c0, vl0, f0, z, vd);
+        if (SUB && kid_shape(d.c0)) sd |= vd;
         count_child<B>(cnt, finite, z);
         if (e1 - e0 > 1) {
-            child_set_ap(d.c1, vl1, f1, z, vd);
+            vd = 0;
+            child_set_ap<SUB>(d.c1, vl1, f1, z, vd);
+            if (SUB && kid_shape(d.c1)) sd |= vd;
             count_child<B>(cnt, finite, z);
         }
         first = e0 + 2;
@@ -122,21 +130,22 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     // optimal code (three or more children: Z0 = {c}, Z1 = {} still admits a child at
     // count 1 <= max - 2) or a leaf can be absent
     uint64_t rx, rs;
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, !a.all_present || e1 - e0 > 2, rx, rs);
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1,
+                  !a.all_present || e1 - e0 > 2 || sd != 0u, rx, rs);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
 #ifndef PM_SK_UP_WAVES
 #define PM_SK_UP_WAVES 1
 #endif
-template <int B, bool AP>
+template <int B, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock, PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    sankoff_up_node<B, AP>(a, a.desc[item], tile, lane);
+    sankoff_up_node<B, AP, SUB>(a, a.desc[item], tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
 // k_sankoff_up's waves over a.desc, the rest one workgroup per (wide node, tile) over wdesc
 // with BW-bit counters (the 16-child class counted at the wider width: same sums).
 static_assert(PM_TILE_FAST, "k_sankoff_up_mixed numbers its blocks on one grid axis");
-template <int BW, bool AP>
+template <int BW, bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const NodeDesc* wdesc, int32_t narrow_blocks) {
     __shared__ uint32_t part[16 * BW + 1][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -256,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
         int32_t item;
         int tile;
         wave_item(wave, a.tiles, item, tile);
-        if (item < a.count) sankoff_up_node<2, AP>(a, a.desc[item], tile, lane);
+        if (item < a.count) sankoff_up_node<2, AP, SUB>(a, a.desc[item], tile, lane);
         return;
     }
     const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
@@ -267,13 +276,13 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
 // Narrow post-order levels (PM_OPT_NARROW, see k_fitch_up_band): a run of levels whose
 // nodes all have out-degree <= 3, at most narrow_max of them per level, walked by one
 // launch, one 1024-thread workgroup per tile, a barrier between levels.
-template <bool AP>
+template <bool AP, bool SUB = false>
 __global__ __launch_bounds__(kBandBlock) void k_sankoff_up_band(UpArgs a, const int32_t* class_off, int32_t h0, int32_t h1) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
     for (int32_t h = h0; h < h1; ++h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1];
-        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP>(a, a.desc[i], tile, lane);
+        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP, SUB>(a, a.desc[i], tile, lane);
         __syncthreads();
     }
 }
@@ -418,15 +427,19 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const int64_t wpad = (int64_t)tiles * kWave;
     const int H = (int)ht.up_level_off.size() - 1;
 
-    // nucleotide Sankoff evaluates leaf-parents of one or two leaves inline, like Fitch
+    // nucleotide Sankoff evaluates leaf-parents of one or two leaves inline, like Fitch, and
+    // with every leaf present the S2 / S3 subtrees too (subtree form: their Z0 in the parent's
+    // post-order wave, their finals and records in the tail)
     const bool virt = !block && c->virtual_leaf_parents;
-    const int32_t* child_enc = virt ? dt.child_enc_v : dt.child_enc;
-    const NodeDesc* up_desc = virt ? dt.up_desc_v : dt.up_desc;
-    const NodeDesc* down_desc = virt ? dt.down_desc_v : dt.down_desc;
-    const std::vector<int32_t>& class_off = virt ? ht.up_class_off_v : ht.up_class_off;
-    const std::vector<int32_t>& part_off = virt ? ht.part_off_v : ht.part_off;
-    const PartDesc* parts = virt ? dt.part_desc_v : dt.part_desc;
-    const std::vector<int32_t>& down_off = virt ? ht.down_level_off_v : ht.down_level_off;
+    const bool sub = virt && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
+    const int form = sub ? 2 : virt ? 1 : 0;
+    const int32_t* child_enc = sub ? dt.child_enc_k : virt ? dt.child_enc_v : dt.child_enc;
+    const NodeDesc* up_desc = sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
+    const NodeDesc* down_desc = sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
+    const std::vector<int32_t>& class_off = sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
+    const std::vector<int32_t>& part_off = sub ? ht.part_off_k : virt ? ht.part_off_v : ht.part_off;
+    const PartDesc* parts = sub ? dt.part_desc_k : virt ? dt.part_desc_v : dt.part_desc;
+    const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
     UpArgs up{};
     up.child_off = dt.child_off;
     up.child_enc = child_enc;
@@ -447,7 +460,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     auto launch_parts = [&](int32_t b, int32_t e, hipStream_t s) {
         const int32_t p0 = part_off[b], np = part_off[e] - p0;
         int32_t widest = 0;
-        for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[virt][i]);
+        for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[form][i]);
         UpArgs pa = up;
         pa.desc = up_desc;   // parts name their node by its global up-order position
         UpArgs mg = up;
@@ -472,9 +485,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             while (h1 < H && narrow_up(h1)) ++h1;
             if (h1 - h >= 2) {
                 up.desc = up_desc;
-                const int32_t* tab = dt.lvl + ht.lvl_up[virt ? 1 : 0];
+                const int32_t* tab = dt.lvl + ht.lvl_up[form];
                 timer_begin(c, 0);
-                if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_band<true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                if (sub) hipLaunchKernelGGL((k_sankoff_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_band<true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 else hipLaunchKernelGGL((k_sankoff_up_band<false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 timer_end(c, 0);
                 h = h1 - 1;
@@ -490,7 +504,9 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
                 const int32_t nb = (int32_t)wave_grid(up.count, tiles).x;
                 const dim3 grid((unsigned)(nb + (int64_t)(w8 - m) * tiles));
                 timer_begin(c, 0);
-                if (w8 > w4 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                if (w8 > w4 && sub) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (sub) hipLaunchKernelGGL((k_sankoff_up_mixed<4, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (w8 > w4 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else if (w8 > w4) hipLaunchKernelGGL((k_sankoff_up_mixed<8, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<4, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else hipLaunchKernelGGL((k_sankoff_up_mixed<4, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
@@ -521,7 +537,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             up.count = e - b;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, s, up);
+            if (k == 0 && sub) hipLaunchKernelGGL((k_sankoff_up<2, true, true>), grid, dim3(kBlock), 0, s, up);
+            else if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, s, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, s, up);
             else if (k == 2) hipLaunchKernelGGL(k_sankoff_up_wide<8>, wide, dim3(kBlock), 0, s, up);
@@ -567,16 +584,20 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.absent_code0 = block;
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
+    dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
-    const bool dense_all = virt && ht.down_dense_v;
+    // a pre-order level = one range of dense indices: [down_off[d], down_off[d+1]) in the
+    // leaf-parent form, from down_dense_base_k[d] in the subtree form
+    const bool dense_all = sub ? ht.down_dense_k : virt && ht.down_dense_v;
+    auto dense_base_of = [&](int l) { return !dense_all ? -1 : sub ? ht.down_dense_base_k[l] : down_off[l]; };
     for (int d = 0; d < D; ++d) {
         if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {   // PM_OPT_NARROW
             int d1 = d + 1;
             while (d1 < D && down_off[d1 + 1] - down_off[d1] <= c->narrow_max) ++d1;
             if (d1 - d >= 2) {
                 dn.desc = down_desc;
-                const int32_t* tab = dt.lvl + ht.lvl_down[virt ? 1 : 0];
-                const int32_t* base = dense_all ? tab : nullptr;
+                const int32_t* tab = dt.lvl + ht.lvl_down[form];
+                const int32_t* base = !dense_all ? nullptr : sub ? dt.lvl + ht.lvl_base_k : tab;
                 timer_begin(c, 1);
                 const bool grp = c->group_waves > 0;   // level groups inside the band
                 if (c->leaves_all_present && grp) hipLaunchKernelGGL((k_down_band<Mode::kSankoff, true, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
@@ -591,8 +612,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         dn.desc = down_desc + down_off[d];
         dn.count = down_off[d + 1] - down_off[d];
         if (dn.count == 0) continue;
-        const bool dense = virt && ht.down_dense_v;   // level d = dense indices [down_off[d], down_off[d+1])
-        dn.dense_base = dense ? down_off[d] : -1;
+        const bool dense = dense_all;
+        dn.dense_base = dense_base_of(d);
         // levels d .. d + g - 1 in one launch (PM_OPT_GROUP_*; see launch_fitch)
         auto narrow_down = [&](int l) { return c->narrow_max > 0 && down_off[l + 1] - down_off[l] <= c->narrow_max; };
         auto band_at = [&](int l) { return narrow_down(l) && l + 1 < D && narrow_down(l + 1); };
@@ -608,7 +629,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             for (int k = 0; k < 4; ++k) {
                 const int l = std::min(d + k, d + g - 1);
                 if (k > 0) dn.split[k - 1] = k < g ? down_off[d + k] - down_off[d] : (int32_t)items;
-                dn.dense_g[k] = dense ? down_off[l] : -1;
+                dn.dense_g[k] = dense_base_of(l);
             }
             dn.count = (int32_t)items;
             const dim3 grid = wave_grid(dn.count, tiles);
@@ -628,14 +649,15 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         timer_end(c, 1);
     }
     // children beyond a node's second: one flat launch after the levels (k_tail)
-    const int32_t tail_total = virt ? ht.num_tail_v : ht.num_tail;
+    const int32_t tail_total = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
     if (tail_total > 0) {
         DownArgs t = dn;
-        t.tail = virt ? dt.tail_desc_v : dt.tail_desc;
+        t.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
         t.count = tail_total;
         const dim3 grid = wave_grid(t.count, tiles);
         timer_begin(c, 1);
-        if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, t);
+        if (sub) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true, true>), grid, dim3(kBlock), 0, c->stream, t);
+        else if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, t);
         else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, t);
         timer_end(c, 1);
     }

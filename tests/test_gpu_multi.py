@@ -44,6 +44,7 @@ def test_init_rank_run_gather_equals_run():
     eng.comm_init_rank(uid, 1, 0)
     s = torch.full((eng.num_sites,), -7, dtype=torch.int32, device="cuda")
     r = torch.full((eng.num_sites,), 77, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # the engine's own (non-blocking) stream does not wait for torch's
     eng.run_gather(panman_amd.MODE_FITCH, eng.num_sites, 0, s.data_ptr(), r.data_ptr())
     torch.cuda.synchronize()
     assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()
@@ -71,6 +72,7 @@ def test_device_chunks_of_shards_equal_one_run(mode, world, rule):
     full.close()
     per = panman_amd.chunk_entries(sites, world)
     allc = torch.zeros(per * world, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()   # the engines' own (non-blocking) streams do not wait for torch's
     off, idx, root = panman_amd.random_join_tree(leaves, seed=seed)
     parts, offsets = [], []
     for r, (lo, hi) in enumerate(_ranges(rule, world, sites)):
@@ -85,11 +87,13 @@ def test_device_chunks_of_shards_equal_one_run(mode, world, rule):
         eng.close()
     s = torch.full((sites,), -7, dtype=torch.int32, device="cuda")
     rt = torch.full((sites,), 77, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     helper = _engine(200, 64, 1)
     helper.unpack_site_results(allc.data_ptr(), per, world, sites, s.data_ptr(), rt.data_ptr())
     assert (s.cpu().numpy() == want_score).all() and (rt.cpu().numpy() == want_root).all()
     # a rank whose chunk head says "failed" fails the unpack on every rank
     allc[per] = 0xffffffff
+    torch.cuda.synchronize()
     with pytest.raises(panman_amd.PanmanError, match="failed"):
         helper.unpack_site_results(allc.data_ptr(), per, world, sites, s.data_ptr(), rt.data_ptr())
     helper.close()
@@ -111,12 +115,14 @@ def test_tiny_record_buffer_settles_before_gather(mode):
     eng.comm_init_rank(uid, 1, 0)
     s = torch.zeros(eng.num_sites, dtype=torch.int32, device="cuda")
     r = torch.zeros(eng.num_sites, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # the engine's own (non-blocking) stream does not wait for torch's
     eng.run_gather(mode, eng.num_sites, 0, s.data_ptr(), r.data_ptr())
     assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()
     assert eng.mutation_count() == want_n
     eng.set_record_cap(4)
     eng.run(mode)
     s.zero_()
+    torch.cuda.synchronize()
     eng.site_results_device(s.data_ptr(), r.data_ptr())
     torch.cuda.synchronize()
     assert (s.cpu().numpy() == want_score).all() and (r.cpu().numpy() == want_root).all()

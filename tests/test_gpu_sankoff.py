@@ -8,7 +8,7 @@ import pytest
 
 import panman_amd
 from _trees import CODE, names_for, parse_newick, random_tree
-from test_gpu_fitch import _random_columns, _random_msa
+from test_gpu_fitch import VARIANTS, _random_columns, _random_msa, _variant
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kats.json")
@@ -45,8 +45,9 @@ def test_sankoff_kats_on_gpu(engine, kat):
     assert rootc[0] == (255 if r == -1 else r)
 
 
-def _compare(engine, oracle, off, idx, root, codes, present, cons, forced):
+def _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant="virtual"):
     n = off.shape[0] - 1
+    _variant(engine, variant)
     leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
     node_row = np.full(n, -1, np.int32)
     for r, lid in enumerate(leaf_ids):
@@ -64,6 +65,62 @@ def _compare(engine, oracle, off, idx, root, codes, present, cons, forced):
     score, rootc = engine.site_results()
     assert (rootc == want_root).all()
     assert (score == np.bincount(want[want[:, 0] != root][:, 1], minlength=codes.shape[1])).all()
+    _variant(engine, "virtual")
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("seed", range(4))
+def test_sankoff_all_present_random_codes_vs_oracle(engine, oracle, seed, variant):
+    """Every leaf present -- the subtree form's condition (S2 / S3 subtrees: Z0 inline in the
+    parent's post-order wave, finals and records in the tail) -- with unrelated random codes,
+    so cherries and three- / four-leaf subtrees disagree everywhere; binary, unary and
+    polytomy trees; forced root (defaultState) on odd seeds."""
+    rng = np.random.default_rng(1900 + seed)
+    if seed == 0:
+        off, idx, root = panman_amd.random_join_tree(1500, seed=seed + 3)
+    else:
+        off, idx, root = random_tree(700, rng, max_children=[2, 3, 5][seed - 1], unary=[0.0, 0.1, 0.0][seed - 1])
+    leaves = int((np.diff(off) == 0).sum())
+    sites = [700, 2049, 333, 65][seed]
+    codes, present = _random_columns(rng, leaves, sites, absent_frac=0.0, gap=0.1)
+    assert present.all()
+    cons = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=sites)
+    forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
+    _compare(engine, oracle, off, idx, root, codes, present, cons, forced, variant)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("tree", ["random-join", "sars-like"])
+def test_sankoff_synthetic_columns_sample_vs_oracle(engine, oracle, variant, tree):
+    """Tree-evolved columns from the on-device generator (the bench workload, reduced):
+    every variant gives the oracle's records on a column sample and identical scores."""
+    leaves, sites = 20000, 4096
+    off, idx, root = (panman_amd.random_join_tree(leaves, seed=1) if tree == "random-join"
+                      else panman_amd.sars_like_tree(leaves, seed=1))
+    leaves = int((np.diff(off) == 0).sum())
+    _variant(engine, variant)
+    try:
+        engine.tree_upload(off, idx, root)
+        engine.synth_columns(0, sites, seed=2)
+        engine.run(panman_amd.MODE_SANKOFF)
+        got = engine.mutations()
+        score, rootc = engine.site_results()
+    finally:
+        _variant(engine, "virtual")
+    assert (score == np.bincount(got[got[:, 0] != root][:, 1], minlength=sites)).all()
+    sample = slice(1000, 1096)
+    codes = engine.leaf_codes(sample.start, sample.stop - sample.start, leaves)
+    cons = engine.consensus(sample.start, sample.stop - sample.start)
+    n = off.shape[0] - 1
+    node_row = np.full(n, -1, np.int32)
+    leaf_ids = [i for i in range(n) if off[i] == off[i + 1]]
+    node_row[leaf_ids] = np.arange(len(leaf_ids), dtype=np.int32)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, None, algo=1,
+                                            threads=8, with_root=True)
+    want[:, 1] += sample.start
+    sel = got[(got[:, 1] >= sample.start) & (got[:, 1] < sample.stop)]
+    assert sel.shape == want.shape and (sel == want).all()
+    assert (rootc[sample] == want_root).all()
 
 
 @pytest.mark.parametrize("sites", [1, 33, 700, 2049])
