@@ -31,68 +31,6 @@ namespace {
 #ifndef PM_SUB_UP_WAVES
 #define PM_SUB_UP_WAVES 4
 #endif
-// GROUP (grouped post-order launches, all leaves present).  fold_first_two<SUB, D>: the node
-// d's first two children folded into (both, either, vd); a child of this same launch
-// (pad0 / pad1 = its descriptor index) is recomputed -- its own first two children folded the
-// same way, D - 1 levels further down, then its further children and the AND-else-OR, as its
-// own wave computes its set (fitch_up_node), in registers, without the store -- and the
-// recomputed children go first, while the accumulators are still one set.
-template <bool SUB, int D>
-__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
-                                               uint32_t* both, uint32_t* either, uint32_t& vd);
-
-template <bool SUB, int D>
-__device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc& cd, int tile, int lane, int64_t word,
-                                                uint32_t* x) {
-    uint32_t both[16], either[16], vd = 0;
-    fold_first_two<SUB, D>(a, cd, tile, lane, word, both, either, vd);
-    for (int32_t e = cd.e0 + 2; e < cd.e1; ++e) {
-        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
-        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
-        fold_child<true>(a, c, vl, tile, lane, word, both, either, vd);
-    }
-    const uint32_t nz = any_plane(both);
-#pragma unroll
-    for (int v = 0; v < 16; ++v) x[v] = both[v] | (either[v] & ~nz);
-}
-
-template <bool SUB, int D>
-__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
-                                               uint32_t* both, uint32_t* either, uint32_t& vd) {
-    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
-    const bool two = d.e1 - d.e0 > 1;
-    if (D > 0 && (d.pad0 >= 0 || d.pad1 >= 0)) {
-        uint32_t x0[16];
-        child_recompute<SUB, (D > 0 ? D - 1 : 0)>(a, a.desc_all[d.pad0 >= 0 ? d.pad0 : d.pad1], tile, lane, word, x0);
-        if (d.pad0 >= 0 && d.pad1 >= 0) {
-            uint32_t x1[16];
-            child_recompute<SUB, (D > 0 ? D - 1 : 0)>(a, a.desc_all[d.pad1], tile, lane, word, x1);
-#pragma unroll
-            for (int v = 0; v < 16; ++v) { both[v] = x0[v] & x1[v]; either[v] = x0[v] | x1[v]; }
-            return;
-        }
-#pragma unroll
-        for (int v = 0; v < 16; ++v) { both[v] = x0[v]; either[v] = x0[v]; }
-        if (d.pad0 < 0 || two) {
-            const bool first = d.pad0 < 0;   // the loaded one: slot 0 or slot 1
-            const int32_t c = first ? d.c0 : d.c1;
-            const int4 vl = first ? vl0 : vl1;
-            ChildFetch f;
-            fetch_child_ap<kFitchRec, false, SUB>(a, c, vl, tile, lane, word, f);
-            fold_child_ap<SUB>(c, vl, f, both, either, vd);
-        }
-        return;
-    }
-#pragma unroll
-    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    ChildFetch f0, f1;
-    fetch_child_ap<kFitchRec, false, SUB>(a, d.c0, vl0, tile, lane, word, f0);
-    if (two) fetch_child_ap<kFitchRec, false, SUB>(a, d.c1, vl1, tile, lane, word, f1);
-    __builtin_amdgcn_sched_barrier(0);
-    fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
-    if (two) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
-}
-
 // SUB: subtree form -- the first two children may also be S2 / S3 subtrees (three or four
 // leaves each, evaluated in registers: subtree_set_ap).
 // GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
@@ -109,7 +47,7 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
-        fold_first_two<SUB, kUpGroupDepth>(a, d, tile, lane, word, both, either, vd);
+        fold_first_two<SUB, kUpGroupDepth, kFitchRec>(a, d, tile, lane, word, both, either, vd);
         cw = a.cons[word];
     } else if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;

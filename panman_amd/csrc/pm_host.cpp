@@ -73,9 +73,11 @@ void free_tree(DevTree& t) {
     dev_free(t.part_desc);
     dev_free(t.part_desc_v);
     dev_free(t.part_desc_k);
+    dev_free(t.part_desc_gs);
     dev_free(t.child_enc_k);
     dev_free(t.up_desc_k);
     dev_free(t.up_desc_g);
+    dev_free(t.up_desc_gs);
     dev_free(t.down_desc_k);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
@@ -169,7 +171,8 @@ int alloc_work(pm_ctx* c, int mode) {
     if (!fitch) {   // Sankoff nodes of out-degree > 255: part counters
         const size_t parts = (size_t)std::max(c->ht.part_off.empty() ? 0 : c->ht.part_off.back(),
                                               std::max(c->ht.part_off_v.empty() ? 0 : c->ht.part_off_v.back(),
-                                                       c->ht.part_off_k.empty() ? 0 : c->ht.part_off_k.back()));
+                                                       std::max(c->ht.part_off_k.empty() ? 0 : c->ht.part_off_k.back(),
+                                                                c->ht.part_off_gs.empty() ? 0 : c->ht.part_off_gs.back())));
         const size_t need = parts * kPartPlanes * wpad * sizeof(uint32_t);
         if (need > c->sk_parts_bytes) {
             dev_free(c->sk_parts);
@@ -816,16 +819,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const std::vector<NodeDesc> up_desc_k = make_desc(up_order_k, child_enc_k);
     // Grouped post-order launches of the subtree form (PM_OPT_UP_GROUP): a node of
     // out-degree <= 3 joins the launch of its latest materialised children when each of
-    // those is of out-degree <= 3, computed from earlier launches only, and among its first
-    // two children -- its wave recomputes them in registers (k_fitch_up<.., GROUP>, the
-    // descriptor's pad0 / pad1 = their descriptor indices) -- otherwise the launch after.
-    // Children come before parents in up_order_k (height order).  Only nodes of heights
-    // with at most kUpGroupNodes nodes join a child's launch: big levels fill the chip by
-    // themselves and pay for the recomputation (measured at N*).
-    std::vector<NodeDesc> up_desc_g;
-    {
+    // those is of out-degree <= max_rc (Fitch 3; Sankoff 2: a recomputed child's Z0 is the
+    // AND-else-OR of its children only when it is binary), computed from earlier launches
+    // only, and among its first two children -- its wave recomputes them in registers
+    // (k_fitch_up / k_sankoff_up <.., GROUP>, the descriptor's pad0 / pad1 = their descriptor
+    // indices) -- otherwise the launch after.  Children come before parents in up_order_k
+    // (height order).  Only nodes of heights with at most kUpGroupNodes nodes join a child's
+    // launch: big levels fill the chip by themselves and pay for the recomputation (measured
+    // at N*).
+    auto make_groups = [&](int32_t max_rc, std::vector<int32_t>& level_off, std::vector<int32_t>& class_off,
+                           std::vector<uint8_t>& leafy_out) {
         auto is_mat = [](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
         auto narrow = [&](int32_t d) { return degree_class(ht.child_off[d + 1] - ht.child_off[d]) == 0; };
+        auto recomputable = [&](int32_t d) { return ht.child_off[d + 1] - ht.child_off[d] <= max_rc; };
         std::vector<int32_t> lv(I, -1), inl((size_t)I * 2, -1), hsize(I, 0);
         for (size_t h = 0; h + 1 < ht.up_level_off_k.size(); ++h)
             for (int32_t i = ht.up_level_off_k[h]; i < ht.up_level_off_k[h + 1]; ++i)
@@ -844,7 +850,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1] && ok; ++e) {
                     const int32_t x = child_enc_k[e];
                     if (is_mat(x) && lv[x] == M) {
-                        ok = narrow(x) && e - ht.child_off[d] < 2 && gen[x] < kUpGroupDepth;
+                        ok = recomputable(x) && e - ht.child_off[d] < 2 && gen[x] < kUpGroupDepth;
                         ++top;
                         g = std::max(g, (int)gen[x]);
                     }
@@ -859,33 +865,37 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             G = std::max(G, lv[d] + 1);
         }
         // bucket by (launch, degree class), children-first order kept inside a bucket
-        ht.up_class_off_g.assign((size_t)G * kDegreeClasses + 1, 0);
+        class_off.assign((size_t)G * kDegreeClasses + 1, 0);
         auto key = [&](int32_t d) { return lv[d] * kDegreeClasses + degree_class(ht.child_off[d + 1] - ht.child_off[d]); };
-        for (int32_t d : up_order_k) ++ht.up_class_off_g[key(d) + 1];
-        for (size_t k = 0; k + 1 < ht.up_class_off_g.size(); ++k) ht.up_class_off_g[k + 1] += ht.up_class_off_g[k];
-        std::vector<int32_t> up_order_g(up_order_k.size()), cur(ht.up_class_off_g.begin(), ht.up_class_off_g.end() - 1),
-            pos(I, -1);
+        for (int32_t d : up_order_k) ++class_off[key(d) + 1];
+        for (size_t k = 0; k + 1 < class_off.size(); ++k) class_off[k + 1] += class_off[k];
+        std::vector<int32_t> order(up_order_k.size()), cur(class_off.begin(), class_off.end() - 1), pos(I, -1);
         for (int32_t d : up_order_k) {
             pos[d] = cur[key(d)]++;
-            up_order_g[pos[d]] = d;
+            order[pos[d]] = d;
         }
-        ht.up_level_off_g.assign(G + 1, 0);
-        for (int32_t l = 0; l <= G; ++l) ht.up_level_off_g[l] = ht.up_class_off_g[(size_t)l * kDegreeClasses];
-        ht.up_leafy_g.assign(G, 0);
+        level_off.assign(G + 1, 0);
+        for (int32_t l = 0; l <= G; ++l) level_off[l] = class_off[(size_t)l * kDegreeClasses];
+        leafy_out.assign(G, 0);
         for (int32_t l = 0; l < G; ++l) {
             bool leafy = true;
-            for (int32_t i = ht.up_class_off_g[(size_t)l * kDegreeClasses]; i < ht.up_class_off_g[(size_t)l * kDegreeClasses + 1] && leafy; ++i)
-                for (int32_t e = ht.child_off[up_order_g[i]]; e < ht.child_off[up_order_g[i] + 1]; ++e)
+            for (int32_t i = class_off[(size_t)l * kDegreeClasses]; i < class_off[(size_t)l * kDegreeClasses + 1] && leafy; ++i)
+                for (int32_t e = ht.child_off[order[i]]; e < ht.child_off[order[i] + 1]; ++e)
                     leafy &= !is_mat(child_enc_k[e]);
-            ht.up_leafy_g[l] = leafy;
+            leafy_out[l] = leafy;
         }
-        up_desc_g = make_desc(up_order_g, child_enc_k);
-        for (size_t k = 0; k < up_order_g.size(); ++k) {
-            const int32_t d = up_order_g[k];
-            up_desc_g[k].pad0 = inl[(size_t)d * 2] >= 0 ? pos[inl[(size_t)d * 2]] : -1;
-            up_desc_g[k].pad1 = inl[(size_t)d * 2 + 1] >= 0 ? pos[inl[(size_t)d * 2 + 1]] : -1;
+        std::vector<NodeDesc> desc = make_desc(order, child_enc_k);
+        for (size_t k = 0; k < order.size(); ++k) {
+            const int32_t d = order[k];
+            desc[k].pad0 = inl[(size_t)d * 2] >= 0 ? pos[inl[(size_t)d * 2]] : -1;
+            desc[k].pad1 = inl[(size_t)d * 2 + 1] >= 0 ? pos[inl[(size_t)d * 2 + 1]] : -1;
         }
-    }
+        return std::make_pair(desc, order);
+    };
+    const std::vector<NodeDesc> up_desc_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g).first;
+    // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
+    // above 255 children never group), so pad0 / pad1 here index the grouped array only
+    std::vector<NodeDesc> up_desc_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs).first;
     // subtree-form pre-order descriptors list only the children the level kernel handles:
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)
@@ -964,10 +974,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
-    std::vector<PartDesc> part_desc[3];
-    for (int v = 0; v < 3; ++v) {
-        const std::vector<NodeDesc>& ud = v == 2 ? up_desc_k : v ? up_desc_v : up_desc;
-        std::vector<int32_t>& po = v == 2 ? ht.part_off_k : v ? ht.part_off_v : ht.part_off;
+    std::vector<PartDesc> part_desc[4];
+    for (int v = 0; v < 4; ++v) {
+        const std::vector<NodeDesc>& ud = v == 3 ? up_desc_gs : v == 2 ? up_desc_k : v ? up_desc_v : up_desc;
+        std::vector<int32_t>& po = v == 3 ? ht.part_off_gs : v == 2 ? ht.part_off_k : v ? ht.part_off_v : ht.part_off;
         po.assign(ud.size() + 1, 0);
         ht.up_degree[v].assign(ud.size(), 0);
         for (size_t k = 0; k < ud.size(); ++k) {
@@ -983,15 +993,18 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     for (size_t k = 0; k < up_desc_p.size(); ++k) up_desc_p[k].pad0 = ht.part_off[k];
     for (size_t k = 0; k < up_desc_vp.size(); ++k) up_desc_vp[k].pad0 = ht.part_off_v[k];
     for (size_t k = 0; k < up_desc_kp.size(); ++k) up_desc_kp[k].pad0 = ht.part_off_k[k];
+    for (size_t k = 0; k < up_desc_gs.size(); ++k)   // (grouped nodes have out-degree <= 3: pad0 / pad1 stay theirs)
+        if (up_desc_gs[k].e1 - up_desc_gs[k].e0 > 255) up_desc_gs[k].pad0 = ht.part_off_gs[k];
     upload_phase("parts");
     std::vector<int32_t> lvl;
     {
-        const std::vector<int32_t>* up[4] = {&ht.up_class_off, &ht.up_class_off_v, &ht.up_class_off_k, &ht.up_class_off_g};
+        const std::vector<int32_t>* up[5] = {&ht.up_class_off, &ht.up_class_off_v, &ht.up_class_off_k, &ht.up_class_off_g,
+                                             &ht.up_class_off_gs};
         const std::vector<int32_t>* dn[3] = {&ht.down_level_off, &ht.down_level_off_v, &ht.down_level_off_k};
-        for (int f = 0; f < 4; ++f) {
+        for (int f = 0; f < 5; ++f) {
             ht.lvl_up[f] = (int64_t)lvl.size();
             lvl.insert(lvl.end(), up[f]->begin(), up[f]->end());
-            if (f == 3) break;
+            if (f >= 3) continue;
             ht.lvl_down[f] = (int64_t)lvl.size();
             lvl.insert(lvl.end(), dn[f]->begin(), dn[f]->end());
         }
@@ -1029,9 +1042,11 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = upload(&dt.part_desc, part_desc[0], c->stream)) != hipSuccess ||
         (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess ||
         (e = upload(&dt.part_desc_k, part_desc[2], c->stream)) != hipSuccess ||
+        (e = upload(&dt.part_desc_gs, part_desc[3], c->stream)) != hipSuccess ||
         (e = upload(&dt.child_enc_k, child_enc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.up_desc_k, up_desc_kp, c->stream)) != hipSuccess ||
         (e = upload(&dt.up_desc_g, up_desc_g, c->stream)) != hipSuccess ||
+        (e = upload(&dt.up_desc_gs, up_desc_gs, c->stream)) != hipSuccess ||
         (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
         (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||
         (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess ||

@@ -112,10 +112,12 @@ struct DevTree {
     PartDesc* part_desc = nullptr;
     PartDesc* part_desc_v = nullptr;
     PartDesc* part_desc_k = nullptr;   // subtree form (Sankoff)
+    PartDesc* part_desc_gs = nullptr;  // grouped subtree form (Sankoff)
     // subtree form (Fitch, all leaves present): S2 / S3 nodes inline in their parent too
     int32_t* child_enc_k = nullptr;   // [E] shapes in bits 28-29
     NodeDesc* up_desc_k = nullptr;
     NodeDesc* up_desc_g = nullptr;     // grouped post-order launches of the subtree form
+    NodeDesc* up_desc_gs = nullptr;    // ... Sankoff's (binary recomputed children; pad0 = first part above 255 children)
     NodeDesc* down_desc_k = nullptr;
     int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
@@ -152,20 +154,24 @@ struct HostTree {
     int32_t num_tail = 0, num_tail_v = 0;
     // Sankoff parts: prefix over the up-order descriptors ([I'+1]; nodes of out-degree <= 255
     // have none) of each form, and every descriptor's out-degree
-    std::vector<int32_t> part_off, part_off_v, part_off_k;
-    std::vector<int32_t> up_degree[3];   // [0] plain, [1] leaf-parent form, [2] subtree form
+    std::vector<int32_t> part_off, part_off_v, part_off_k, part_off_gs;
+    std::vector<int32_t> up_degree[4];   // [0] plain, [1] leaf-parent form, [2] subtree form, [3] its Sankoff groups
     // subtree form: levels without the S2 / S3 nodes, each pre-order level's first dense index
     std::vector<int32_t> up_level_off_k, up_class_off_k, down_level_off_k, down_dense_base_k;
     std::vector<uint8_t> up_leafy_k;
     // subtree form, grouped post-order launches (PM_OPT_UP_GROUP): launch l's nodes by class
     std::vector<int32_t> up_level_off_g, up_class_off_g;
     std::vector<uint8_t> up_leafy_g;
+    // ... and Sankoff's (a recomputed child must be binary)
+    std::vector<int32_t> up_level_off_gs, up_class_off_gs;
+    std::vector<uint8_t> up_leafy_gs;
     bool down_dense_k = false;
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
-    // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form
-    int64_t lvl_up[4] = {0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
+    // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form,
+    // (up only) its Fitch groups, its Sankoff groups
+    int64_t lvl_up[5] = {0, 0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
 };
 
 struct Timer {

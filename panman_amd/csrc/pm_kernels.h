@@ -387,7 +387,7 @@ __device__ __forceinline__ void leaf_word(const Args& a, int32_t leaf, int64_t w
 
 // Fold child `c` (child_enc_v encoding; `vl` its leaves if virtual) into (both, either);
 // `vd` collects the sites where a leaf-parent's two leaves disagree (dirty lanes).
-template <bool AP>
+template <bool AP, int REC = kFitchRec>
 __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
                                            uint32_t* both, uint32_t* either, uint32_t& vd) {
     if (c < 0) {   // leaf (src/fitchSankoff.cpp:32-38, absent -> 0)
@@ -420,7 +420,7 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
     } else {       // materialised internal child: compressed record
         const size_t rec = (size_t)c * a.tiles + tile;
         const RecMask mk = rec_mask(a.cmask, rec);
-        const uint4* p = a.sets + rec * kFitchRec;
+        const uint4* p = a.sets + rec * REC;
         if ((mk.x >> lane) & 1ull) {
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
@@ -586,6 +586,70 @@ __device__ __forceinline__ void virtual_set16(const Args& a, int32_t v, int64_t 
 #pragma unroll
         for (int k = 0; k < 16; ++k) s[k] |= x[k];
     }
+}
+
+// GROUP (grouped post-order launches, all leaves present).  fold_first_two<SUB, D, REC>: the node
+// d's first two children folded into (both, either, vd); a child of this same launch
+// (pad0 / pad1 = its descriptor index) is recomputed -- its own first two children folded the
+// same way, D - 1 levels further down, then its further children and the AND-else-OR, as its
+// own wave computes its set (fitch_up_node), in registers, without the store -- and the
+// recomputed children go first, while the accumulators are still one set.  REC: the record
+// stride (Fitch sets, or Sankoff's whose first 16 planes are Z0; a recomputed Sankoff child is
+// binary, so its Z0 is this same AND-else-OR of its children's Z0).
+template <bool SUB, int D, int REC>
+__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
+                                               uint32_t* both, uint32_t* either, uint32_t& vd);
+
+template <bool SUB, int D, int REC>
+__device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc& cd, int tile, int lane, int64_t word,
+                                                uint32_t* x) {
+    uint32_t both[16], either[16], vd = 0;
+    fold_first_two<SUB, D, REC>(a, cd, tile, lane, word, both, either, vd);
+    for (int32_t e = cd.e0 + 2; e < cd.e1; ++e) {
+        const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
+        fold_child<true, REC>(a, c, vl, tile, lane, word, both, either, vd);
+    }
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = both[v] | (either[v] & ~nz);
+}
+
+template <bool SUB, int D, int REC>
+__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
+                                               uint32_t* both, uint32_t* either, uint32_t& vd) {
+    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
+    const bool two = d.e1 - d.e0 > 1;
+    if (D > 0 && (d.pad0 >= 0 || d.pad1 >= 0)) {
+        uint32_t x0[16];
+        child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[d.pad0 >= 0 ? d.pad0 : d.pad1], tile, lane, word, x0);
+        if (d.pad0 >= 0 && d.pad1 >= 0) {
+            uint32_t x1[16];
+            child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[d.pad1], tile, lane, word, x1);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) { both[v] = x0[v] & x1[v]; either[v] = x0[v] | x1[v]; }
+            return;
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) { both[v] = x0[v]; either[v] = x0[v]; }
+        if (d.pad0 < 0 || two) {
+            const bool first = d.pad0 < 0;   // the loaded one: slot 0 or slot 1
+            const int32_t c = first ? d.c0 : d.c1;
+            const int4 vl = first ? vl0 : vl1;
+            ChildFetch f;
+            fetch_child_ap<REC, false, SUB>(a, c, vl, tile, lane, word, f);
+            fold_child_ap<SUB>(c, vl, f, both, either, vd);
+        }
+        return;
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
+    ChildFetch f0, f1;
+    fetch_child_ap<REC, false, SUB>(a, d.c0, vl0, tile, lane, word, f0);
+    if (two) fetch_child_ap<REC, false, SUB>(a, d.c1, vl1, tile, lane, word, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
+    if (two) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
 }
 
 // bit-sliced a < b for 4-bit codes

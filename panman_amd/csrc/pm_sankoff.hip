@@ -56,7 +56,11 @@ __device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& fi
 // of three / four leaves, whose Z0 (= their Fitch set: binary unit-cost Sankoff keeps the
 // codes of maximum count, AND if non-empty else OR) comes from subtree_set_ap in registers.
 // Their records need the leaves wherever the subtree's leaves disagree (sd: dirty lanes).
-template <int B, bool AP, bool SUB = false>
+// GROUP (grouped post-order launches, subtree form): the descriptor's pad0 / pad1 (>= 0) name
+// first / second children of this same launch -- binary, so their Z0 is the AND-else-OR of
+// their children's Z0 -- recomputed in registers (fold_first_two) instead of loaded; the
+// first two children's counts then follow from their AND (count 2) and OR (count >= 1).
+template <int B, bool AP, bool SUB = false, bool GROUP = false>
 __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node;
     const int64_t word = (int64_t)tile * kWave + lane;
@@ -69,7 +73,20 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     uint32_t finite = 0, z[16], sd = 0;
     const int32_t e0 = d.e0, e1 = d.e1;
     int32_t first = e0;
-    if constexpr (AP) {
+    if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
+        static_assert(!GROUP || (AP && SUB && B >= 2), "grouped launches: subtree form, narrow nodes");
+        uint32_t both[16], either[16], vd = 0;
+        fold_first_two<SUB, kUpGroupDepth, kSankoffRec>(a, d, tile, lane, word, both, either, vd);
+        const bool two = e1 - e0 > 1;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            cnt[v][0] = two ? either[v] & ~both[v] : either[v];
+            cnt[v][1] = two ? both[v] : 0u;
+        }
+        finite = any_plane(either);
+        sd = vd;   // (also a cherry's disagreeing leaves: extra dirty lanes, harmless)
+        first = e0 + 2;
+    } else if constexpr (AP) {
         const int4 vl0 = SUB ? make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]) : make_int4(d.vl0[0], d.vl0[1], -1, -1);
         const int4 vl1 = SUB ? make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]) : make_int4(d.vl1[0], d.vl1[1], -1, -1);
         ChildFetch f0, f1;
@@ -138,14 +155,14 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
 #ifndef PM_SK_UP_WAVES
 #define PM_SK_UP_WAVES 1
 #endif
-template <int B, bool AP, bool SUB = false>
+template <int B, bool AP, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBlock, PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    sankoff_up_node<B, AP, SUB>(a, a.desc[item], tile, lane);
+    sankoff_up_node<B, AP, SUB, GROUP>(a, a.desc[item], tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
@@ -257,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
 // k_sankoff_up's waves over a.desc, the rest one workgroup per (wide node, tile) over wdesc
 // with BW-bit counters (the 16-child class counted at the wider width: same sums).
 static_assert(PM_TILE_FAST, "k_sankoff_up_mixed numbers its blocks on one grid axis");
-template <int BW, bool AP, bool SUB = false>
+template <int BW, bool AP, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const NodeDesc* wdesc, int32_t narrow_blocks) {
     __shared__ uint32_t part[16 * BW + 1][kWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -265,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
         int32_t item;
         int tile;
         wave_item(wave, a.tiles, item, tile);
-        if (item < a.count) sankoff_up_node<2, AP, SUB>(a, a.desc[item], tile, lane);
+        if (item < a.count) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[item], tile, lane);
         return;
     }
     const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
@@ -276,13 +293,13 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
 // Narrow post-order levels (PM_OPT_NARROW, see k_fitch_up_band): a run of levels whose
 // nodes all have out-degree <= 3, at most narrow_max of them per level, walked by one
 // launch, one 1024-thread workgroup per tile, a barrier between levels.
-template <bool AP, bool SUB = false>
+template <bool AP, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBandBlock) void k_sankoff_up_band(UpArgs a, const int32_t* class_off, int32_t h0, int32_t h1) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int tile = blockIdx.x;
     for (int32_t h = h0; h < h1; ++h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1];
-        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP, SUB>(a, a.desc[i], tile, lane);
+        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[i], tile, lane);
         __syncthreads();
     }
 }
@@ -425,20 +442,21 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     const DevTree& dt = c->dt;
     const int32_t tiles = (c->words + kWave - 1) / kWave;
     const int64_t wpad = (int64_t)tiles * kWave;
-    const int H = (int)ht.up_level_off.size() - 1;
 
     // nucleotide Sankoff evaluates leaf-parents of one or two leaves inline, like Fitch, and
     // with every leaf present the S2 / S3 subtrees too (subtree form: their Z0 in the parent's
     // post-order wave, their finals and records in the tail)
     const bool virt = !block && c->virtual_leaf_parents;
     const bool sub = virt && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
+    const bool grp = sub && c->up_group;   // grouped post-order launches (PM_OPT_UP_GROUP)
     const int form = sub ? 2 : virt ? 1 : 0;
     const int32_t* child_enc = sub ? dt.child_enc_k : virt ? dt.child_enc_v : dt.child_enc;
-    const NodeDesc* up_desc = sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
+    const NodeDesc* up_desc = grp ? dt.up_desc_gs : sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
     const NodeDesc* down_desc = sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
-    const std::vector<int32_t>& class_off = sub ? ht.up_class_off_k : virt ? ht.up_class_off_v : ht.up_class_off;
-    const std::vector<int32_t>& part_off = sub ? ht.part_off_k : virt ? ht.part_off_v : ht.part_off;
-    const PartDesc* parts = sub ? dt.part_desc_k : virt ? dt.part_desc_v : dt.part_desc;
+    const std::vector<int32_t>& class_off = grp ? ht.up_class_off_gs : sub ? ht.up_class_off_k
+                                          : virt ? ht.up_class_off_v : ht.up_class_off;
+    const std::vector<int32_t>& part_off = grp ? ht.part_off_gs : sub ? ht.part_off_k : virt ? ht.part_off_v : ht.part_off;
+    const PartDesc* parts = grp ? dt.part_desc_gs : sub ? dt.part_desc_k : virt ? dt.part_desc_v : dt.part_desc;
     const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
     UpArgs up{};
     up.child_off = dt.child_off;
@@ -456,11 +474,13 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.root_dense = dt.root_dense;
     up.tiles = tiles;
     up.wpad = wpad;
+    up.desc_all = up_desc;   // grouped launches: pad0 / pad1 index the whole array
+    const int H = (int)(grp ? ht.up_level_off_gs : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off).size() - 1;
     // nodes [b, e) of one level with more than 255 children: parts, then the merge
     auto launch_parts = [&](int32_t b, int32_t e, hipStream_t s) {
         const int32_t p0 = part_off[b], np = part_off[e] - p0;
         int32_t widest = 0;
-        for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[form][i]);
+        for (int32_t i = b; i < e; ++i) widest = std::max(widest, ht.up_degree[grp ? 3 : form][i]);
         UpArgs pa = up;
         pa.desc = up_desc;   // parts name their node by its global up-order position
         UpArgs mg = up;
@@ -485,9 +505,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             while (h1 < H && narrow_up(h1)) ++h1;
             if (h1 - h >= 2) {
                 up.desc = up_desc;
-                const int32_t* tab = dt.lvl + ht.lvl_up[form];
+                const int32_t* tab = dt.lvl + ht.lvl_up[grp ? 4 : form];
                 timer_begin(c, 0);
-                if (sub) hipLaunchKernelGGL((k_sankoff_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                if (grp) hipLaunchKernelGGL((k_sankoff_up_band<true, true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
+                else if (sub) hipLaunchKernelGGL((k_sankoff_up_band<true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 else if (c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_band<true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 else hipLaunchKernelGGL((k_sankoff_up_band<false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, up, tab, h, h1);
                 timer_end(c, 0);
@@ -504,7 +525,9 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
                 const int32_t nb = (int32_t)wave_grid(up.count, tiles).x;
                 const dim3 grid((unsigned)(nb + (int64_t)(w8 - m) * tiles));
                 timer_begin(c, 0);
-                if (w8 > w4 && sub) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                if (w8 > w4 && grp) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (grp) hipLaunchKernelGGL((k_sankoff_up_mixed<4, true, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
+                else if (w8 > w4 && sub) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else if (sub) hipLaunchKernelGGL((k_sankoff_up_mixed<4, true, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else if (w8 > w4 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up_mixed<8, true>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
                 else if (w8 > w4) hipLaunchKernelGGL((k_sankoff_up_mixed<8, false>), grid, dim3(kBlock), 0, c->stream, up, up_desc + m, nb);
@@ -537,7 +560,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             up.count = e - b;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (k == 0 && sub) hipLaunchKernelGGL((k_sankoff_up<2, true, true>), grid, dim3(kBlock), 0, s, up);
+            if (k == 0 && grp) hipLaunchKernelGGL((k_sankoff_up<2, true, true, true>), grid, dim3(kBlock), 0, s, up);
+            else if (k == 0 && sub) hipLaunchKernelGGL((k_sankoff_up<2, true, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, s, up);
             else if (k == 1) hipLaunchKernelGGL(k_sankoff_up_wide<4>, wide, dim3(kBlock), 0, s, up);

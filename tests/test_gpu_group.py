@@ -21,10 +21,10 @@ def engine():
     e.close()
 
 
-def _run(engine, waves, narrow, levels=4):
+def _run(engine, waves, narrow, levels=4, mode=panman_amd.MODE_FITCH):
     engine.set_group(waves, levels)
     engine.set_narrow(narrow)
-    engine.run(panman_amd.MODE_FITCH)
+    engine.run(mode)
     got = engine.mutations()
     score, rootc = engine.site_results()
     return got, score, rootc
@@ -86,17 +86,21 @@ def test_group_option_range(engine):
 
 
 @pytest.mark.parametrize("narrow", [0, 16, 1024])
-@pytest.mark.parametrize("tree", ["sars-like", "random-join", "polytomy"])
-def test_up_groups_equal_heights(engine, narrow, tree):
+@pytest.mark.parametrize("tree", ["sars-like", "random-join", "polytomy", "wide"])
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_up_groups_equal_heights(engine, narrow, tree, mode):
     """PM_OPT_UP_GROUP: post-order launches where nodes of out-degree <= 3 recompute their
-    same-launch children (subtree form) -- identical records to one launch per height, with
-    and without narrow bands over the grouped launches."""
+    same-launch children (subtree form; Sankoff: binary children only) -- identical records
+    to one launch per height, with and without narrow bands over the grouped launches, and
+    (wide) with Sankoff nodes of more than 255 children, whose parts index the grouped array."""
     if tree == "sars-like":
         off, idx, root = panman_amd.sars_like_tree(6000, seed=31)
     elif tree == "random-join":
         off, idx, root = panman_amd.random_join_tree(6000, seed=32)
-    else:
+    elif tree == "polytomy":
         off, idx, root = random_tree(3000, np.random.default_rng(33), max_children=4, unary=0.0)
+    else:
+        off, idx, root = random_tree(3000, np.random.default_rng(34), max_children=300, unary=0.0)
     _variant(engine, "virtual")
     engine.tree_upload(off, idx, root)
     engine.synth_columns(0, 4500, seed=6)
@@ -104,7 +108,7 @@ def test_up_groups_equal_heights(engine, narrow, tree):
     try:
         for grp in (False, True):
             engine.set_up_group(grp)
-            res.append(_run(engine, 32768, narrow))
+            res.append(_run(engine, 32768, narrow, mode=mode))
     finally:
         engine.set_up_group(True)
         engine.set_narrow(16)
