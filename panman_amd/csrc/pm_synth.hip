@@ -4,7 +4,7 @@
 // Generator (SURVEY.md §8d "Synthetic inputs"): root i.i.d. uniform ACGT; per edge and
 // site a substitution (mu = 1e-3, uniform to another base) and a gap opening (1e-4,
 // geometric length, mean 5); at leaves IUPAC ambiguity (1e-5) and N-runs (start 1e-4,
-// mean length 50).  Runs are clipped at 32-site word boundaries (one lane owns a word).
+// mean length 50).  Runs are clipped at global 32-site block boundaries.
 // Randomness is counter-based (splitmix64 of seed, node, global site), so every rank and
 // the CPU baseline see the same columns for the same global site.
 #include "pm_bits.h"
@@ -34,11 +34,24 @@ constexpr uint32_t kNExtend = 4209067950u; // 0.98 -> mean length 50
 
 __device__ __forceinline__ uint32_t base_from(uint32_t r) { return 1u << (r & 3u); }
 
+// Run states (gap, N-run) restart at every global 32-site block and advance on random draws
+// alone, so a word that starts mid-block (a shard boundary that is not a multiple of 32)
+// first replays the draws of the block's earlier sites: every shard rule sees the same
+// columns as one unsharded run.
 __device__ uint4 evolve_word(uint4 par, uint64_t seed, uint64_t node, int64_t gsite0, bool leaf) {
     uint32_t b[4] = {0, 0, 0, 0};
     bool in_gap = false, in_n = false;
+    for (int64_t gs = gsite0 - (gsite0 & 31); gs < gsite0; ++gs) {
+        const uint32_t g = (uint32_t)rnd(seed, node, (uint64_t)gs, 2);
+        in_gap = in_gap ? g < kGapExtend : g < kGapOpen;
+        if (leaf) {
+            const uint32_t nq = (uint32_t)rnd(seed, node, (uint64_t)gs, 4);
+            in_n = in_n ? nq < kNExtend : nq < kNOpen;
+        }
+    }
     for (int k = 0; k < 32; ++k) {
         const uint64_t gs = (uint64_t)(gsite0 + k);
+        if ((gs & 31u) == 0) in_gap = in_n = false;
         uint32_t c = code_at(par.x, par.y, par.z, par.w, k);
         const uint64_t r = rnd(seed, node, gs, 1);
         const uint32_t r0 = (uint32_t)r, r1 = (uint32_t)(r >> 32);
@@ -49,15 +62,17 @@ __device__ uint4 evolve_word(uint4 par, uint64_t seed, uint64_t node, int64_t gs
         const uint32_t g = (uint32_t)rnd(seed, node, gs, 2);
         in_gap = in_gap ? g < kGapExtend : g < kGapOpen;
         if (in_gap) c = 0;
-        if (leaf && c != 0) {
-            const uint64_t q = rnd(seed, node, gs, 3);
-            if ((uint32_t)q < kIupac) {
-                const uint32_t amb[10] = {3, 5, 6, 7, 9, 10, 11, 12, 13, 14};
-                c = amb[(q >> 32) % 10];
-            }
+        if (leaf) {
             const uint32_t nq = (uint32_t)rnd(seed, node, gs, 4);
             in_n = in_n ? nq < kNExtend : nq < kNOpen;
-            if (in_n) c = 15;
+            if (c != 0) {
+                const uint64_t q = rnd(seed, node, gs, 3);
+                if ((uint32_t)q < kIupac) {
+                    const uint32_t amb[10] = {3, 5, 6, 7, 9, 10, 11, 12, 13, 14};
+                    c = amb[(q >> 32) % 10];
+                }
+                if (in_n) c = 15;
+            }
         }
         b[0] |= (c & 1u) << k;
         b[1] |= ((c >> 1) & 1u) << k;

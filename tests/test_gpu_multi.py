@@ -157,3 +157,23 @@ def test_design_bytes_consistent(mode):
 def test_stream_copy_rate_is_physical():
     gbs = panman_amd.stream_copy_rate(0, gib=1, reps=3)
     assert 1000.0 < gbs < 8000.0
+
+
+@pytest.mark.parametrize("lo,n", [(2049, 2050), (31, 100), (3750, 3750), (1, 1)])
+def test_synthetic_columns_are_shard_consistent(lo, n):
+    """The on-device generator gives a shard [lo, lo + n) the columns of one unsharded run
+    (runs restart at global 32-site blocks; a mid-block shard start replays the block's draws),
+    so bench.py --gpus N and the chunk tests see one alignment whatever the shard rule."""
+    leaves = 3000
+    full = _engine(leaves, lo + n + 40, seed=6)
+    want = full.leaf_codes(lo, n, leaves)
+    want_c = full.consensus(lo, n)
+    full.close()
+    off, idx, root = panman_amd.random_join_tree(leaves, seed=6)
+    eng = panman_amd.Engine(0)
+    eng.tree_upload(off, idx, root)
+    eng.synth_columns(lo, n, seed=7)
+    got = eng.leaf_codes(0, n, leaves)
+    got_c = eng.consensus(0, n)
+    eng.close()
+    assert (got == want).all() and (got_c == want_c).all()
