@@ -86,9 +86,9 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     }
     // dirty lanes: complex, or a leaf-parent child's leaves disagree; every lane when some
     // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
-    uint64_t mx, ms;
-    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
-    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms);
+    uint64_t mx, ms, md;
+    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md, n == a.root_dense);
 }
 
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
@@ -219,8 +219,8 @@ __device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, 
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
-    uint64_t mx, ms;
-    store_fitch_set(a.sets, a.cmask, a.cons[word], d.node, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms);
+    uint64_t mx, ms, md;
+    store_fitch_set(a.sets, a.cmask, a.cons[word], d.node, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
     push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms);
 }
 
@@ -599,6 +599,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         DownArgs t = dn;
         t.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
         t.count = tail_total;
+        t.num_s = sub ? ht.num_tail_s : 0;
+        t.sbase = ht.sbase;
         const dim3 grid = wave_grid(t.count, tiles);
         timer_begin(c, 1);
         if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, t);

@@ -567,23 +567,27 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
                 ht.leaf_id.push_back(i);
             }
         }
-        // stable counting sort by (virtual, depth): DFS order kept within a key
+        // stable counting sort by key: DFS order kept within a key
         int32_t maxd = 0;
         for (const int32_t i : inner) maxd = std::max(maxd, depth[i]);
-        // key (leaf-parent form virtual, depth, subtree-form virtual): a pre-order level of
-        // either form is one contiguous range of dense indices
-        // (subtree form: within a depth, nodes without an S2 / S3 child, then those with one,
-        // then the S2 / S3 nodes -- so each half of a subtree-form level is one range too)
+        // key: the materialised nodes by (depth, has an S2 / S3 child) -- a subtree-form
+        // pre-order level, and each half of it, is one contiguous range of dense indices --
+        // then the S2 / S3 nodes by depth -- the order of the subtree form's tail items, so a
+        // tail wave knows its S2 / S3 node, and the masks its parent pushed there, from its
+        // item index alone -- then the virtual leaf-parents.  (The leaf-parent form's levels,
+        // which include the S2 / S3 nodes, are then two ranges: its pre-order kernels read
+        // the node from the descriptor.)
         auto has_sub_child = [&](int32_t u) {
             for (int32_t e = off[u]; e < off[u + 1]; ++e)
                 if (sshape_id(idx[e])) return true;
             return false;
         };
-        const int32_t nk = 8 * (maxd + 1);
+        const int32_t D1 = maxd + 1, nk = 4 * D1;
         std::vector<int32_t> key(inner.size()), start(nk + 1, 0);
         for (size_t k = 0; k < inner.size(); ++k) {
             const int32_t u = inner[k];
-            key[k] = (virtual_id(u) ? 4 * (maxd + 1) : 0) + 4 * depth[u] + (sshape_id(u) ? 2 : has_sub_child(u) ? 1 : 0);
+            key[k] = virtual_id(u) ? 3 * D1 + depth[u] : sshape_id(u) ? 2 * D1 + depth[u]
+                                                       : 2 * depth[u] + (has_sub_child(u) ? 1 : 0);
             ++start[key[k] + 1];
         }
         for (int32_t k = 0; k < nk; ++k) start[k + 1] += start[k];
@@ -943,9 +947,13 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     std::vector<TailDesc> tail_desc_v = make_tail(down_order_v, child_enc_v);
     ht.num_tail = (int32_t)tail_desc.size();
     ht.num_tail_v = (int32_t)tail_desc_v.size();
-    std::vector<TailDesc> tail_desc_k = tail_desc_v;   // + every S2 / S3 node, its parent's final read back
+    // subtree form: every S2 / S3 node, in dense order (item k = dense index sbase + k), then
+    // the leaf-parent form's items
+    std::vector<TailDesc> tail_desc_k;
+    ht.sbase = -1;
     for (int32_t d = 0; d < I; ++d) {
         if (!sshape[d]) continue;
+        if (ht.sbase < 0) ht.sbase = d;
         TailDesc t{};
         t.parent = parent_dense[d];
         t.enc = (d | kVirtualBit) | (sshape[d] << kShapeShift);
@@ -956,7 +964,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         for (int j = 0; j < 4; ++j) t.id[1 + j] = t.vl[j] >= 0 ? ht.leaf_id[t.vl[j]] : -1;
         tail_desc_k.push_back(t);
     }
-    ht.num_tail_k = (int32_t)tail_desc_k.size();
+    ht.num_tail_s = (int32_t)tail_desc_k.size();
+    for (int32_t k = 0; k < ht.num_tail_s; ++k)
+        if (ht.sbase + k >= I || !sshape[ht.sbase + k]) return fail(c, PM_ERR_STATE, "S2 / S3 nodes not one dense range");
     // tail items by their parent's pre-order level (the subtree form's levels are the leaf-
     // parent form's, S2 / S3 nodes removed): neighbouring waves read neighbouring parents
     {
@@ -970,8 +980,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         };
         by_level(tail_desc, down_order, ht.down_level_off);
         by_level(tail_desc_v, down_order_v, ht.down_level_off_v);
-        by_level(tail_desc_k, down_order_v, ht.down_level_off_v);
     }
+    tail_desc_k.insert(tail_desc_k.end(), tail_desc_v.begin(), tail_desc_v.end());
+    ht.num_tail_k = (int32_t)tail_desc_k.size();
 
     // Sankoff parts: nodes of out-degree > 255, children cut into kPartChildren-wide parts
     std::vector<PartDesc> part_desc[4];

@@ -169,6 +169,8 @@ struct HostTree {
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
+    int32_t num_tail_s = 0;               // subtree form: the first num_tail_s tail items are the S2 / S3 nodes
+    int32_t sbase = -1;                   // ... dense indices sbase + item
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form,
     // (up only) its Fitch groups, its Sankoff groups
     int64_t lvl_up[5] = {0, 0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;

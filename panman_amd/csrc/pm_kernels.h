@@ -148,13 +148,29 @@ __device__ __forceinline__ void push_masks(uint64_t* cm, int32_t tiles, int tile
 
 // push_masks for every materialised child of the node with children [e0, e1) (child
 // encodings as in UpArgs::child_enc; the first two also in c0, c1); lanes share the list.
+// An S2 / S3 child (subtree form) gets the node's dirty lanes too (word 5; every lane at the
+// root): its tail wave reads the three from its own, never otherwise used, mask record --
+// addressed by its item index alone -- instead of the parent's behind its descriptor.
 __device__ __forceinline__ bool materialised(int32_t c) { return c >= 0 && !(c & kVirtualBit); }
 
+__device__ __forceinline__ void push_sub(uint64_t* cm, int32_t tiles, int tile, int32_t c, uint64_t mx, uint64_t ms,
+                                         uint64_t md) {
+    uint64_t* q = cm + kMaskWords * ((size_t)(c & kDenseMask) * tiles + tile);
+    q[3] = mx;
+    q[4] = ms;
+    q[5] = md;
+}
+
+__device__ __forceinline__ bool sub_shaped(int32_t c) { return c >= 0 && (c & kVirtualBit) && ((c >> kShapeShift) & 3); }
+
 __device__ __forceinline__ void push_children(const UpArgs& a, int tile, int lane, int32_t e0, int32_t e1, int32_t c0,
-                                              int32_t c1, uint64_t mx, uint64_t ms) {
+                                              int32_t c1, uint64_t mx, uint64_t ms, uint64_t md = 0, bool root = false) {
     if (lane == 0) {
         if (materialised(c0)) push_masks(a.cmask, a.tiles, tile, c0, mx, ms);
         if (e1 - e0 > 1 && materialised(c1)) push_masks(a.cmask, a.tiles, tile, c1, mx, ms);
+        const uint64_t dd = root ? ~0ull : md;
+        if (sub_shaped(c0)) push_sub(a.cmask, a.tiles, tile, c0, mx, ms, dd);
+        if (e1 - e0 > 1 && sub_shaped(c1)) push_sub(a.cmask, a.tiles, tile, c1, mx, ms, dd);
     }
     for (int32_t e = e0 + 2 + lane; e < e1; e += kWave) {
         const int32_t c = a.child_enc[e];
@@ -175,11 +191,11 @@ __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int 
 // holds c, the node's final is c (src/fitchSankoff.cpp:115-123) and no child record exists.
 __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t rec, int lane, bool complex_word,
                                                bool dirty_extra, const uint32_t* code, const uint4& cw, uint64_t& mx,
-                                               uint64_t& ms) {
+                                               uint64_t& ms, uint64_t& md) {
     const bool same = !complex_word && code[0] == cw.x && code[1] == cw.y && code[2] == cw.z && code[3] == cw.w;
     mx = __ballot(complex_word);
     ms = __ballot(!complex_word && !same);
-    const uint64_t md = __ballot(complex_word || dirty_extra);
+    md = __ballot(complex_word || dirty_extra);
     if (!complex_word && !same) p[lanes_below(ms)] = make_uint4(code[0], code[1], code[2], code[3]);
     if (lane == 0) {
         cm[kMaskWords * rec] = mx;
@@ -264,10 +280,10 @@ __device__ __forceinline__ void load_fitch_set(const uint4* sets, const uint64_t
     load_fitch_set(sets + rec * kFitchRec, rec_mask(cmask, rec), cons, lane, word, s);
 }
 
-// Returns the record's (x, s) masks through mx / ms (for push_masks).
+// Returns the record's (x, s, d) masks through mx / ms / md (for push_children).
 __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, const uint4& cw, int64_t node,
                                                 int32_t tiles, int tile, int lane, const uint32_t* s,
-                                                bool dirty_extra, uint64_t& mx, uint64_t& ms) {
+                                                bool dirty_extra, uint64_t& mx, uint64_t& ms, uint64_t& md) {
     uint32_t one = 0, two = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -279,7 +295,7 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
     uint4* p = sets + rec * kFitchRec;
     uint32_t code[4];
     code_from_onehot(s, code[0], code[1], code[2], code[3]);
-    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cw, mx, ms);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cw, mx, ms, md);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -324,7 +340,8 @@ __device__ __forceinline__ void load_sankoff(const uint4* sets, const uint64_t* 
 
 __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, const uint4* cons, int64_t node,
                                               int32_t tiles, int tile, int lane, int64_t word, const uint32_t* z0,
-                                              const uint32_t* z1, bool dirty_extra, uint64_t& mx, uint64_t& ms) {
+                                              const uint32_t* z1, bool dirty_extra, uint64_t& mx, uint64_t& ms,
+                                              uint64_t& md) {
     uint32_t one = 0, two = 0, any1 = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -337,7 +354,7 @@ __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, cons
     uint4* p = sets + rec * kSankoffRec;
     uint32_t code[4];
     code_from_onehot(z0, code[0], code[1], code[2], code[3]);
-    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons[word], mx, ms);
+    rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cons[word], mx, ms, md);
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -693,6 +710,8 @@ struct DownArgs {
     const uint4* forced;   // Sankoff / block defaultState per site (nullable)
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
     bool all_present;      // every leaf present at every site
+    int32_t num_s;         // k_tail (subtree form): items [0, num_s) are the S2 / S3 nodes ...
+    int32_t sbase;         // ... of dense index sbase + item
 };
 
 template <class Args>
@@ -1360,11 +1379,23 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     const TailDesc& t = a.tail[item];
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint32_t valid = valid_mask(a, word);
-    const bool proot = t.parent == a.root_dense;
     constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    // the parent's (x, s, d) masks: an S2 / S3 item finds them in its own mask record, pushed
+    // there by the parent's post-order wave (every lane dirty at the root), loaded beside the
+    // descriptor; other items read the parent's record after the descriptor
+    RecMask pm;
+    bool proot;
+    if (SUB && item < a.num_s) {
+        const uint64_t* q = a.cmask + kMaskWords * ((size_t)(a.sbase + item) * a.tiles + tile);
+        pm = RecMask{q[3], q[4], q[5], 0, 0};
+        if (pm.d == 0) return;   // no dirty lane: the child holds the parent's code everywhere
+        proot = t.parent == a.root_dense;
+    } else {
+        proot = t.parent == a.root_dense;
+        pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
+        if (!proot && pm.d == 0) return;
+    }
     const size_t prec = (size_t)t.parent * a.tiles + tile;
-    const RecMask pm = rec_mask(a.cmask, prec);
-    if (!proot && pm.d == 0) return;   // no dirty lane: the child holds the parent's code everywhere
     const bool dirty = proot || ((pm.d >> lane) & 1ull);
     Kid k;
     kid_fetch<M, AP, SUB, false>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);

@@ -146,10 +146,10 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     // dirty lanes: complex ones, and all when a child's code can differ from a single
     // optimal code (three or more children: Z0 = {c}, Z1 = {} still admits a child at
     // count 1 <= max - 2) or a leaf can be absent
-    uint64_t rx, rs;
+    uint64_t rx, rs, rd;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1,
-                  !a.all_present || e1 - e0 > 2 || sd != 0u, rx, rs);
-    push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
+                  !a.all_present || e1 - e0 > 2 || sd != 0u, rx, rs, rd);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs, rd, n == a.root_dense);
 }
 
 #ifndef PM_SK_UP_WAVES
@@ -254,8 +254,8 @@ __device__ __forceinline__ void sankoff_wide_node(const UpArgs& a, const NodeDes
         z0[v] = cand[v] & finite;
         z1[v] = eq;
     }
-    uint64_t rx, rs;
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs);
+    uint64_t rx, rs, rd;
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs, rd);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
@@ -430,8 +430,8 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_merge(UpArgs a, const uint32
         z0[v] &= finite;
         z1[v] &= finite;
     }
-    uint64_t rx, rs;
-    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs);
+    uint64_t rx, rs, rd;
+    store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs, rd);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
@@ -678,6 +678,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         DownArgs t = dn;
         t.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
         t.count = tail_total;
+        t.num_s = sub ? ht.num_tail_s : 0;
+        t.sbase = ht.sbase;
         const dim3 grid = wave_grid(t.count, tiles);
         timer_begin(c, 1);
         if (sub) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true, true>), grid, dim3(kBlock), 0, c->stream, t);
