@@ -42,8 +42,6 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
 
     uint4 cw;   // consensus word for the store; loaded after the children's loads (see below)
     uint32_t both[16], either[16], vd = 0;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
@@ -57,9 +55,15 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         // after the children's consensus loads: loaded before them, the compiler reuses it
         // for them through register copies that wait on every outstanding load
         cw = a.cons[word];
-        fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
+        // the accumulators start as the first child's set (no all-ones / zero planes live
+        // beside the loads in flight)
+        child_set_ap<SUB>(d.c0, vl0, f0, both, vd);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) either[v] = both[v];
         if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
     } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
         fold_child<AP>(a, d.c0, vl0, tile, lane, word, both, either, vd);
         if (e1 - e0 > 1) fold_child<AP>(a, d.c1, vl1, tile, lane, word, both, either, vd);
         cw = a.cons[word];
@@ -480,7 +484,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             const bool leafy = grp ? ht.up_leafy_g[h] : sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
             timer_begin(c, 0);
             if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (grp) hipLaunchKernelGGL((k_fitch_up<true, false, true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            else if (grp && ht.up_recomp_g[h]) hipLaunchKernelGGL((k_fitch_up<true, false, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);

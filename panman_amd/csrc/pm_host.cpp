@@ -832,7 +832,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     // launch: big levels fill the chip by themselves and pay for the recomputation (measured
     // at N*).
     auto make_groups = [&](int32_t max_rc, std::vector<int32_t>& level_off, std::vector<int32_t>& class_off,
-                           std::vector<uint8_t>& leafy_out) {
+                           std::vector<uint8_t>& leafy_out, std::vector<uint8_t>& recomp_out) {
         auto is_mat = [](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
         auto narrow = [&](int32_t d) { return degree_class(ht.child_off[d + 1] - ht.child_off[d]) == 0; };
         auto recomputable = [&](int32_t d) { return ht.child_off[d + 1] - ht.child_off[d] <= max_rc; };
@@ -889,17 +889,21 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             leafy_out[l] = leafy;
         }
         std::vector<NodeDesc> desc = make_desc(order, child_enc_k);
+        recomp_out.assign(G, 0);   // launches where some node recomputes a child (the others run the plain kernel)
         for (size_t k = 0; k < order.size(); ++k) {
             const int32_t d = order[k];
             desc[k].pad0 = inl[(size_t)d * 2] >= 0 ? pos[inl[(size_t)d * 2]] : -1;
             desc[k].pad1 = inl[(size_t)d * 2 + 1] >= 0 ? pos[inl[(size_t)d * 2 + 1]] : -1;
+            if (desc[k].pad0 >= 0 || desc[k].pad1 >= 0) recomp_out[lv[d]] = 1;
         }
         return std::make_pair(desc, order);
     };
-    const std::vector<NodeDesc> up_desc_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g).first;
+    const std::vector<NodeDesc> up_desc_g =
+        make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g).first;
     // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
     // above 255 children never group), so pad0 / pad1 here index the grouped array only
-    std::vector<NodeDesc> up_desc_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs).first;
+    std::vector<NodeDesc> up_desc_gs =
+        make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs).first;
     // subtree-form pre-order descriptors list only the children the level kernel handles:
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)

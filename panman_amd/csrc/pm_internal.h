@@ -161,10 +161,10 @@ struct HostTree {
     std::vector<uint8_t> up_leafy_k;
     // subtree form, grouped post-order launches (PM_OPT_UP_GROUP): launch l's nodes by class
     std::vector<int32_t> up_level_off_g, up_class_off_g;
-    std::vector<uint8_t> up_leafy_g;
+    std::vector<uint8_t> up_leafy_g, up_recomp_g;   // (recomp: some node of the launch recomputes a child)
     // ... and Sankoff's (a recomputed child must be binary)
     std::vector<int32_t> up_level_off_gs, up_class_off_gs;
-    std::vector<uint8_t> up_leafy_gs;
+    std::vector<uint8_t> up_leafy_gs, up_recomp_gs;
     bool down_dense_k = false;
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0

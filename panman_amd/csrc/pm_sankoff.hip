@@ -560,7 +560,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             up.count = e - b;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
-            if (k == 0 && grp) hipLaunchKernelGGL((k_sankoff_up<2, true, true, true>), grid, dim3(kBlock), 0, s, up);
+            if (k == 0 && grp && ht.up_recomp_gs[h]) hipLaunchKernelGGL((k_sankoff_up<2, true, true, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0 && sub) hipLaunchKernelGGL((k_sankoff_up<2, true, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0 && c->leaves_all_present) hipLaunchKernelGGL((k_sankoff_up<2, true>), grid, dim3(kBlock), 0, s, up);
             else if (k == 0) hipLaunchKernelGGL((k_sankoff_up<2, false>), grid, dim3(kBlock), 0, s, up);
