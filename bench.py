@@ -716,14 +716,21 @@ def replay_block(args, world, rank, local):
                          f"({secs:.1f}s on {threads} threads, leaves in parallel as the reference's "
                          f"tbb::parallel_for_each over leaves, src/fasta.cpp:1993)"}
     # PMC-measured HBM bytes per k_replay_tile launch (tools/pmc_traffic.py, key replay:LxC)
-    traffic = None
+    traffic, traffic_note = None, "no PMC traffic for this workload"
     if os.path.exists(args.traffic):
         try:
-            traffic = json.load(open(args.traffic)).get("k_replay_tile", {}).get(f"replay:{leaves}x{cols}")
+            entry = json.load(open(args.traffic)).get("k_replay_tile", {})
+            key = f"replay:{leaves}x{cols}"
+            if key in entry and entry.get(key + ":build") == panman_amd.build_id():
+                traffic = entry[key]
+                traffic_note = f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes on this build ({panman_amd.build_id()})"
+            elif key in entry:
+                traffic_note = (f"PMC traffic measured on build {entry.get(key + ':build')}, the loaded library is "
+                                f"{panman_amd.build_id()}: re-profile")
         except (OSError, ValueError):
             traffic = None
     out = {
-        "metric": "FASTA replay leaf*column/s (aligned, GPU replay kernels)",
+        "metric": "FASTA replay leaf*column/s (aligned, GPU replay kernels)", "build_id": panman_amd.build_id(),
         "value": value, "unit": "leaf*column/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8 (ASCII IUPAC)",
@@ -735,7 +742,7 @@ def replay_block(args, world, rank, local):
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
         "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "design_bytes_per_launch": alg_bytes,
+                     "traffic": traffic, "traffic_note": traffic_note, "design_bytes_per_launch": alg_bytes,
                      "bytes_model": "row bytes written once + consensus row once + 5 B per path edit",
                      "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,
                      "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},

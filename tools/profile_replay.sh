@@ -11,5 +11,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
     > "$out/$c.json" 2> "$out/$c.log"
 done
 key=$(python3 -c "import json;d=json.load(open('$out/FETCH_SIZE.json'));c=d['config'];print(f\"replay:{c['leaves_per_gpu']}x{c['columns']}\")")
-python3 tools/pmc_traffic.py "$out/FETCH_SIZE" "$out/WRITE_SIZE" "$key" "$out/traffic.json" > "$out/traffic.txt"
+build=$(python3 -c "import json;print(json.load(open('$out/FETCH_SIZE.json'))['build_id'])")
+python3 tools/pmc_traffic.py "$out/FETCH_SIZE" "$out/WRITE_SIZE" "$key" "$out/traffic.json" "$build" > "$out/traffic.txt"
 cat "$out/traffic.txt"
