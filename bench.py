@@ -60,9 +60,6 @@ def parse():
                    help="Fitch: PM_OPT_GROUP_WAVES, most waves of grouped pre-order levels in one launch "
                         "(-1: library default, 0: off)")
     p.add_argument("--group-levels", type=int, default=4, help="PM_OPT_GROUP_LEVELS (2 to 4)")
-    p.add_argument("--up-emit", type=int, default=-1,
-                   help="Fitch: PM_OPT_UP_EMIT (leaf-ish children's records at one-code lanes in the post-order; "
-                        "-1: library default)")
     p.add_argument("--no-up-group", action="store_true",
                    help="Fitch: post-order launches by height (PM_OPT_UP_GROUP off)")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
@@ -126,8 +123,6 @@ def main():
         eng.set_narrow(args.narrow)
     if args.no_up_group:
         eng.set_up_group(False)
-    if args.up_emit >= 0:
-        eng.set_up_emit(bool(args.up_emit))
     if args.group >= 0 or args.group_levels != 4:
         eng.set_group(args.group if args.group >= 0 else 32768, args.group_levels)
 

@@ -103,10 +103,6 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
  *                  latest children have out-degree <= 3 runs in their post-order launch,
  *                  recomputing them, instead of one launch per height; 0 = by height.
- *   PM_OPT_UP_EMIT (default 0): Fitch with every leaf present -- a non-root node of out-degree
- *                  <= 2 writes its leaf and leaf-parent children's records in the post-order
- *                  at the lanes where its set is one code (its final there whatever its
- *                  parent holds), so the pre-order reads leaves at its complex lanes only.
  *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the
  *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
  *                  re-run with a larger buffer when its results are read (pm_mutation_count,
@@ -122,7 +118,6 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_GROUP_LEVELS 9
 #define PM_OPT_UP_GROUP 10
 #define PM_OPT_RECORD_CAP 12
-#define PM_OPT_UP_EMIT 13
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

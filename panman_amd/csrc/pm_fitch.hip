@@ -35,61 +35,20 @@ namespace {
 // leaves each, evaluated in registers: subtree_set_ap).
 // GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
 // launch, recomputed here (child_recompute) instead of loaded.
-// EMIT (post-order emission, every leaf present): a non-root node of out-degree <= 2 whose
-// set is one code c at a lane has final c there whatever its parent holds
-// (src/fitchSankoff.cpp:115-123), and so has each leaf-parent child (c is in its set:
-// AND-else-OR of one-code sets), so the records of its leaf and leaf-parent children at
-// those lanes -- each leaf against c -- are written here, from the leaf words this wave
-// loaded anyway; the node's dirty lanes (RecMask::d) are then its complex lanes only, which
-// is all its pre-order wave still reads leaves for.  S2 / S3 children keep the full dirty
-// lanes (pushed to their own mask records): the tail writes all their records.
-constexpr int kUpEmitQuads = 2 * 4 * kWave;   // four streams' entries (8 KiB per wave)
-
-template <int32_t W>
-__device__ __forceinline__ void up_kid_ids(const UpArgs& a, int32_t c, int4 vl, uint32_t& ia, uint32_t& ib) {
-    if (c < 0) {
-        ia = (uint32_t)a.leaf_id[-c - 1];
-    } else if ((c & kVirtualBit) && !((c >> kShapeShift) & 3)) {
-        ia = (uint32_t)a.leaf_id[__builtin_amdgcn_readfirstlane(vl.x)];
-        const int32_t l1 = __builtin_amdgcn_readfirstlane(vl.y);
-        if (l1 >= 0) ib = (uint32_t)a.leaf_id[l1];
-    }
-}
-
-__device__ __forceinline__ void up_kid_emit(const UpArgs& a, Emit& em, int lane, int32_t c, int4 vl, const ChildFetch& f,
-                                            uint32_t ia, uint32_t ib, uint32_t m, const uint32_t* C, uint32_t site0) {
-    // (at most four streams of 64 entries: the stage holds them all, kUpEmitQuads)
-    if (c < 0) {
-        emit_stream<false>(a, em, lane, ia, m & diff4(f.code, C), site0, f.code.x, f.code.y, f.code.z, f.code.w, C);
-    } else if ((c & kVirtualBit) && !((c >> kShapeShift) & 3)) {
-        emit_stream<false>(a, em, lane, ia, m & diff4(f.code, C), site0, f.code.x, f.code.y, f.code.z, f.code.w, C);
-        if (__builtin_amdgcn_readfirstlane(vl.y) >= 0)
-            emit_stream<false>(a, em, lane, ib, m & diff4(f.v[0], C), site0, f.v[0].x, f.v[0].y, f.v[0].z, f.v[0].w, C);
-    }
-}
-
-template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false, bool EMIT = false>
-__device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane,
-                                              uint4* stage = nullptr) {
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
+__device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
 
     uint4 cw;   // consensus word for the store; loaded after the children's loads (see below)
     uint32_t both[16], either[16], vd = 0;
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
-    static_assert(!EMIT || AP, "post-order emission: every leaf present");
-    const bool emit = EMIT && n != a.root_dense && e1 - e0 <= 2 && !(GROUP && (d.pad0 >= 0 || d.pad1 >= 0));
-    uint32_t id0a = 0, id0b = 0, id1a = 0, id1b = 0;   // leaf ids of the emitted children (scalar loads)
-    if (emit) {
-        up_kid_ids<0>(a, d.c0, vl0, id0a, id0b);
-        if (e1 - e0 > 1) up_kid_ids<1>(a, d.c1, vl1, id1a, id1b);
-    }
-    ChildFetch f0, f1;
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
         fold_first_two<SUB, kUpGroupDepth, kFitchRec>(a, d, tile, lane, word, both, either, vd);
         cw = a.cons[word];
     } else if constexpr (AP) {   // both children's loads in flight together
+        ChildFetch f0, f1;
         fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c0, vl0, tile, lane, word, f0);
         if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c1, vl1, tile, lane, word, f1);
         __builtin_amdgcn_sched_barrier(0);
@@ -132,35 +91,18 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     // dirty lanes: complex, or a leaf-parent child's leaves disagree; every lane when some
     // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
     uint64_t mx, ms, md;
-    if (!emit) {
-        store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
-        push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md, n == a.root_dense);
-        return;
-    }
-    // own dirty lanes: complex only; S2 / S3 children get complex | disagreeing leaves
-    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, false, mx, ms, md);
-    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md | __ballot(vd != 0u), false);
-    if constexpr (EMIT) {
-        uint32_t C[4];
-        code_from_onehot(both, C[0], C[1], C[2], C[3]);   // the node's code where it is one
-        const uint32_t m = ((mx >> lane) & 1ull) ? 0u : valid_mask(a, word);
-        Emit em{stage, shard_of((uint32_t)n, tile), 0u, 0u};
-        const uint32_t site0 = (uint32_t)(word * 32);
-        up_kid_emit(a, em, lane, d.c0, vl0, f0, id0a, id0b, m, C, site0);
-        if (e1 - e0 > 1) up_kid_emit(a, em, lane, d.c1, vl1, f1, id1a, id1b, m, C, site0);
-        emit_flush(a, em, lane);
-    }
+    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
+    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md, n == a.root_dense);
 }
 
-template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false, bool EMIT = false>
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
-    __shared__ uint4 stage[EMIT ? kWavesPerBlock : 1][EMIT ? kUpEmitQuads : 1];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    fitch_up_node<AP, LEAFY, SUB, GROUP, EMIT>(a, a.desc[item], tile, lane, stage[EMIT ? wave : 0]);
+    fitch_up_node<AP, LEAFY, SUB, GROUP>(a, a.desc[item], tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
@@ -473,16 +415,6 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const int form = sub ? 2 : virt ? 1 : 0;   // pre-order level tables (lvl_down)
     const int up_form = grp ? 3 : form;        // post-order ones (lvl_up)
     up.desc_all = up_desc;
-    up.leaf_id = dt.leaf_id;
-    up.recs = c->recs;
-    up.shard_cap = c->shard_cap;
-    up.shard_cnt = c->shard_cnt;
-    up.words = c->words;
-    up.sites = c->num_sites;
-    // post-order emission (PM_OPT_UP_EMIT): the level kernels of the every-leaf-present forms
-    const bool emit = c->up_emit && ap && !block;
-    hipError_t e = hipMemsetAsync(c->shard_cnt, 0, sizeof(uint32_t) * kShards, c->stream);
-    if (e != hipSuccess) return e;
     const int H = (int)up_off.size() - 1;
     // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
     auto narrow_up = [&](int h) {
@@ -551,15 +483,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             const dim3 grid = wave_grid(up.count, tiles);
             const bool leafy = grp ? ht.up_leafy_g[h] : sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
             timer_begin(c, 0);
-            if (sub && leafy && emit) hipLaunchKernelGGL((k_fitch_up<true, true, true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (grp && ht.up_recomp_g[h] && emit) hipLaunchKernelGGL((k_fitch_up<true, false, true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
+            if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (grp && ht.up_recomp_g[h]) hipLaunchKernelGGL((k_fitch_up<true, false, true, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (sub && emit) hipLaunchKernelGGL((k_fitch_up<true, false, true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (ap && leafy && emit) hipLaunchKernelGGL((k_fitch_up<true, true, false, false, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap && leafy) hipLaunchKernelGGL((k_fitch_up<true, true>), grid, dim3(kBlock), 0, c->stream, up);
-            else if (ap && emit) hipLaunchKernelGGL((k_fitch_up<true, false, false, false, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (ap) hipLaunchKernelGGL((k_fitch_up<true, false>), grid, dim3(kBlock), 0, c->stream, up);
             else hipLaunchKernelGGL((k_fitch_up<false, false>), grid, dim3(kBlock), 0, c->stream, up);
             if (fork) {
@@ -570,6 +497,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         }
     }
 
+    hipError_t e = hipMemsetAsync(c->shard_cnt, 0, sizeof(uint32_t) * kShards, c->stream);
+    if (e != hipSuccess) return e;
     DownArgs dn{};
     dn.child_off = dt.child_off;
     dn.child_enc = child_enc;

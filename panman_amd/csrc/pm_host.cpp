@@ -205,7 +205,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 // Everything a captured run depends on: a different value means a different graph.
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
-                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group, (uint64_t)c->up_emit,
+                              (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -431,10 +431,6 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_GROUP_LEVELS) {
         if (value < 2 || value > 4) return fail(c, PM_ERR_ARG, "PM_OPT_GROUP_LEVELS: 2 to 4");
         c->group_levels = (int32_t)value;
-        return PM_OK;
-    }
-    if (option == PM_OPT_UP_EMIT) {
-        c->up_emit = value != 0;
         return PM_OK;
     }
     if (option == PM_OPT_RECORD_CAP) {

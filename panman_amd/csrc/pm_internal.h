@@ -203,7 +203,6 @@ struct pm_ctx {
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
-    bool up_emit = false;             // Fitch, every leaf present: leaf-ish children's records at one-code lanes in the post-order (PM_OPT_UP_EMIT)
 
     // column shard
     int64_t num_sites = 0;

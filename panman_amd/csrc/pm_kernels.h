@@ -84,13 +84,6 @@ struct UpArgs {
     int64_t wpad;
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
     bool all_present;      // every leaf present at every site (dirty-lane rules)
-    // post-order emission (k_fitch_up<.., EMIT>): records, as DownArgs
-    const int32_t* leaf_id;
-    pm_mut* recs;
-    int64_t shard_cap;
-    uint32_t* shard_cnt;
-    int64_t words;
-    int64_t sites;
 };
 
 // Load 16 planes (quads q0..q0+3) of a record of Q quads.
@@ -838,15 +831,14 @@ __device__ __forceinline__ void emit_flush(const Args& a, Emit& em, int lane) {
 }
 
 // Stage one stream: node id (wave-uniform), diff mask D, the child's code planes c, the
-// parent's code planes pc.  Every lane of the wave calls it.  CHECK = false: the caller's
-// stage holds every entry its streams can make (no flush on the way).
-template <bool CHECK = true, class Args>
+// parent's code planes pc.  Every lane of the wave calls it.
+template <class Args>
 __device__ __forceinline__ void emit_stream(const Args& a, Emit& em, int lane, uint32_t node, uint32_t D, uint32_t site0,
                                             uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const uint32_t* pc) {
     const uint64_t m = __ballot(D != 0);
     if (m == 0) return;
     const uint32_t k = (uint32_t)__builtin_popcountll(m);
-    if (CHECK && em.n + k > kEntryCap) emit_flush(a, em, lane);
+    if (em.n + k > kEntryCap) emit_flush(a, em, lane);
     if (D) {
         const uint32_t at = em.n + lanes_below(m);
         em.lds[2 * at] = make_uint4(D, node, site0, ~(pc[0] | pc[1] | pc[2] | pc[3]));

@@ -226,47 +226,3 @@ def test_sars_like_tree_vs_oracle(engine, oracle, variant):
     assert sel.shape == want.shape and (sel == want).all()
     assert (rootc[sample] == want_root).all()
     assert (score == np.bincount(got[got[:, 0] != root][:, 1], minlength=sites)).all()
-
-
-@pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("tree", ["random-join", "sars-like", "polytomy", "unary"])
-def test_up_emit_equal(engine, oracle, variant, tree):
-    """PM_OPT_UP_EMIT: leaf / leaf-parent children's records written by the post-order at
-    their parent's one-code lanes (the pre-order then reads leaves at complex lanes only)
-    -- identical records, scores and root codes to the pre-order writing them all (checked
-    against the oracle by the other tests); forced root (refState) on the polytomy tree."""
-    rng = np.random.default_rng(77)
-    if tree == "random-join":
-        off, idx, root = panman_amd.random_join_tree(6000, seed=71)
-    elif tree == "sars-like":
-        off, idx, root = panman_amd.sars_like_tree(6000, seed=72)
-    else:
-        off, idx, root = random_tree(3000, rng, max_children=4 if tree == "polytomy" else 2,
-                                     unary=0.2 if tree == "unary" else 0.0)
-    leaves = int((np.diff(off) == 0).sum())
-    sites = 3001
-    _variant(engine, variant)
-    res = []
-    try:
-        engine.tree_upload(off, idx, root)
-        if tree in ("random-join", "sars-like"):
-            engine.synth_columns(0, sites, seed=8)
-        else:
-            codes, present = _random_columns(rng, leaves, sites, absent_frac=0.0, gap=0.1)
-            n = off.shape[0] - 1
-            node_row = np.full(n, -1, np.int32)
-            node_row[[i for i in range(n) if off[i] == off[i + 1]]] = np.arange(leaves, dtype=np.int32)
-            cons = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=sites)
-            engine.leaves_upload(codes, node_row)
-            engine.sites_upload(cons, rng.integers(0, 16, size=sites).astype(np.uint8) if tree == "polytomy" else None)
-        for on in (False, True):
-            engine.set_up_emit(on)
-            engine.run(panman_amd.MODE_FITCH)
-            res.append((engine.mutations(),) + tuple(engine.site_results()))
-    finally:
-        engine.set_up_emit(False)
-        _variant(engine, "virtual")
-    (w, ws, wr), (g, gs, gr) = res
-    assert w.shape[0] > 0
-    assert g.shape == w.shape and (g == w).all()
-    assert (gs == ws).all() and (gr == wr).all()
