@@ -1,16 +1,23 @@
 #!/bin/bash
-# Build an experimental variant of the library with extra -D flags:
-#   tools/build_variant.sh NAME "-DPM_DOWN_WAVES=7 ..."  ->  build_var/NAME/libpanman_amd.so
+# Build an experimental variant of the library with extra -D flags and, optionally, a source
+# patch (a python script editing a copy of panman_amd/csrc given as its argument):
+#   tools/build_variant.sh NAME "-DPM_DOWN_WAVES=7 ..." [PATCH.py]  ->  build_var/NAME/libpanman_amd.so
 # Use it with PANMAN_AMD_LIB=build_var/NAME/libpanman_amd.so python bench.py ...
 set -euo pipefail
 cd "$(dirname "$0")/.."
-name=$1; flags=${2:-}
+name=$1; flags=${2:-}; patch=${3:-}
 out=build_var/$name
 mkdir -p "$out"
+src=panman_amd/csrc
+if [ -n "$patch" ]; then
+  rm -rf "$out/src" "$out/include" && mkdir -p "$out/src" && cp -r panman_amd/csrc "$out/src/csrc" && cp -r include "$out/include"
+  python3 "$patch" "$out/src/csrc"
+  src=$out/src/csrc
+fi
 objs=()
-for f in panman_amd/csrc/*.cpp panman_amd/csrc/*.hip; do
+for f in $src/*.cpp $src/*.hip; do
   o=$out/$(basename "$f").o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $flags -x hip -c "$f" -o "$o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I"$(pwd)/include" $flags -x hip -c "$f" -o "$o" &
   objs+=("$o")
 done
 wait

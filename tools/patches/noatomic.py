@@ -1,0 +1,9 @@
+"""Timing experiment: emit_flush takes a fixed per-shard base instead of the shard atomic
+(records overwrite each other -- results invalid; measures what the reservation costs)."""
+import sys
+p = sys.argv[1] + "/pm_kernels.h"
+s = open(p).read()
+old = "    if (lane == 0) base = atomicAdd(&a.shard_cnt[em.shard], total);\n"
+assert old in s
+s = s.replace(old, "    base = (em.shard * 977u) % (uint32_t)(a.shard_cap > 4096 ? a.shard_cap - 4096 : 1);\n")
+open(p, "w").write(s)
