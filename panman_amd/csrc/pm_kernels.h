@@ -1317,7 +1317,7 @@ template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
 #define PM_DOWN_WAVES 8
 #endif
 #ifndef PM_SK_DOWN_WAVES
-#define PM_SK_DOWN_WAVES 7
+#define PM_SK_DOWN_WAVES 6
 #endif
 __global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? PM_DOWN_WAVES : (M == Mode::kSankoff && AP) ? PM_SK_DOWN_WAVES : 1) void k_down(DownArgs a) {
     __shared__ uint4 stage[kWavesPerBlock][kEntryQuads];
