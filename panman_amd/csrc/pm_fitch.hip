@@ -41,7 +41,9 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     const int64_t word = (int64_t)tile * kWave + lane;
 
     uint4 cw;   // consensus word for the store; loaded after the children's loads (see below)
-    uint32_t both[16], either[16], vd = 0;
+    // vd0 / vd1: the first / second child's disagreeing-leaf sites (vd: every child's)
+    uint32_t both[16], either[16], vd = 0, vd0 = 0, vd1 = 0;
+    bool split = false;
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
@@ -57,10 +59,12 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         cw = a.cons[word];
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
-        child_set_ap<SUB>(d.c0, vl0, f0, both, vd);
+        child_set_ap<SUB>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
-        if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
+        if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd1);
+        vd = vd0 | vd1;
+        split = true;
     } else {
 #pragma unroll
         for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
@@ -92,7 +96,19 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
     uint64_t mx, ms, md;
     store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
-    push_children(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md, n == a.root_dense);
+    // The first / second child's own dirty lanes (mask words 6 / 7 for the pre-order
+    // descriptor's first / second child; an S2 / S3 child's pushed into its record): this node's complex lanes plus the lanes where that child's
+    // leaves disagree.  Elsewhere every site's set is one code c, which all the child's
+    // leaves hold, so its finals are c and it has no record (leaf_rule).  (The grouped
+    // recomputation keeps one vd: both get the node's dirty lanes.)
+    uint64_t md0 = md, md1 = md;
+    if (AP && split) {
+        md0 = mx | __ballot(vd0 != 0u);
+        md1 = mx | __ballot(vd1 != 0u);
+    }
+    push_children2(a, tile, lane, e0, e1, d.c0, d.c1, mx, ms, md0, md1, n == a.root_dense);
+    // (keyed by the pre-order descriptor's children, which omit S2 / S3 ones: pm_host.cpp)
+    store_kid_masks(a.cmask, (size_t)n * a.tiles + tile, lane, sub_shaped(d.c0) ? md1 : md0, md1);
 }
 
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
@@ -226,6 +242,7 @@ __device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, 
     uint64_t mx, ms, md;
     store_fitch_set(a.sets, a.cmask, a.cons[word], d.node, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
     push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms);
+    store_kid_masks(a.cmask, (size_t)d.node * a.tiles + tile, lane, md, md);
 }
 
 // One workgroup = one wide node x tile.

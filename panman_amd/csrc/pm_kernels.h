@@ -163,18 +163,34 @@ __device__ __forceinline__ void push_sub(uint64_t* cm, int32_t tiles, int tile, 
 
 __device__ __forceinline__ bool sub_shaped(int32_t c) { return c >= 0 && (c & kVirtualBit) && ((c >> kShapeShift) & 3); }
 
-__device__ __forceinline__ void push_children(const UpArgs& a, int tile, int lane, int32_t e0, int32_t e1, int32_t c0,
-                                              int32_t c1, uint64_t mx, uint64_t ms, uint64_t md = 0, bool root = false) {
+// md0 / md1: the lanes an S2 / S3 first / second child's tail wave must read (Fitch: the
+// node's complex lanes plus that child's own disagreeing-leaf lanes, see fitch_up_node;
+// otherwise the node's dirty lanes).
+__device__ __forceinline__ void push_children2(const UpArgs& a, int tile, int lane, int32_t e0, int32_t e1, int32_t c0,
+                                               int32_t c1, uint64_t mx, uint64_t ms, uint64_t md0, uint64_t md1, bool root) {
     if (lane == 0) {
         if (materialised(c0)) push_masks(a.cmask, a.tiles, tile, c0, mx, ms);
         if (e1 - e0 > 1 && materialised(c1)) push_masks(a.cmask, a.tiles, tile, c1, mx, ms);
-        const uint64_t dd = root ? ~0ull : md;
-        if (sub_shaped(c0)) push_sub(a.cmask, a.tiles, tile, c0, mx, ms, dd);
-        if (e1 - e0 > 1 && sub_shaped(c1)) push_sub(a.cmask, a.tiles, tile, c1, mx, ms, dd);
+        if (sub_shaped(c0)) push_sub(a.cmask, a.tiles, tile, c0, mx, ms, root ? ~0ull : md0);
+        if (e1 - e0 > 1 && sub_shaped(c1)) push_sub(a.cmask, a.tiles, tile, c1, mx, ms, root ? ~0ull : md1);
     }
     for (int32_t e = e0 + 2 + lane; e < e1; e += kWave) {
         const int32_t c = a.child_enc[e];
         if (materialised(c)) push_masks(a.cmask, a.tiles, tile, c, mx, ms);
+    }
+}
+
+__device__ __forceinline__ void push_children(const UpArgs& a, int tile, int lane, int32_t e0, int32_t e1, int32_t c0,
+                                              int32_t c1, uint64_t mx, uint64_t ms, uint64_t md = 0, bool root = false) {
+    push_children2(a, tile, lane, e0, e1, c0, c1, mx, ms, md, md, root);
+}
+
+// Fitch records: the lanes the pre-order pass must read the first / second child's leaves
+// at (words 6, 7; fitch_up_node), a subset of d.
+__device__ __forceinline__ void store_kid_masks(uint64_t* cm, size_t rec, int lane, uint64_t k0, uint64_t k1) {
+    if (lane == 0) {
+        cm[kMaskWords * rec + 6] = k0;
+        cm[kMaskWords * rec + 7] = k1;
     }
 }
 
@@ -898,6 +914,13 @@ struct Kid {
 
 __device__ __forceinline__ int kid_shape(int32_t enc) { return enc >= 0 && (enc & kVirtualBit) ? (enc >> kShapeShift) & 3 : 0; }
 
+// Fitch with every leaf present: at a lane where a node's set is one code c at every site
+// (not complex) each leaf child holds c and the node's final is c (rec_store_head), so a
+// leaf child's records lie in the node's complex lanes (RecMask::x).  Not for Sankoff (a
+// one-code Z0 can take its parent's code from Z1) nor with absent leaves.
+template <Mode M, bool AP>
+__device__ __forceinline__ bool leaf_rule(int32_t enc) { return M == Mode::kFitch && AP && enc < 0; }
+
 // A clean lane of the parent (not `dirty`, RecMask::d) fetches nothing: its children hold
 // the parent's code there, so their masks stay 0 and they emit no records.
 // Loads are written as "initialise, then exec-masked load" with the leaf choice made on
@@ -1272,10 +1295,20 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
         const uint4 q = is_root ? a.cons[word] : parent_final<REC>(a, parent, m, tile, lane, word);
         pc[0] = q.x; pc[1] = q.y; pc[2] = q.z; pc[3] = q.w;
     }
-    const bool dirty = is_root || ((m.d >> lane) & 1ull);
+    // Fitch, every leaf present: a leaf child differs from this node's final only at its
+    // complex lanes, a virtual child only there and where its own leaves disagree (mask
+    // words 6, 7: store_kid_masks) -- not at the lanes another child made dirty
+    uint64_t k0 = m.d, k1 = m.d;
+    if constexpr (M == Mode::kFitch && AP) {
+        const uint64_t* q = a.cmask + kMaskWords * rec;
+        k0 = d.c0 < 0 ? m.x : q[6];
+        k1 = d.c1 < 0 ? m.x : q[7];
+    }
+    const bool dirty0 = is_root || ((k0 >> lane) & 1ull);
+    const bool dirty1 = is_root || ((k1 >> lane) & 1ull);
     Kid kids[2];
-    kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty, kids[1]);
+    kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty0, kids[0]);
+    if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty1, kids[1]);
     uint32_t z1[16];
     if constexpr (M == Mode::kSankoff) {
         load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
@@ -1393,6 +1426,7 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     } else {
         proot = t.parent == a.root_dense;
         pm = rec_mask(a.cmask, (size_t)t.parent * a.tiles + tile);
+        if (leaf_rule<M, AP>(t.enc)) pm.d = pm.x;   // a leaf: the parent's complex lanes only
         if (!proot && pm.d == 0) return;
     }
     const size_t prec = (size_t)t.parent * a.tiles + tile;

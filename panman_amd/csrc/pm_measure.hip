@@ -112,6 +112,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             if (sub && ht.sshape[d]) vnode[d] = (uint8_t)(ht.sshape[d] + 2);
         }
     const double lane = 16.0, word_row = lane * kWave;   // one lane's code planes; one wave's leaf word
+    const bool leaf_rule = mode == PM_MODE_FITCH && c->leaves_all_present;
     const double cx_full = mode == PM_MODE_FITCH ? 64.0 : 128.0;   // complex lane: 16 planes / Z0 + Z1
     const double cx_read_up = 64.0;                                // the parent reads Fitch planes / Z0
     double up = 0.0, down = 0.0;
@@ -129,19 +130,28 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             up += rec;
             part[2] += rec;
             const double dirty = d == root ? kWave : popc(q[2]);
+            // Fitch, every leaf present: leaf children are read at complex lanes only, an
+            // S2 / S3 child at the lanes its parent pushed into its record (leaf_rule)
+            const double dirty_leaf = leaf_rule && d != root ? popc(q[0]) : dirty;
+            // words 6 / 7 follow the pre-order descriptor, which drops S2 / S3 children
+            auto s_child = [&](int32_t e) { return sub && ht.child_enc[e] >= 0 && vnode[ht.child_enc[e]] > 2; };
             for (int32_t k = e0; k < e1; ++k) {
                 const int32_t ch = ht.child_enc[k];
                 if (ch < 0) {
                     up += word_row;
-                    down += lane * dirty;
+                    down += lane * dirty_leaf;
                     part[0] += word_row;
-                    part[5] += lane * dirty;
+                    part[5] += lane * dirty_leaf;
                 } else if (vnode[ch]) {
                     const int32_t nl = vnode[ch];
+                    // (Fitch, all present: the first two children's own masks, words 6 / 7)
+                    const double dv = vnode[ch] > 2 ? popc(mk(ch, t)[5])
+                                      : leaf_rule && d != root && k < e0 + 2 ? popc(q[6 + (k - e0) - (k > e0 && s_child(e0))])
+                                                                             : dirty;
                     up += word_row * nl;
-                    down += lane * dirty * nl;
+                    down += lane * dv * nl;
                     part[0] += word_row * nl;
-                    part[5] += lane * dirty * nl;
+                    part[5] += lane * dv * nl;
                 } else {
                     const uint64_t* r = mk(ch, t);
                     const double b = 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
@@ -153,7 +163,10 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                 // its dirty non-consensus lanes
                 const bool tail = (k >= e0 + 2 && (ch < 0 || vnode[ch])) || (sub && ch >= 0 && vnode[ch] > 2);
                 if (tail) {
-                    const double b = 128.0 + lane * popc((q[0] | q[1]) & (d == root ? ~0ull : q[2]));
+                    const uint64_t dm = d == root ? ~0ull
+                                        : ch >= 0 && vnode[ch] > 2 ? mk(ch, t)[5]
+                                        : ch < 0 && leaf_rule ? q[0] : q[2];
+                    const double b = 128.0 + lane * popc((q[0] | q[1]) & dm);
                     down += b;
                     part[7] += b;
                 }
