@@ -1272,19 +1272,26 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
         const int32_t chain[3] = {d.pad1, d.pad0, parent};
         // the top one's parent, whose final is stored (-1: the top one is the root)
         const int32_t above = gen == 1 ? d.pad0 : gen == 2 ? d.pad1 : d.pad1 >= 0 ? a.parent_dense[d.pad1] : -1;
+        // every ancestor's masks first (uniform loads, all in flight together), then each
+        // set: the chain waits on one round trip per ancestor, not two
+        RecMask mv[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (k < gen) mv[k] = rec_mask(a.cmask, (size_t)chain[k + 3 - gen] * a.tiles + tile);
         uint4 q;
-        for (int k = 0; k < gen; ++k) {
-            const int32_t v = chain[k + 3 - gen];
-            const size_t vrec = (size_t)v * a.tiles + tile;
-            const RecMask mv = rec_mask(a.cmask, vrec);   // its (x, s) and the final above's (px, ps)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= gen) break;
+            const size_t vrec = (size_t)chain[k + 3 - gen] * a.tiles + tile;
             const bool vroot = k == 0 && above < 0;
-            if (k == 0) q = vroot ? a.cons[word] : parent_final<REC>(a, above, mv, tile, lane, word);
+            // (the top one: the final above it, from its pushed (px, ps))
+            if (k == 0) q = vroot ? a.cons[word] : parent_final<REC>(a, above, mv[0], tile, lane, word);
             uint32_t vown[16], vz1[16], gc[4] = {q.x, q.y, q.z, q.w}, VF[4], vpres;
             if constexpr (M == Mode::kSankoff) {
-                load_sankoff(a.sets + vrec * REC, mv, a.cons, lane, word, vown, vz1, !vroot);
+                load_sankoff(a.sets + vrec * REC, mv[k], a.cons, lane, word, vown, vz1, !vroot);
             } else {
                 SetFetch f;
-                fetch_fitch_set(a.sets + vrec * REC, mv, a.cons, lane, word, f);
+                fetch_fitch_set(a.sets + vrec * REC, mv[k], a.cons, lane, word, f);
                 expand_fitch_set(f, vown);
             }
             resolve_final<M>(a, vroot, word, vown, vz1, gc, VF, vpres);
