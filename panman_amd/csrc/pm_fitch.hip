@@ -31,6 +31,12 @@ namespace {
 #ifndef PM_SUB_UP_WAVES
 #define PM_SUB_UP_WAVES 4
 #endif
+// GROUP: 4 waves per SIMD, where the recomputation spills ~80 B/lane to scratch; 3 waves
+// (~150 VGPRs, no scratch) cost C3 2 %.  A spilling build of this kernel once gave wrong sets
+// at scale (DESIGN.md, S2 / S3 leaf packing): the at-scale parity tests guard every build.
+#ifndef PM_GROUP_UP_WAVES
+#define PM_GROUP_UP_WAVES 4
+#endif
 // SUB: subtree form -- the first two children may also be S2 / S3 subtrees (three or four
 // leaves each, evaluated in registers: subtree_set_ap).
 // GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
@@ -112,7 +118,7 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
 }
 
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
-__global__ __launch_bounds__(kBlock, SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
+__global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;

@@ -32,7 +32,8 @@ constexpr int kShards = 1024;
 constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
-                                  // complex, parent's simple, 3 pad (one 64-B scalar load)
+                                  // complex, parent's simple, an S2 / S3 node's pushed dirty lanes,
+                                  // Fitch: the first / second child's dirty lanes (one 64-B line)
 // Grouped post-order launches (PM_OPT_UP_GROUP): heights of at most this many nodes group.
 #ifndef PM_UP_GROUP_NODES
 #define PM_UP_GROUP_NODES 2048

@@ -59,7 +59,10 @@ inline dim3 block_grid(int32_t count, int32_t tiles) {
 
 // Levels holding nodes of both out-degree classes go to one mixed launch when the narrow
 // part is at most this many waves (the mixed kernel runs at the wide kernel's occupancy).
-constexpr int64_t kMixedMaxWaves = 4096;
+#ifndef PM_MIXED_MAX_WAVES
+#define PM_MIXED_MAX_WAVES 4096
+#endif
+constexpr int64_t kMixedMaxWaves = PM_MIXED_MAX_WAVES;
 // Narrow-level band launches (PM_OPT_NARROW): one workgroup of 16 waves per tile.
 constexpr int kBandWaves = 16;
 constexpr int kBandBlock = kBandWaves * kWave;

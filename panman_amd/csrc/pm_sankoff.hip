@@ -155,8 +155,12 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
 #ifndef PM_SK_UP_WAVES
 #define PM_SK_UP_WAVES 1
 #endif
+// GROUP: 4 waves per SIMD (3: no scratch spills, C3 Sankoff 2-3 % slower; see PM_GROUP_UP_WAVES)
+#ifndef PM_SK_GROUP_UP_WAVES
+#define PM_SK_GROUP_UP_WAVES 4
+#endif
 template <int B, bool AP, bool SUB = false, bool GROUP = false>
-__global__ __launch_bounds__(kBlock, GROUP ? 4 : PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
+__global__ __launch_bounds__(kBlock, GROUP ? PM_SK_GROUP_UP_WAVES : PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
