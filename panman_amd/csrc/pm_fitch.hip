@@ -628,6 +628,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         t.count = tail_total;
         t.num_s = sub ? ht.num_tail_s : 0;
         t.sbase = ht.sbase;
+        t.sub_planes = c->sub_planes;
         const dim3 grid = wave_grid(t.count, tiles);
         timer_begin(c, 1);
         if (sub) hipLaunchKernelGGL((k_tail<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, t);

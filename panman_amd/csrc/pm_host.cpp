@@ -101,6 +101,9 @@ void free_columns(pm_ctx* c) {
     dev_free(c->score);
     dev_free(c->root_code);
     dev_free(c->root_final);
+    dev_free(c->sub_planes);
+    c->sub_planes_bytes = 0;
+    c->sub_planes_ok = false;
     c->has_leaves = c->has_sites = c->has_forced = false;
     c->ran = false;
 }
@@ -214,6 +217,7 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
                               (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
                               (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
                               (uint64_t)(uintptr_t)c->root_code, (uint64_t)(uintptr_t)c->shard_cnt,
+                              (uint64_t)(uintptr_t)c->sub_planes,
                               (uint64_t)(uintptr_t)c->dt.child_off, (uint64_t)(uintptr_t)c->stream};
     uint64_t h = 1469598103934665603ull;
     for (uint64_t v : parts) h = (h ^ v) * 1099511628211ull;
@@ -319,6 +323,27 @@ using namespace pm;
 
 namespace pm {
 
+int build_sub_planes(pm_ctx* c) {
+    // (only the subtree form reads it, and that form needs every leaf present)
+    if (c->sub_planes_ok || !c->has_tree || !c->has_leaves || !c->leaves_all_present) return PM_OK;
+    if (c->ht.num_tail_s == 0) {
+        c->sub_planes_ok = true;
+        return PM_OK;
+    }
+    const size_t need = (size_t)c->ht.num_tail_s * (size_t)wpad_of(c) * 4 * sizeof(uint4);
+    hipError_t e = hipSuccess;
+    if (need > c->sub_planes_bytes) {
+        dev_free(c->sub_planes);
+        c->sub_planes_bytes = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&c->sub_planes), need)) != hipSuccess)
+            return fail(c, PM_ERR_OOM, std::string("subtree leaf layout: ") + hipGetErrorString(e));
+        c->sub_planes_bytes = need;
+    }
+    if ((e = launch_sub_planes(c)) != hipSuccess) return hip_fail(c, e, "subtree leaf layout");
+    c->sub_planes_ok = true;
+    return PM_OK;
+}
+
 // Leaf columns already on the device (packed codes, [row][row_stride]); every leaf with a
 // row is fully present.  Used by drivers that produce the columns on the GPU (reroot).
 int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_stride, const int32_t* node_row) {
@@ -342,7 +367,8 @@ int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_st
     dev_free(d_rows);
     if (e != hipSuccess) return hip_fail(c, e, "leaf install");
     c->has_leaves = true;
-    return PM_OK;
+    c->sub_planes_ok = false;
+    return build_sub_planes(c);
 }
 
 }  // namespace pm
@@ -470,6 +496,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     };
     if (!c || !t || !t->child_offsets || t->num_nodes < 2) return fail(c, PM_ERR_ARG, "bad tree");
     (void)hipSetDevice(c->device);
+    c->sub_planes_ok = false;   // its S2 / S3 nodes are this tree's
     const int32_t N = t->num_nodes;
     const int32_t* off = t->child_offsets;
     const int32_t* idx = t->child_index;
@@ -1124,7 +1151,8 @@ int pm_leaves_upload(pm_ctx* c, int64_t S, const uint8_t* codes4, int64_t row_st
     dev_free(d_present);
     if (e != hipSuccess) return hip_fail(c, e, "leaf upload");
     c->has_leaves = true;
-    return PM_OK;
+    c->sub_planes_ok = false;
+    return build_sub_planes(c);
 }
 
 int pm_sites_upload(pm_ctx* c, const uint8_t* consensus4, const uint8_t* forced4) {
@@ -1155,6 +1183,7 @@ int pm_run(pm_ctx* c, int mode) {
     if (!c->has_tree || !c->has_leaves || !c->has_sites) return fail(c, PM_ERR_STATE, "tree, leaves and sites first");
     (void)hipSetDevice(c->device);
     int rc = alloc_work(c, mode);
+    if (rc == PM_OK) rc = build_sub_planes(c);   // (current after every upload; a new tree resets it)
     if (rc != PM_OK) return rc;
     return run_once(c, mode);
 }
@@ -1264,7 +1293,8 @@ int pm_synth_columns(pm_ctx* c, int64_t site_begin, int64_t S, uint64_t seed) {
     c->has_leaves = c->has_sites = true;
     c->leaves_all_present = true;
     c->has_forced = false;
-    return PM_OK;
+    c->sub_planes_ok = false;
+    return build_sub_planes(c);
 }
 
 int pm_leaf_codes_fetch(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* out) {

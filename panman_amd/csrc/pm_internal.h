@@ -232,6 +232,12 @@ struct pm_ctx {
     int64_t shard_cap = 0;
     int64_t record_cap = 0;           // PM_OPT_RECORD_CAP: first allocation per shard (0 = a guess)
     uint32_t* shard_cnt = nullptr;    // [kShards]
+    // subtree form: each S2 / S3 node's three or four leaf words side by side per word
+    // ([num_tail_s][wpad][4] uint4, built from leaf_planes by build_sub_planes), so a wave that
+    // reads a subtree's leaves at scattered lanes draws one 64-B sector per lane, not four
+    uint4* sub_planes = nullptr;
+    size_t sub_planes_bytes = 0;
+    bool sub_planes_ok = false;
     int32_t* score = nullptr;         // [S]
     uint8_t* root_code = nullptr;     // [S]
     bool ran = false;
@@ -278,6 +284,9 @@ hipError_t launch_fitch(pm_ctx* c, bool block);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
 // Records of the last run, sorted by (node, site) on the device, copied to host `out`.
 hipError_t sort_records_to_host(pm_ctx* c, const std::vector<uint32_t>& counts, int64_t n, pm_mut* out);
+// (Re)build the S2 / S3 leaf layout after the leaf columns or the tree changed (no-op when
+// it is current or the tree has no S2 / S3 node).
+int build_sub_planes(pm_ctx* c);
 static_assert(sizeof(pm_mut) == 8, "pm_mut is {node, site_info}");
 hipError_t launch_score(pm_ctx* c);
 hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_stride, const int32_t* d_row_of_leaf,
@@ -285,6 +294,7 @@ hipError_t launch_pack_codes(pm_ctx* c, const uint8_t* d_codes4, int64_t row_str
 hipError_t launch_pack_sites(pm_ctx* c, const uint8_t* d_codes4, uint4* dst);
 hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
+hipError_t launch_sub_planes(pm_ctx* c);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
 void free_replay(pm_ctx* c);
 void comm_release(pm_ctx* c);   // pm_rccl.hip

@@ -89,6 +89,12 @@ struct UpArgs {
     bool all_present;      // every leaf present at every site (dirty-lane rules)
 };
 
+// The leaf words of S2 / S3 node `item` (dense index sbase + item) at one word: vl[0..3]'s
+// words in four consecutive uint4 (pm_ctx::sub_planes).
+__device__ __forceinline__ const uint4* sub_word(const uint4* sub_planes, int32_t item, int64_t wpad, int64_t word) {
+    return sub_planes + ((size_t)item * wpad + word) * 4;
+}
+
 // Load 16 planes (quads q0..q0+3) of a record of Q quads.
 template <int Q = 4>
 __device__ __forceinline__ void load_set16(const uint4* sets, int64_t node, int32_t tiles, int tile,
@@ -502,6 +508,9 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
     if (c < 0) {
         f.code = a.leaf_planes[(size_t)(-c - 1) * a.wpad + word];
     } else if (c & kVirtualBit) {
+        // (an S2 / S3 child's leaves from their rows, every lane: coalesced.  The side-by-side
+        // layout, sub_planes, is for the tail's scattered dirty lanes; read here it made the
+        // post-order 6 % slower -- four times the cache lines per load instruction.)
         const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
         f.code = a.leaf_planes[(size_t)l0 * a.wpad + word];
         if (l1 >= 0) f.v[0] = a.leaf_planes[(size_t)l1 * a.wpad + word];
@@ -731,6 +740,7 @@ struct DownArgs {
     bool all_present;      // every leaf present at every site
     int32_t num_s;         // k_tail (subtree form): items [0, num_s) are the S2 / S3 nodes ...
     int32_t sbase;         // ... of dense index sbase + item
+    const uint4* sub_planes;   // ... whose leaves sit side by side there (sub_word)
 };
 
 template <class Args>
@@ -1442,7 +1452,21 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     const size_t prec = (size_t)t.parent * a.tiles + tile;
     const bool dirty = proot || ((pm.d >> lane) & 1ull);
     Kid k;
-    kid_fetch<M, AP, SUB, false>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
+    if (SUB && item < a.num_s) {   // an S2 / S3 node: its leaves' words in one 64-B row
+        k.enc = t.enc;
+        k.L0 = k.L1 = k.L2 = k.L3 = make_uint4(0, 0, 0, 0);
+        k.m0 = k.m1 = 0;
+        const uint4* q = sub_word(a.sub_planes, item, a.wpad, word);
+        if (dirty) {
+            k.L0 = q[0];
+            k.L1 = q[1];
+            k.L2 = q[2];
+            k.m0 = k.m1 = ~0u;
+        }
+        if (dirty && kid_shape(t.enc) == 2) k.L3 = q[3];
+    } else {
+        kid_fetch<M, AP, SUB, false>(a, t.enc, make_int4(t.vl[0], t.vl[1], t.vl[2], t.vl[3]), word, dirty, k);
+    }
     // the parent's final, dirty lanes only (elsewhere the child emits nothing)
     const uint4* fsrc = proot ? a.root_final + word
                               : ((pm.x >> lane) & 1ull) ? a.sets + prec * REC + final_slot(pm)

@@ -235,6 +235,29 @@ hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed) {
     return hipMemcpyAsync(c->cons, root_dst, sizeof(uint4) * wpad, hipMemcpyDeviceToDevice, c->stream);
 }
 
+// S2 / S3 leaf layout (pm_ctx::sub_planes): thread = (S2 / S3 item, word), its three or four
+// leaves' words copied side by side (tail descriptors hold the leaves, -1 padded).
+__global__ __launch_bounds__(256) void k_sub_planes(const TailDesc* tail, int32_t num_s, const uint4* leaf_planes,
+                                                    int64_t wpad, uint4* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)num_s * wpad) return;
+    const int32_t item = (int32_t)(i / wpad);
+    const int64_t word = i - (int64_t)item * wpad;
+    const TailDesc& t = tail[item];
+    uint4* o = out + (size_t)i * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = t.vl[j] >= 0 ? leaf_planes[(size_t)t.vl[j] * wpad + word] : make_uint4(0, 0, 0, 0);
+}
+
+hipError_t launch_sub_planes(pm_ctx* c) {
+    const int64_t wpad = (int64_t)((c->words + kWave - 1) / kWave) * kWave;
+    const int64_t n = (int64_t)c->ht.num_tail_s * wpad;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sub_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->dt.tail_desc_k,
+                       c->ht.num_tail_s, c->leaf_planes, wpad, c->sub_planes);
+    return hipGetLastError();
+}
+
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out) {
     const int64_t wpad = (int64_t)((c->words + kWave - 1) / kWave) * kWave;
     const int64_t n = (int64_t)c->dt.num_leaves * ns;
