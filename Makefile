@@ -1,7 +1,7 @@
 # libpanman_amd.so: HIP kernels + C-ABI for gfx950 (MI355X).  No CPU fallback inside.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -mllvm -amdgpu-atomic-optimizer-strategy=None
 SRC := $(wildcard panman_amd/csrc/*.cpp) $(wildcard panman_amd/csrc/*.hip)
 HDR := $(wildcard panman_amd/csrc/*.h) include/panman_gpu.h
 OBJ := $(patsubst panman_amd/csrc/%,build/%.o,$(SRC)) build/pm_build_id.o

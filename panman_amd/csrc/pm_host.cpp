@@ -514,6 +514,11 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             parent[ch] = i;
         }
     if (off[t->root + 1] == off[t->root]) return fail(c, PM_ERR_ARG, "root must be internal");
+    // a child's encoding keeps the dense internal index in its low kShapeShift bits (the
+    // subtree shape above them): more internal nodes would mix shape bits into indices
+    int64_t internal = 0;
+    for (int32_t i = 0; i < N; ++i) internal += off[i + 1] > off[i];
+    if (internal > kDenseMask) return fail(c, PM_ERR_ARG, "too many internal nodes (limit 2^28 - 1)");
     // BFS from the root: depth + connectivity.
     std::vector<int32_t> bfs;
     bfs.reserve(N);

@@ -809,27 +809,13 @@ __device__ __forceinline__ uint32_t rec_low(uint32_t c0, uint32_t c1, uint32_t c
 // trip count is at most kHeavyBits plus one per heavy entry instead of the largest count (32).
 constexpr int kHeavyBits = 4;
 
-template <class Args>
-__device__ __forceinline__ void emit_flush(const Args& a, Emit& em, int lane) {
-    if (em.n == 0) return;
-    uint32_t total;
-    (void)wave_exclusive_scan(em.cnt, total);
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.shard_cnt[em.shard], total);
-    base = __builtin_amdgcn_readfirstlane(base);
-    pm_mut* out = a.recs + (size_t)em.shard * a.shard_cap;
-    const int64_t cap = a.shard_cap;
-    for (uint32_t r0 = 0; r0 < em.n; r0 += kWave) {
-        const uint32_t j = r0 + (uint32_t)lane;
-        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
-        if (j < em.n) {
-            e0 = em.lds[2 * j];
-            e1 = em.lds[2 * j + 1];
-        }
-        const uint32_t D = e0.x, node = e0.y, site0 = e0.z, pz = e0.w;
-        const uint32_t c = (uint32_t)__builtin_popcount(D);
-        uint32_t tot;
-        const uint32_t p0 = base + wave_exclusive_scan(c, tot);
+// One round of a flush: entries e0 / e1 (one per lane, D = 0 past the staged ones), the
+// lane's first record at p0.
+__device__ __forceinline__ void emit_round(pm_mut* out, int64_t cap, const uint4& e0, const uint4& e1, uint32_t p0,
+                                           int lane) {
+    const uint32_t D = e0.x, node = e0.y, site0 = e0.z, pz = e0.w;
+    const uint32_t c = (uint32_t)__builtin_popcount(D);
+    {
         const bool heavy = c > (uint32_t)kHeavyBits;
         uint32_t d = heavy ? 0u : D, p = p0;
         while (d) {
@@ -853,7 +839,59 @@ __device__ __forceinline__ void emit_flush(const Args& a, Emit& em, int lane) {
                 if ((int64_t)q < cap) out[q] = pm_mut{hn, ((hs + (uint32_t)bit) << 8) | rec_low(h0, h1, h2, h3, hz, bit)};
             }
         }
+    }
+}
+
+// entry j (< kEntryCap: inside the wave's area, so read without a branch); D = 0 past the
+// staged entries
+__device__ __forceinline__ void emit_load(const Emit& em, uint32_t j, uint4& e0, uint4& e1) {
+    e0 = em.lds[2 * j];
+    e1 = em.lds[2 * j + 1];
+    if (j >= em.n) e0.x = 0;
+}
+
+// The reservation (one returned atomic) is issued first; the first round's entries and their
+// positions relative to it are read while it is in flight.  (The library is built with
+// -amdgpu-atomic-optimizer-strategy=None: the optimizer wraps this already wave-aggregated
+// atomic in a scan of its own whose readfirstlane waits for the atomic right away.)
+// PEEL: the first round is a copy of its own, its stores also issued before the loop's code
+// -- faster for the Fitch kernels (k_down + k_tail 7.08 -> 6.92 ms at N*), slower for the
+// larger Sankoff ones (10.18 -> 10.39 ms), which take the loop (10.10 ms).
+template <bool PEEL = false, class Args>
+__device__ __forceinline__ void emit_flush(const Args& a, Emit& em, int lane) {
+    if (em.n == 0) return;
+    uint32_t total;
+    (void)wave_exclusive_scan(em.cnt, total);
+    uint32_t got = 0;
+    if (lane == 0) got = atomicAdd(&a.shard_cnt[em.shard], total);
+    pm_mut* out = a.recs + (size_t)em.shard * a.shard_cap;
+    const int64_t cap = a.shard_cap;
+    // each round's entries and relative positions are read before the round; the first
+    // round's while the reservation is in flight
+    uint4 e0, e1;
+    emit_load(em, (uint32_t)lane, e0, e1);
+    uint32_t tot;
+    uint32_t rel = wave_exclusive_scan((uint32_t)__builtin_popcount(e0.x), tot);
+    uint32_t base = __builtin_amdgcn_readfirstlane(got);
+    if constexpr (PEEL) {
+        emit_round(out, cap, e0, e1, base + rel, lane);
         base += tot;
+        for (uint32_t r0 = kWave; r0 < em.n; r0 += kWave) {
+            emit_load(em, r0 + (uint32_t)lane, e0, e1);
+            const uint32_t p0 = base + wave_exclusive_scan((uint32_t)__builtin_popcount(e0.x), tot);
+            emit_round(out, cap, e0, e1, p0, lane);
+            base += tot;
+        }
+        em.n = 0;
+        em.cnt = 0;
+        return;
+    }
+    for (uint32_t r0 = kWave;; r0 += kWave) {
+        emit_round(out, cap, e0, e1, base + rel, lane);
+        base += tot;
+        if (r0 >= em.n) break;
+        emit_load(em, r0 + (uint32_t)lane, e0, e1);
+        rel = wave_exclusive_scan((uint32_t)__builtin_popcount(e0.x), tot);
     }
     em.n = 0;
     em.cnt = 0;
@@ -1357,7 +1395,7 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     emit_stream(a, em, lane, node_id, self_diff, site0, F[0], F[1], F[2], F[3], pc);
     kid_emit<M>(a, em, lane, kids[0], kids[0].id0, kids[0].id1, kids[0].id2, valid, F, site0);
     if (e1 - e0 > 1) kid_emit<M>(a, em, lane, kids[1], kids[1].id0, kids[1].id1, kids[1].id2, valid, F, site0);
-    emit_flush(a, em, lane);
+    emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
 // GROUP: items [split[g-1], split[g]) are the group's level g (split[-1] = 0, unused
@@ -1479,7 +1517,7 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     const uint32_t site0 = (uint32_t)(word * 32);
     if (SUB && kid_shape(t.enc)) subtree_emit<M>(a, em, lane, t.id, t.ix, t.iy, k, kid_shape(t.enc), valid, F, site0);
     else kid_emit<M>(a, em, lane, k, (uint32_t)t.id[0], (uint32_t)t.id[1], (uint32_t)t.id[2], valid, F, site0);
-    emit_flush(a, em, lane);
+    emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
 }  // namespace pm

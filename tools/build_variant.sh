@@ -17,7 +17,7 @@ fi
 objs=()
 for f in $src/*.cpp $src/*.hip; do
   o=$out/$(basename "$f").o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I"$(pwd)/include" $flags -x hip -c "$f" -o "$o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -amdgpu-atomic-optimizer-strategy=None -I"$(pwd)/include" $flags -x hip -c "$f" -o "$o" &
   objs+=("$o")
 done
 wait
