@@ -148,6 +148,10 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         const size_t first = ecol.size();
         for (int64_t k = p->nuc_mut_offsets[v]; k < p->nuc_mut_offsets[v + 1]; ++k) {
             const int32_t id = p->nuc_mut_primary[k];
+            // secondary blocks (blockGaps, src/fasta.cpp:1230-1233) are never written by
+            // TreeGroup::writeToFile; refused rather than applied to the primary block
+            if (p->nuc_mut_secondary && p->nuc_mut_secondary[k] != -1)
+                return fail(c, PM_ERR_UNSUPPORTED, "mutation on a secondary block (blockGaps)");
             const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
             int32_t n = (int32_t)(info >> 4);
             if (type > 5) continue;           // no-op types

@@ -50,6 +50,17 @@ def test_random_panmat_vs_oracle(engine, oracle, seed):
         assert got == want
 
 
+def test_secondary_block_mutation_is_refused(engine):
+    # a nucleotide mutation on a secondary block (blockGaps, which TreeGroup::writeToFile never
+    # writes) fails loudly instead of being applied to its primary block
+    rng = np.random.default_rng(11)
+    off, idx, root = random_tree(12, rng, max_children=3)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2)
+    pm.add_nuc_mut(pm.leaves()[0], 0, 1, -1, 0, [2], secondary=0)
+    with pytest.raises(panman_amd.PanmanError, match="secondary block"):
+        engine.fasta(pm, True)
+
+
 def test_long_blocks_wrap_vs_oracle(engine, oracle):
     rng = np.random.default_rng(5)
     off, idx, root = random_tree(30, rng, max_children=3)
