@@ -5,9 +5,10 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 SRC := $(wildcard panman_amd/csrc/*.cpp) $(wildcard panman_amd/csrc/*.hip)
 HDR := $(wildcard panman_amd/csrc/*.h) include/panman_gpu.h
 OBJ := $(patsubst panman_amd/csrc/%,build/%.o,$(SRC)) build/pm_build_id.o
-# build id = hash of every library source and header: profiles/traffic_fitch.json entries carry
-# the id they were measured on, and bench.py reports no PMC traffic for a different build
-BUILD_ID := $(shell cat $(sort $(SRC) $(HDR)) | sha256sum | cut -c1-16)
+# build id = hash of every library source and header and of the compile flags:
+# profiles/traffic_fitch.json entries carry the id they were measured on, and bench.py reports
+# no PMC traffic for a different build
+BUILD_ID := $(shell (cat $(sort $(SRC) $(HDR)); echo '$(HIPCC) $(HIPFLAGS)') | sha256sum | cut -c1-16)
 LIB := panman_amd/libpanman_amd.so
 CLI := bin/panmanUtils
 DEMO := bin/facade_demo
@@ -18,7 +19,7 @@ build/%.o: panman_amd/csrc/% $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-build/pm_build_id.o: $(SRC) $(HDR)
+build/pm_build_id.o: $(SRC) $(HDR) Makefile
 	@mkdir -p build
 	@printf 'extern "C" const char* pm_build_id(void) { return "%s"; }\n' $(BUILD_ID) > build/pm_build_id.cpp
 	g++ -O2 -fPIC -c build/pm_build_id.cpp -o $@
