@@ -15,11 +15,18 @@ DEMO := bin/facade_demo
 
 all: $(LIB) $(CLI) $(DEMO) oracle
 
-build/%.o: panman_amd/csrc/% $(HDR)
+# the compile line, rewritten only when it changes: a flag-only change (make HIPFLAGS=...)
+# rebuilds every object and the build id without a clean
+FLAGS_LINE := $(HIPCC) $(HIPFLAGS)
+build/flags.stamp: FORCE
+	@mkdir -p build
+	@echo '$(FLAGS_LINE)' | cmp -s - $@ || echo '$(FLAGS_LINE)' > $@
+
+build/%.o: panman_amd/csrc/% $(HDR) build/flags.stamp
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-build/pm_build_id.o: $(SRC) $(HDR) Makefile
+build/pm_build_id.o: $(SRC) $(HDR) Makefile build/flags.stamp
 	@mkdir -p build
 	@printf 'extern "C" const char* pm_build_id(void) { return "%s"; }\n' $(BUILD_ID) > build/pm_build_id.cpp
 	g++ -O2 -fPIC -c build/pm_build_id.cpp -o $@
@@ -46,4 +53,5 @@ clean:
 	rm -rf build bin $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean FORCE
+FORCE:

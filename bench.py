@@ -115,8 +115,12 @@ def main():
     eng = panman_amd.Engine(local)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
+    panman_amd.phase_reset()
     eng.tree_upload(off, idx, root)
     eng.synth_columns(lo, s_local, seed=2)
+    upload_phases = {}
+    for name, secs in panman_amd.phase_report():
+        upload_phases[name] = round(upload_phases.get(name, 0.0) + secs, 4)
     if args.no_subtree:
         eng.set_subtree(False)
     if args.narrow >= 0:
@@ -147,10 +151,12 @@ def main():
 
     mode = panman_amd.MODE_FITCH if args.mode == "fitch" else panman_amd.MODE_SANKOFF
     main_block = parsimony_block(args, eng, mode, ctx)
+    footprint = {"fitch" if mode == panman_amd.MODE_FITCH else "sankoff": eng.memory_footprint()}
     secondary = {}
     if mode == panman_amd.MODE_FITCH and "sankoff" in extra:
         log(rank, f"[bench] secondary: Sankoff on the same workload ({time.time() - t0:.1f}s)")
         secondary["sankoff"] = parsimony_block(args, eng, panman_amd.MODE_SANKOFF, ctx)
+        footprint["fitch+sankoff"] = eng.memory_footprint()   # (grow-only buffers: both modes' records)
         eng.run(mode)   # leave the context as the main line ran it (cpu-baseline parity sample)
         torch.cuda.synchronize()
 
@@ -203,12 +209,20 @@ def main():
                 "launch": ("hipGraph replay" if args.graph else "eager") + ", per-level kernels",
             },
             "roofline": main_block["roofline"],
+            "upload": {"phases_s": upload_phases,
+                       "scope": "tree flattening + descriptor upload (tree.*), on-device column generation, "
+                                "and the S2 / S3 side-by-side leaf copy (upload.sub_planes, k_sub_planes)"},
+            "footprint": {"device_bytes": footprint,
+                          "hbm_bytes_per_gpu": 288 * 2**30,
+                          "note": "pm_memory_footprint: device buffers the context holds after the run"},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "end_to_end": e2e,
             "commands": commands,
             "secondary": {k: {kk: v[kk] for kk in ("value", "unit", "ms_per_step", "metric", "roofline",
-                                                   "config", "cpu_baseline", "parity_sample")
+                                                   "config", "cpu_baseline", "parity_sample", "host_format_s",
+                                                   "format_phases_s", "end_to_end_leaf_col_per_s",
+                                                   "upload", "footprint")
                               if kk in v}
                           for k, v in secondary.items()} or None,
         }
@@ -550,14 +564,31 @@ def commands_block(args):
                                       "M2 20000x300 (serial TBB stand-in)": "19.47 s"},
            "runs": []}
 
+    def phases_of(pairs):
+        """(name, seconds) list -> {name: seconds}, repeated names summed."""
+        out = {}
+        for name, secs in pairs:
+            out[name] = round(out.get(name, 0.0) + secs, 4)
+        return out
+
     def run_cli(argv, cwd, stdout=None):
+        """Wall seconds of one CLI run, and its phase log (PANMAN_PHASES=1 on stderr)."""
+        env = dict(os.environ, PANMAN_PHASES="1")
         t = time.perf_counter()
         r = subprocess.run([cli] + argv, cwd=cwd, stdout=stdout or subprocess.PIPE, stderr=subprocess.PIPE,
-                           timeout=600)
+                           timeout=600, env=env)
         dt = time.perf_counter() - t
         if r.returncode != 0:
             raise RuntimeError(f"panmanUtils {' '.join(argv)}: {r.stderr.decode(errors='replace')[-400:]}")
-        return dt
+        pairs = []
+        for line in r.stderr.decode(errors="replace").splitlines():
+            name, tab, secs = line.rpartition("\t")
+            if tab and name and not name.startswith("#"):
+                try:
+                    pairs.append((name, float(secs)))
+                except ValueError:
+                    pass
+        return dt, phases_of(pairs)
 
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
         for leaves, sites in ((2000, 2000), (20000, 300)):
@@ -569,7 +600,7 @@ def commands_block(args):
             for low_mem in (False, True):
                 flag = ["--low-mem-mode"] if low_mem else []
                 try:
-                    gpu_s = run_cli(["-M", "a.fa", "-N", "t.nwk", "-o", "cmd"] + flag, tmp)
+                    gpu_s, cli_phases = run_cli(["-M", "a.fa", "-N", "t.nwk", "-o", "cmd"] + flag, tmp)
                 except (RuntimeError, subprocess.TimeoutExpired) as exc:
                     out["runs"].append({"command": f"-M {'--low-mem-mode ' if low_mem else ''}{leaves}x{sites}",
                                         "error": str(exc)})
@@ -577,9 +608,11 @@ def commands_block(args):
                 nt = threads if low_mem else 1
                 mode = panman_amd.MODE_SANKOFF if low_mem else panman_amd.MODE_FITCH
                 panman_amd.msa_build(nwk, msa, "", mode)   # warm (the first call pays the kernels' load)
+                panman_amd.phase_reset()
                 t = time.perf_counter()
                 gdump = panman_amd.msa_build(nwk, msa, "", mode)
                 gpu_drv_s = time.perf_counter() - t
+                drv_phases = phases_of(panman_amd.phase_report())
                 t = time.perf_counter()
                 dump = o.msa_build(nwk, msa, "", mode=1 if low_mem else 0, threads=nt)
                 cpu_s = time.perf_counter() - t
@@ -595,6 +628,7 @@ def commands_block(args):
                     "oracle_scope": "construction only (the CLI also starts a process, initialises HIP and writes "
                                     "the .panman: Cap'n Proto + xz level 9)",
                     "speedup_driver": round(cpu_s / gpu_drv_s, 2), "speedup_cli": round(cpu_s / gpu_s, 2),
+                    "gpu_cli_phases_s": cli_phases, "gpu_driver_phases_s": drv_phases,
                     "dumps_identical": gdump == dump, "oracle_nucmut_records": recs})
         # C5: -I <file> --fasta-aligned, text to stdout (discarded)
         from panman_amd.synth import c5_panmat
@@ -603,13 +637,24 @@ def commands_block(args):
         try:
             panman_amd.write_panman(path, [pm])
             with open(os.devnull, "wb") as devnull:
-                gpu_s = run_cli(["-I", path, "-m"], tmp, stdout=devnull)
+                gpu_s, cli_phases = run_cli(["-I", path, "-m"], tmp, stdout=devnull)
             eng = panman_amd.Engine(0)
             try:
-                eng.fasta(pm, True)   # warm
-                t = time.perf_counter()
-                gtext = eng.fasta(pm, True)
-                gpu_drv_s = time.perf_counter() - t
+                import ctypes as C
+                st, keep = pm.as_struct()
+                walls = []
+                for rep in range(3):   # warm-up, then the better of two timed calls
+                    ptr, n = C.c_void_p(), C.c_int64(0)
+                    panman_amd.phase_reset()
+                    t = time.perf_counter()
+                    eng._check(eng.lib.pm_fasta(eng.ctx, C.byref(st), 1, C.byref(ptr), C.byref(n)), "pm_fasta")
+                    walls.append(time.perf_counter() - t)
+                    phases = phases_of(panman_amd.phase_report())
+                    if rep < 2:
+                        eng.lib.pm_free(ptr)
+                gtext = eng._take_text(ptr, n)   # (the Python str copy: outside the timed call)
+                del keep
+                gpu_drv_s = min(walls[1:])
             finally:
                 eng.close()
             text, cpu_s = o.fasta(pm, True, timed=True, threads=threads)
@@ -619,7 +664,9 @@ def commands_block(args):
                             f"{len(text) / 1e9:.2f} GB",
                 "gpu_cli_wall_s": round(gpu_s, 3),
                 "gpu_driver_s": round(gpu_drv_s, 3),
-                "gpu_driver_scope": "pm_fasta in this process: replay, text on the device, D2H into host memory",
+                "gpu_driver_scope": "the pm_fasta C call in this process: flatten + upload, replay, text on the "
+                                    "device, download into one host buffer (the Python str copy excluded)",
+                "gpu_cli_phases_s": cli_phases, "gpu_driver_phases_s": phases,
                 "oracle_driver_s": round(cpu_s, 3), "oracle_threads": threads,
                 "oracle_scope": "replay + text in memory (the CLI also starts a process, loads and xz-decodes "
                                 "the file and writes the text)",
@@ -715,10 +762,17 @@ def replay_block(args, world, rank, local):
     kms = ms[3] / args.steps
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     # host formatting (aligned FASTA of every leaf)
+    ptr, n = C.c_void_p(), C.c_int64(0)
+    eng._check(eng.lib.pm_replay_format(eng.ctx, 1, C.byref(ptr), C.byref(n)), "pm_replay_format")
+    eng.lib.pm_free(ptr)   # (warm: the context's text buffer and pinned download slots)
+    panman_amd.phase_reset()
     tf = time.perf_counter()
     ptr, n = C.c_void_p(), C.c_int64(0)
     eng._check(eng.lib.pm_replay_format(eng.ctx, 1, C.byref(ptr), C.byref(n)), "pm_replay_format")
     fmt_s = time.perf_counter() - tf
+    fmt_phases = {}
+    for name, secs in panman_amd.phase_report():
+        fmt_phases[name] = round(fmt_phases.get(name, 0.0) + secs, 4)
     text = panman_amd.engine.bytes_at(ptr, n.value)   # (ctypes.string_at truncates past 2 GiB)
     eng.lib.pm_free(ptr)
     cpu = parity = None
@@ -770,6 +824,9 @@ def replay_block(args, world, rank, local):
                      "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,
                      "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},
         "host_format_s": round(fmt_s, 3),
+        "format_phases_s": fmt_phases,
+        "format_scope": "pm_replay_format: segment table (host), text kernels, download of the text into one "
+                        "host buffer (pinned slots drained by host threads)",
         "end_to_end_leaf_col_per_s": units / (kms * 1e-3 + fmt_s),
         "cpu_baseline": cpu, "parity_sample": parity,
     }

@@ -189,7 +189,7 @@ int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
  * The gathered unit is one chunk per rank of `per` = ceil(S/ranks)+3 u64 entries: entry 0 =
  * site_begin << 32 | count (count 0xffffffff: that rank failed), then one entry per site =
  * score (int32) | root code << 32.  The same layout moves through any other collective:
- *   pm_pack_site_results    the ctx's last run into a chunk in device memory (async);
+ *   pm_pack_site_results    the ctx's last run into a chunk in device memory; syncs;
  *   pm_unpack_site_results  ranks x per gathered entries (device) into score / root device
  *                           vectors; checks the heads (failed rank, overlaps, gaps); syncs.
  *   pm_chunk_entries / pm_chunk_pack / pm_chunk_unpack  the same on host memory, no GPU. */
@@ -221,11 +221,25 @@ int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_s
  * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
  * words, finals written, tail items.  `n` >= 5.  Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
+/* Device bytes the context holds now (n entries of): out[0] total, [1] leaf rows (code planes,
+ * presence, flags), [2] the S2 / S3 side-by-side leaf copy, [3] state-set records, [4] record
+ * masks, [5] Sankoff part counters, [6] mutation-record shards, [7] the flattened tree
+ * (descriptors, level tables), [8] per-site columns (consensus, forced, finals of the root,
+ * score, root code), [9] replay rows, FASTA text, gather and generator buffers.  No GPU call. */
+int pm_memory_footprint(pm_ctx* ctx, int64_t* out, int n);
 /* Hash of the library's sources (16 hex digits): profiled PMC traffic is tied to it. */
 const char* pm_build_id(void);
 /* Achievable HBM rate on `device`: a 16-B-per-lane streaming copy of `bytes` bytes, `reps`
  * times; *gbs = (read + write bytes) / s / 1e9. */
 int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs);
+
+/* Phase log: the drivers (pm_fasta, pm_msa_build / pm_msa_to_panman*, pm_panman_load /
+ * pm_panman_write, pm_create) append the wall time of each host / device phase of every
+ * call to one process-wide log.  pm_phase_report writes it as "name\tseconds\n" lines into
+ * buf (truncated to len - 1 bytes, NUL-terminated) and returns the bytes the whole report
+ * needs (with the NUL); pm_phase_reset empties it (it also stops growing at 4096 entries). */
+void pm_phase_reset(void);
+int64_t pm_phase_report(char* buf, int64_t len);
 
 /* ---- column drivers ------------------------------------------------------------------ */
 /* Drop-in for Tree(msa, newick, FILE_TYPE::MSA (mode PM_MODE_FITCH, "M1") or

@@ -102,6 +102,9 @@ _SIGS = {
     "pm_summary_compute": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Summary)]),
     "pm_design_bytes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "pm_build_id": (C.c_char_p, []),
+    "pm_phase_reset": (None, []),
+    "pm_memory_footprint": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "pm_phase_report": (C.c_int64, [C.c_char_p, C.c_int64]),
     "pm_stream_copy_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
@@ -111,6 +114,24 @@ def build_id() -> str:
     """Hash of the loaded library's sources (pm_build_id)."""
     lib = load()
     return lib.pm_build_id().decode() if hasattr(lib, "pm_build_id") else "unknown"
+
+
+def phase_reset() -> None:
+    """Empty the library's phase log (pm_phase_reset)."""
+    load().pm_phase_reset()
+
+
+def phase_report() -> list[tuple[str, float]]:
+    """(phase, seconds) the library's drivers logged since the last phase_reset."""
+    lib = load()
+    need = lib.pm_phase_report(None, 0)
+    buf = C.create_string_buffer(int(need))
+    lib.pm_phase_report(buf, need)
+    out = []
+    for line in buf.value.decode().splitlines():
+        name, _, secs = line.rpartition("\t")
+        out.append((name, float(secs)))
+    return out
 
 
 def header_symbols() -> list[str]:

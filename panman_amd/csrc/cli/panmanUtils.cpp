@@ -150,6 +150,12 @@ bool read_file(const std::string& path, std::string& out) {
     return true;
 }
 
+// a CLI phase in the same log as the library's (PANMAN_PHASES)
+void cli_phase(const char* name, Clock::time_point t0) {
+    if (const char* ph = std::getenv("PANMAN_PHASES"); ph && ph[0] == '1')
+        std::cerr << name << "\t" << ns_since(t0) * 1e-9 << "\n";
+}
+
 void print_error(const std::string& e) { std::cerr << "\033[1;31mError: " << e << "\033[0m\n"; }
 
 int build_from_msa(const Options& o, const std::vector<int>& devices) {
@@ -163,6 +169,7 @@ int build_from_msa(const Options& o, const std::vector<int>& devices) {
         return 1;
     }
     std::string msa, newick;
+    const auto r0 = Clock::now();
     if (!read_file(o.get("input-msa"), msa)) {
         print_error("cannot read " + o.get("input-msa"));
         return 1;
@@ -171,6 +178,7 @@ int build_from_msa(const Options& o, const std::vector<int>& devices) {
         print_error("cannot read " + o.get("input-newick"));
         return 1;
     }
+    cli_phase("cli.read_inputs", r0);
     const std::string ref = o.has("reference") ? o.get("reference") : "";
     const int mode = o.has("low-mem-mode") ? PM_MODE_SANKOFF : PM_MODE_FITCH;
     std::cout << "Creating PanMAN from MSA and Newick" << std::endl;
@@ -430,8 +438,10 @@ int from_panman(const Options& o, const std::vector<int>& devices) {
                 status = 1;
                 break;
             }
+            const auto w0 = Clock::now();
             if (!sink(aligned ? ".msa" : ".fasta", i, text, (size_t)len)) status = 1;
             pm_free(text);
+            cli_phase("cli.write_text", w0);
         }
         std::cout << "\nFASTA execution time: " << ns_since(f0) << " nanoseconds\n";
     }
@@ -439,9 +449,28 @@ int from_panman(const Options& o, const std::vector<int>& devices) {
     return status;
 }
 
+int run(int argc, char** argv);
+
 }  // namespace
 
+// PANMAN_PHASES=1: the library's phase log (pm_phase_report: HIP init, parse, upload, GPU
+// run, grouping, capnp, xz, download ...) and the CLI's own wall time, on stderr.
 int main(int argc, char** argv) {
+    pm_phase_reset();
+    const auto t0 = Clock::now();
+    const int rc = run(argc, argv);
+    const char* ph = std::getenv("PANMAN_PHASES");
+    if (ph && ph[0] == '1') {
+        std::vector<char> buf((size_t)pm_phase_report(nullptr, 0));
+        pm_phase_report(buf.data(), (int64_t)buf.size());
+        std::cerr << "#phases\n" << buf.data() << "cli.total\t" << ns_since(t0) * 1e-9 << "\n";
+    }
+    return rc;
+}
+
+namespace {
+
+int run(int argc, char** argv) {
     Options o;
     std::string err;
     if (!parse(argc, argv, o, err)) {
@@ -472,3 +501,5 @@ int main(int argc, char** argv) {
     usage(std::cerr);
     return 1;
 }
+
+}  // namespace

@@ -120,6 +120,10 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
 __global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#ifdef PM_UP_LDS_PAD   // occupancy experiments only: caps the resident workgroups per CU
+    __shared__ uint32_t occ_pad[PM_UP_LDS_PAD / 4];
+    if (a.count < 0) occ_pad[threadIdx.x] = 0;
+#endif
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);

@@ -151,7 +151,6 @@ int alloc_work(pm_ctx* c, int mode) {
     const size_t planes = fitch ? 20 : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
     const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * kMaskWords * sizeof(uint64_t);
-    const size_t need_fin = (size_t)c->dt.num_internal * wpad * sizeof(uint4);
     hipError_t e;
     if (need_sets > c->sets_bytes) {
         dev_free(c->sets);
@@ -164,12 +163,6 @@ int alloc_work(pm_ctx* c, int mode) {
         if ((e = hipMalloc(reinterpret_cast<void**>(&c->cmask), need_mask)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));
         c->cmask_bytes = need_mask;
-    }
-    if (need_fin > c->finals_bytes) {
-        dev_free(c->finals);
-        if ((e = hipMalloc(reinterpret_cast<void**>(&c->finals), need_fin)) != hipSuccess)
-            return fail(c, PM_ERR_OOM, std::string("finals: ") + hipGetErrorString(e));
-        c->finals_bytes = need_fin;
     }
     if (!fitch) {   // Sankoff nodes of out-degree > 255: part counters
         const size_t parts = (size_t)std::max(c->ht.part_off.empty() ? 0 : c->ht.part_off.back(),
@@ -212,7 +205,7 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
-                              (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->finals, (uint64_t)(uintptr_t)c->root_final,
+                              (uint64_t)(uintptr_t)c->cmask, (uint64_t)(uintptr_t)c->root_final,
                               (uint64_t)(uintptr_t)c->leaf_planes, (uint64_t)(uintptr_t)c->leaf_present,
                               (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
                               (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
@@ -339,7 +332,10 @@ int build_sub_planes(pm_ctx* c) {
             return fail(c, PM_ERR_OOM, std::string("subtree leaf layout: ") + hipGetErrorString(e));
         c->sub_planes_bytes = need;
     }
+    PhaseClock clock;
     if ((e = launch_sub_planes(c)) != hipSuccess) return hip_fail(c, e, "subtree leaf layout");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "subtree leaf layout");
+    clock.lap("upload.sub_planes");
     c->sub_planes_ok = true;
     return PM_OK;
 }
@@ -378,6 +374,7 @@ extern "C" {
 int pm_create(int device, pm_ctx** out) {
     if (!out) return PM_ERR_ARG;
     *out = nullptr;
+    PhaseClock clock;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0) return PM_ERR_HIP;
@@ -397,6 +394,7 @@ int pm_create(int device, pm_ctx** out) {
     }
     c->stream = c->own_stream;
     *out = c;
+    clock.lap("hip.create_context");
     return PM_OK;
 }
 
@@ -409,6 +407,7 @@ void pm_destroy(pm_ctx* c) {
     free_tree(c->dt);
     free_replay(c);
     comm_release(c);
+    free_hostio(c);
     for (auto& v : c->timers)
         for (auto& t : v) {
             (void)hipEventDestroy(t.a);
@@ -489,8 +488,12 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     const bool timing = std::getenv("PM_UPLOAD_TIMING") != nullptr;
     auto t_last = std::chrono::steady_clock::now();
     auto upload_phase = [&](const char* what) {
-        if (!timing) return;
         const auto now = std::chrono::steady_clock::now();
+        phase_add(std::string("tree.") + what, std::chrono::duration<double>(now - t_last).count());
+        if (!timing) {
+            t_last = now;
+            return;
+        }
         std::fprintf(stderr, "[pm_tree_upload] %-16s %8.2f s\n", what, std::chrono::duration<double>(now - t_last).count());
         t_last = now;
     };
@@ -1067,41 +1070,47 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     dt.num_leaves = L;
     dt.root_dense = ht.dense_of[t->root];
     hipError_t e;
-    if ((e = upload(&dt.child_off, ht.child_off, c->stream)) != hipSuccess ||
-        (e = upload(&dt.child_enc, ht.child_enc, c->stream)) != hipSuccess ||
-        (e = upload(&dt.parent_dense, parent_dense, c->stream)) != hipSuccess ||
-        (e = upload(&dt.internal_id, ht.internal_id, c->stream)) != hipSuccess ||
-        (e = upload(&dt.leaf_id, ht.leaf_id, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_order, up_order, c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_order, down_order, c->stream)) != hipSuccess ||
-        (e = upload(&dt.leaf_parent, leaf_parent, c->stream)) != hipSuccess ||
-        (e = upload(&dt.leaf_down, leaf_down, c->stream)) != hipSuccess ||
-        (e = upload(&dt.child_enc_v, child_enc_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_order_v, up_order_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_order_v, down_order_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_desc, down_desc, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc, up_desc_p, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_v, up_desc_vp, c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_desc_v, down_desc_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.vleaf, vleaf, c->stream)) != hipSuccess ||
-        (e = upload(&dt.tail_desc, tail_desc, c->stream)) != hipSuccess ||
-        (e = upload(&dt.tail_desc_v, tail_desc_v, c->stream)) != hipSuccess ||
-        (e = upload(&dt.part_desc, part_desc[0], c->stream)) != hipSuccess ||
-        (e = upload(&dt.part_desc_v, part_desc[1], c->stream)) != hipSuccess ||
-        (e = upload(&dt.part_desc_k, part_desc[2], c->stream)) != hipSuccess ||
-        (e = upload(&dt.part_desc_gs, part_desc[3], c->stream)) != hipSuccess ||
-        (e = upload(&dt.child_enc_k, child_enc_k, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_k, up_desc_kp, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_g, up_desc_g, c->stream)) != hipSuccess ||
-        (e = upload(&dt.up_desc_gs, up_desc_gs, c->stream)) != hipSuccess ||
-        (e = upload(&dt.down_desc_k, down_desc_k, c->stream)) != hipSuccess ||
-        (e = upload(&dt.vinner, vinner, c->stream)) != hipSuccess ||
-        (e = upload(&dt.tail_desc_k, tail_desc_k, c->stream)) != hipSuccess ||
-        (e = upload(&dt.lvl, lvl, c->stream)) != hipSuccess) {
+    size_t tree_bytes = 0;   // (pm_memory_footprint)
+    auto up = [&](auto** dst, const auto& v) {
+        tree_bytes += sizeof(v[0]) * v.size();
+        return upload(dst, v, c->stream);
+    };
+    if ((e = up(&dt.child_off, ht.child_off)) != hipSuccess ||
+        (e = up(&dt.child_enc, ht.child_enc)) != hipSuccess ||
+        (e = up(&dt.parent_dense, parent_dense)) != hipSuccess ||
+        (e = up(&dt.internal_id, ht.internal_id)) != hipSuccess ||
+        (e = up(&dt.leaf_id, ht.leaf_id)) != hipSuccess ||
+        (e = up(&dt.up_order, up_order)) != hipSuccess ||
+        (e = up(&dt.down_order, down_order)) != hipSuccess ||
+        (e = up(&dt.leaf_parent, leaf_parent)) != hipSuccess ||
+        (e = up(&dt.leaf_down, leaf_down)) != hipSuccess ||
+        (e = up(&dt.child_enc_v, child_enc_v)) != hipSuccess ||
+        (e = up(&dt.up_order_v, up_order_v)) != hipSuccess ||
+        (e = up(&dt.down_order_v, down_order_v)) != hipSuccess ||
+        (e = up(&dt.down_desc, down_desc)) != hipSuccess ||
+        (e = up(&dt.up_desc, up_desc_p)) != hipSuccess ||
+        (e = up(&dt.up_desc_v, up_desc_vp)) != hipSuccess ||
+        (e = up(&dt.down_desc_v, down_desc_v)) != hipSuccess ||
+        (e = up(&dt.vleaf, vleaf)) != hipSuccess ||
+        (e = up(&dt.tail_desc, tail_desc)) != hipSuccess ||
+        (e = up(&dt.tail_desc_v, tail_desc_v)) != hipSuccess ||
+        (e = up(&dt.part_desc, part_desc[0])) != hipSuccess ||
+        (e = up(&dt.part_desc_v, part_desc[1])) != hipSuccess ||
+        (e = up(&dt.part_desc_k, part_desc[2])) != hipSuccess ||
+        (e = up(&dt.part_desc_gs, part_desc[3])) != hipSuccess ||
+        (e = up(&dt.child_enc_k, child_enc_k)) != hipSuccess ||
+        (e = up(&dt.up_desc_k, up_desc_kp)) != hipSuccess ||
+        (e = up(&dt.up_desc_g, up_desc_g)) != hipSuccess ||
+        (e = up(&dt.up_desc_gs, up_desc_gs)) != hipSuccess ||
+        (e = up(&dt.down_desc_k, down_desc_k)) != hipSuccess ||
+        (e = up(&dt.vinner, vinner)) != hipSuccess ||
+        (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
+        (e = up(&dt.lvl, lvl)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
     c->dt = dt;
+    c->tree_bytes = tree_bytes;
     c->ht = std::move(ht);
     c->max_degree = 0;
     for (int32_t d = 0; d < I; ++d) c->max_degree = std::max(c->max_degree, c->ht.child_off[d + 1] - c->ht.child_off[d]);
@@ -1288,12 +1297,17 @@ int pm_synth_columns(pm_ctx* c, int64_t site_begin, int64_t S, uint64_t seed) {
     (void)hipSetDevice(c->device);
     int rc = alloc_columns(c, S);
     if (rc != PM_OK) return rc;
-    rc = alloc_work(c, PM_MODE_FITCH);   // the generator stages internal sequences in `finals`
-    if (rc != PM_OK) return rc;
+    // the generator stages internal sequences in `finals` ([I][W] uint4), scratch freed after it
+    // (15 GB at 1M leaves x 30k sites that a run does not need)
+    hipError_t e = dev_alloc(&c->finals, (size_t)c->dt.num_internal * wpad_of(c));
+    if (e != hipSuccess) return fail(c, PM_ERR_OOM, std::string("generator scratch: ") + hipGetErrorString(e));
+    c->finals_bytes = sizeof(uint4) * (size_t)c->dt.num_internal * wpad_of(c);
     std::vector<uint8_t> flag(c->dt.num_leaves, kLeafPresent);
-    hipError_t e = hipMemcpyAsync(c->leaf_flag, flag.data(), flag.size(), hipMemcpyHostToDevice, c->stream);
+    e = hipMemcpyAsync(c->leaf_flag, flag.data(), flag.size(), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_synth(c, site_begin, seed);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(c->finals);
+    c->finals_bytes = 0;
     if (e != hipSuccess) return hip_fail(c, e, "synthetic columns");
     c->has_leaves = c->has_sites = true;
     c->leaves_all_present = true;

@@ -17,7 +17,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -196,6 +198,7 @@ struct pm_ctx {
 
     pm::HostTree ht;
     pm::DevTree dt;
+    size_t tree_bytes = 0;            // device bytes of the flattened tree (descriptors, level tables)
     bool has_tree = false;
     int32_t max_degree = 0;
     bool virtual_leaf_parents = true; // Fitch: leaf-parents evaluated inline (PM_OPT_VIRTUAL)
@@ -262,6 +265,15 @@ struct pm_ctx {
     int comm_rank = 0, comm_size = 1;
     void* gather_buf = nullptr;       // [send chunk | ranks x chunk] packed site results
     size_t gather_bytes = 0;
+
+    // grow-only buffers kept between calls (pm_hostio.cpp): pinned download slots, the FASTA
+    // text and replay rows on the device
+    void* stage = nullptr;
+    hipEvent_t stage_ev[3] = {nullptr, nullptr, nullptr};
+    void* text_buf = nullptr;
+    size_t text_cap = 0;
+    void* rows_buf = nullptr;
+    size_t rows_cap = 0;
 };
 
 namespace pm {
@@ -299,6 +311,25 @@ hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t 
 void free_replay(pm_ctx* c);
 void comm_release(pm_ctx* c);   // pm_rccl.hip
 int leaves_install(pm_ctx* c, int64_t S, const uint8_t* d_codes4, int64_t row_stride, const int32_t* node_row);
+
+// host plumbing (pm_hostio.cpp)
+// Phase log (pm_phase_report): drivers append (name, seconds) of their host / device phases.
+void phase_add(const std::string& name, double seconds);
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t;
+    PhaseClock();
+    double lap(const char* name);   // seconds since construction / the last lap, logged as `name`
+};
+int host_threads();   // host worker threads (PM_HOST_THREADS, else min(16, cores))
+void host_parallel_for(int tasks, const std::function<void(int)>& fn);
+// malloc with transparent huge pages requested for large blocks (released with free / pm_free)
+void* host_alloc_large(size_t n);
+// dst (pageable host) <- src (device), n bytes, through pinned slots drained by host threads;
+// synchronous on the ctx stream
+hipError_t d2h_large(pm_ctx* c, void* dst, const void* src, size_t n);
+// *buf grown (contents dropped) to hold `need` bytes
+hipError_t grow_device(void** buf, size_t* cap, size_t need);
+void free_hostio(pm_ctx* c);
 
 // replay kernels (pm_replay.hip)
 struct ReplayDev {

@@ -103,6 +103,7 @@ struct MsaResult {
 MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_c, int mode,
                        const std::vector<int>& devices) {
     MsaResult res;
+    PhaseClock clock;
     std::string newick(newick_c), err;
     const size_t nl = newick.find('\n');
     if (nl != std::string::npos) newick.resize(nl);
@@ -151,6 +152,7 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
 
     res.consensus = consensus;
     res.muts.assign(t.name.size(), {});
+    clock.lap("msa.parse");
     if (width == 0) return res;
 
     // CSR + leaf rows (rows in name order; leaves missing from the alignment are absent)
@@ -202,9 +204,11 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
     for (int g = 0; g < G; ++g)
         for (int h = 0; h < g; ++h) distinct &= devices[g] != devices[h];
     for (int g = 0; g < G && distinct; ++g) distinct &= lo[g + 1] > lo[g];
+    clock.lap("msa.pack_columns");
     std::vector<CtxGuard> cg(G);
     for (int g = 0; g < G; ++g)
         if (pm_create(devices[g], &cg[g].c) != PM_OK) return dump_error("no HIP device " + std::to_string(devices[g]));
+    clock.lap("hip.create_contexts");
     auto each = [&](auto&& fn) {   // one host thread per shard
         std::vector<std::thread> th;
         for (int g = 0; g < G; ++g)
@@ -225,6 +229,11 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
             (!distinct && pm_run(cg[g].c, mode) != PM_OK))
             msg[g] = pm_last_error(cg[g].c);
     });
+    clock.lap("msa.upload");
+    if (uploaded && !distinct)
+        each([&](int g) {
+            if (hipStreamSynchronize(cg[g].c->stream) != hipSuccess) msg[g] = "GPU run failed";
+        });
     std::vector<int32_t> score;
     if (uploaded && distinct) {
         std::vector<pm_ctx*> ctxs(G);
@@ -234,6 +243,7 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
             pm_multi_run(ctxs.data(), G, mode, lo.data(), S, score.data(), nullptr) != PM_OK)
             return dump_error(std::string("multi-GPU run: ") + pm_last_error(ctxs[0]));
     }
+    clock.lap("msa.gpu_run");
     if (uploaded)
         each([&](int g) {
             int64_t n = 0;
@@ -258,6 +268,7 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
             for (const pm_mut& m : v) nonroot += m.node != (uint32_t)t.root;
         if (total != nonroot) return dump_error("gathered parsimony score disagrees with the shards' records");
     }
+    clock.lap("msa.fetch_records");
     std::vector<pm_mut> recs;
     for (auto& v : part) recs.insert(recs.end(), v.begin(), v.end());
     if (G > 1) std::stable_sort(recs.begin(), recs.end(), [](const pm_mut& x, const pm_mut& y) { return x.node < y.node; });
@@ -269,6 +280,7 @@ MsaResult build_result(const char* newick_c, const char* msa_c, const char* ref_
         group_node(recs.data() + a, b - a, res.muts[recs[a].node]);
         a = b;
     }
+    clock.lap("msa.group");
     return res;
 }
 
@@ -339,6 +351,7 @@ int pm_msa_to_panman_multi(const char* newick, const char* msa_text, const char*
         set_err(r.err);
         return PM_ERR_ARG;
     }
+    const auto t_conv = std::chrono::steady_clock::now();
     const int32_t N = (int32_t)r.t.name.size();
     std::vector<int32_t> off(N + 1, 0), idx;
     std::string names;
@@ -395,6 +408,7 @@ int pm_msa_to_panman_multi(const char* newick, const char* msa_text, const char*
     p.nuc_mut_nucs = nnucs.data();
     p.branch_length = r.t.length.data();
     const pm_panmat* list[1] = {&p};
+    pm::phase_add("msa.to_panmat", std::chrono::duration<double>(std::chrono::steady_clock::now() - t_conv).count());
     const int rc = pm_panman_write(out_path, list, 1, 1);
     if (rc != PM_OK) set_err(std::string("cannot write ") + out_path);
     return rc;

@@ -857,6 +857,7 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
     };
     if (!path || !out) return PM_ERR_ARG;
     *out = nullptr;
+    PhaseClock clock;
     FILE* f = std::fopen(path, "rb");
     if (!f) { set_err(std::string("cannot open ") + path); return PM_ERR_ARG; }
     std::vector<uint8_t> raw;
@@ -864,6 +865,7 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
     size_t n;
     while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
     std::fclose(f);
+    clock.lap("panman.read_file");
     Msg m;
     std::string e;
     const bool is_xz = raw.size() >= 6 && raw[0] == 0xFD && raw[1] == '7' && raw[2] == 'z' && raw[3] == 'X';
@@ -872,6 +874,7 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
     } else {
         m.bytes.swap(raw);   // an uncompressed capnp message is accepted too
     }
+    clock.lap("panman.xz_decode");
     if (!m.init()) { set_err(m.err); return PM_ERR_ARG; }
     Struct tg;
     if (!read_struct(m, 0, 0, tg)) { set_err(m.err); return PM_ERR_ARG; }
@@ -885,6 +888,7 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
             delete pm_;
             return PM_ERR_ARG;
         }
+    clock.lap("panman.capnp_decode");
     *out = pm_;
     return PM_OK;
 }
@@ -951,6 +955,7 @@ void pm_panman_free(pm_panman* p) { delete p; }
 
 int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, int compress) {
     if (!path || (!trees && count > 0) || count < 0) return PM_ERR_ARG;
+    PhaseClock clock;
     Writer wr;
     const size_t tg = wr.alloc(2);
     wr.struct_ptr(0, tg, 0, 2);
@@ -963,8 +968,10 @@ int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, 
     std::memcpy(msg.data() + 8, wr.w.data(), wr.w.size() * 8);
     std::vector<uint8_t> outb;
     std::string e;
+    clock.lap("panman.capnp_encode");
     if (compress) {
         if (!xz_encode(msg.data(), msg.size(), outb, e)) return PM_ERR_HIP;
+        clock.lap("panman.xz_encode");
     } else {
         outb.swap(msg);
     }
@@ -972,6 +979,7 @@ int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, 
     if (!f) return PM_ERR_ARG;
     const bool ok = std::fwrite(outb.data(), 1, outb.size(), f) == outb.size();
     std::fclose(f);
+    clock.lap("panman.write_file");
     return ok ? PM_OK : PM_ERR_ARG;
 }
 

@@ -123,23 +123,32 @@ int32_t* gather_status(pm_ctx* c, int64_t per) {
     return reinterpret_cast<int32_t*>(static_cast<uint64_t*>(c->gather_buf) + (size_t)per * (c->comm_size + 1));
 }
 
-// pm_run on the ctx's shard, record-buffer overflow settled (a re-run with a bigger buffer:
-// the score counts only stored records), then the packed chunk into the send buffer.  On a
-// local failure the chunk carries the failed head instead, so the caller still joins the
-// collective and every rank learns of it from the heads.
-int enqueue_shard(pm_ctx* c, int mode, int64_t total_sites, int64_t site_begin, int64_t per) {
-    int rc = PM_OK;
+// A rank's shard in two halves, so that one process driving several GPUs (pm_multi_run)
+// queues every rank's pm_run before it waits on any of them.
+//
+// shard_begin: the send chunk is stamped "failed" first (memset, its error checked: a chunk
+// is failed until a successful pack overwrites it, so a rank whose run or pack breaks can
+// never hand the others a previous call's healthy results), then pm_run on the shard.
+int shard_begin(pm_ctx* c, int mode, int64_t total_sites, int64_t site_begin, int64_t per) {
+    uint32_t* head = static_cast<uint32_t*>(c->gather_buf);   // little-endian u64: count low, begin high
+    hipError_t e = hipMemsetD32Async(head, kChunkFailed, 1, c->stream);
+    if (e == hipSuccess) e = hipMemsetD32Async(head + 1, 0u, 1, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "stamp send chunk");
     if (site_begin < 0 || site_begin > UINT32_MAX || c->num_sites > per - 1 || site_begin + c->num_sites > total_sites)
-        rc = fail(c, PM_ERR_ARG, "shard outside [0, total_sites) or wider than ceil(total / ranks) + 2");
-    if (rc == PM_OK) rc = pm_run(c, mode);
+        return fail(c, PM_ERR_ARG, "shard outside [0, total_sites) or wider than ceil(total / ranks) + 2");
+    return pm_run(c, mode);
+}
+
+// shard_finish: record-buffer overflow settled (a re-run with a bigger buffer: the score
+// counts only stored records), then the packed chunk into the send buffer.  A failed rank's
+// chunk keeps the failed head, so the caller still joins the collective and every rank
+// learns of it from the heads.
+int shard_finish(pm_ctx* c, int rc, int64_t site_begin) {
     if (rc == PM_OK) rc = settle_run(c);
-    const bool ok = rc == PM_OK;
-    const int64_t count = ok ? c->num_sites : 0;
-    hipLaunchKernelGGL(k_pack_results, dim3((unsigned)((count + kBlock) / kBlock)), dim3(kBlock), 0, c->stream,
-                       ok ? c->score : nullptr, ok ? c->root_code : nullptr, site_begin, count, ok,
-                       static_cast<uint64_t*>(c->gather_buf));
-    const hipError_t e = hipGetLastError();
     if (rc != PM_OK) return rc;
+    hipLaunchKernelGGL(k_pack_results, dim3((unsigned)((c->num_sites + kBlock) / kBlock)), dim3(kBlock), 0, c->stream,
+                       c->score, c->root_code, site_begin, c->num_sites, true, static_cast<uint64_t*>(c->gather_buf));
+    const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PM_OK : hip_fail(c, e, "pack site results");
 }
 
@@ -235,7 +244,7 @@ int pm_run_gather(pm_ctx* c, int mode, int64_t total_sites, int64_t site_begin, 
     int rc = ensure_gather(c, per);   // (a rank that cannot allocate a few KiB cannot join)
     if (rc != PM_OK) return rc;
     // rank-specific work: a failure is carried in this rank's chunk head, the collective joined
-    const int local = enqueue_shard(c, mode, total_sites, site_begin, per);
+    const int local = shard_finish(c, shard_begin(c, mode, total_sites, site_begin, per), site_begin);
     rc = gather_call(c, per);
     if (rc == PM_OK) rc = enqueue_unpack(c, static_cast<const uint64_t*>(c->gather_buf) + per, total_sites, per,
                                          score_device, root_device);
@@ -253,7 +262,10 @@ int pm_pack_site_results(pm_ctx* c, int64_t site_begin, int64_t per, void* chunk
         return fail(c, PM_ERR_ARG, "shard wider than the chunk (per - 1 sites)");
     hipLaunchKernelGGL(k_pack_results, dim3((unsigned)((c->num_sites + kBlock) / kBlock)), dim3(kBlock), 0, c->stream,
                        c->score, c->root_code, site_begin, c->num_sites, true, static_cast<uint64_t*>(chunk_device));
-    const hipError_t e = hipGetLastError();
+    // synchronous: the caller's collective may run on another stream (torch's), which nothing
+    // orders after this one
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     return e == hipSuccess ? PM_OK : hip_fail(c, e, "pack site results");
 }
 
@@ -324,7 +336,12 @@ int pm_multi_run(pm_ctx* const* ctxs, int n, int mode, const int64_t* site_begin
             hipMalloc(&out_r[i], (size_t)total_sites) != hipSuccess)
             rc = fail(ctxs[i], PM_ERR_OOM, "gathered results");
         if (rc == PM_OK) rc = ensure_gather(ctxs[i], per);
-        if (rc == PM_OK) rc = enqueue_shard(ctxs[i], mode, total_sites, site_begin[i], per);
+        if (rc == PM_OK) rc = shard_begin(ctxs[i], mode, total_sites, site_begin[i], per);
+    }
+    // every rank's run is queued before the first wait: the GPUs run their shards together
+    for (int i = 0; i < n && rc == PM_OK; ++i) {
+        (void)hipSetDevice(ctxs[i]->device);
+        rc = shard_finish(ctxs[i], rc, site_begin[i]);
     }
     if (rc == PM_OK) {   // one process drives every rank: the collective is one RCCL group
         (void)rccl().group_start();

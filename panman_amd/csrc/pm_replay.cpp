@@ -47,6 +47,7 @@ hipError_t dput(T** dst, const std::vector<T>& v, hipStream_t s) {
 }  // namespace
 
 int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin, int64_t leaf_end) {
+    PhaseClock clock;
     const int32_t N = p->num_nodes;
     if (N < 1 || p->root < 0 || p->root >= N || !p->child_offsets || !p->names)
         return fail(c, PM_ERR_ARG, "bad PanMAT topology");
@@ -296,12 +297,16 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         tile_blk[t] = id;
     }
 
+    clock.lap("replay.prepare_host");
     // ---- device
     std::vector<char> cons_row(stride, '-');
     std::memcpy(cons_row.data(), cons.data(), cons.size());
     hipError_t e;
-    if ((e = hipMalloc(reinterpret_cast<void**>(&r.d_rows), (size_t)std::max<int64_t>(L, 1) * stride)) != hipSuccess)
+    // (the rows live in the context's grow-only buffer: a 5 GB hipMalloc + hipFree per call
+    // is not free, and pm_fasta prepares again on every call)
+    if ((e = grow_device(&c->rows_buf, &c->rows_cap, (size_t)std::max<int64_t>(L, 1) * stride)) != hipSuccess)
         return fail(c, PM_ERR_OOM, "replay rows");
+    r.d_rows = static_cast<char*>(c->rows_buf);
     if ((e = dput(&r.d_cons, cons_row, c->stream)) != hipSuccess || (e = dput(&r.d_parent, r.parent, c->stream)) != hipSuccess ||
         (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, presence, c->stream)) != hipSuccess ||
         (e = dput(&r.d_eoff, eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, ecol, c->stream)) != hipSuccess ||
@@ -311,6 +316,7 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         (e = dput(&r.d_path_off, path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, path_all, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
+    clock.lap("replay.upload");
     ReplayDev& d = r.dev;
     d.leaves = L;
     d.row_stride = stride;
@@ -336,14 +342,10 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     return PM_OK;
 }
 
-namespace {
-
-}  // namespace
-
 void free_replay(pm_ctx* c) {
     if (!c->replay) return;
     ReplayState* r = c->replay;
-    dfree(r->d_rows);
+    r->d_rows = nullptr;   // (c->rows_buf, kept)
     dfree(r->d_cons);
     dfree(r->d_parent);
     dfree(r->d_leaf);
@@ -407,12 +409,15 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     if (!c || !text || !length) return PM_ERR_ARG;
     if (!c->replay || !c->replay->ran) return fail(c, PM_ERR_STATE, "run the replay first");
     (void)hipSetDevice(c->device);
+    PhaseClock clock;
     const ReplayState& r = *c->replay;
     const int32_t L = (int32_t)r.leaves.size();
     const int32_t M = r.max_id + 1;
     std::vector<FmtSeg> seg((size_t)L * M);
+    const int32_t LB = 64;   // leaves per host task
+    host_parallel_for((L + LB - 1) / LB, [&](int task) {
     std::vector<int32_t> order(M);
-    for (int32_t li = 0; li < L; ++li) {
+    for (int32_t li = task * LB; li < std::min(L, (task + 1) * LB); ++li) {
         for (int32_t i = 0; i < M; ++i) order[i] = i;
         const auto& ex = r.exists[li];
         if (r.rotation[li] != 0) {   // rotate to the rotationIndexes-th existing block (:1950-1964)
@@ -434,6 +439,7 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
             }
         }
     }
+    });
     std::vector<int64_t> name_off(L + 1, 0);
     std::string names;
     for (int32_t li = 0; li < L; ++li) {
@@ -444,11 +450,12 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     FmtSeg* d_seg = nullptr;
     int64_t *d_len = nullptr, *d_off = nullptr, *d_line = nullptr, *d_start = nullptr, *d_text_off = nullptr,
             *d_name_off = nullptr;
-    char *d_names = nullptr, *d_text = nullptr;
+    char *d_names = nullptr, *d_text = nullptr;   // (d_text: the context's grow-only text buffer)
     auto cleanup = [&]() {
         dfree(d_seg); dfree(d_len); dfree(d_off); dfree(d_line); dfree(d_start); dfree(d_text_off);
-        dfree(d_name_off); dfree(d_names); dfree(d_text);
+        dfree(d_name_off); dfree(d_names);
     };
+    clock.lap("fasta.segments_host");
     hipError_t e = dput(&d_seg, seg, c->stream);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_len), sizeof(int64_t) * std::max<size_t>(NS, 1));
     if (e != hipSuccess) {
@@ -486,20 +493,16 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
         text_off[li + 1] = text_off[li] + hdr + p + p / 70 + 1;
     }
     const int64_t total = text_off[L];
-    char* out = static_cast<char*>(std::malloc((size_t)total + 1));
-    if (!out) {
-        cleanup();
-        return fail(c, PM_ERR_OOM, "FASTA text");
-    }
+    clock.lap("fasta.count");
     if ((e = dput(&d_off, off, c->stream)) != hipSuccess || (e = dput(&d_line, line, c->stream)) != hipSuccess ||
         (e = dput(&d_start, start, c->stream)) != hipSuccess || (e = dput(&d_text_off, text_off, c->stream)) != hipSuccess ||
         (e = dput(&d_name_off, name_off, c->stream)) != hipSuccess ||
         (e = dput(&d_names, std::vector<char>(names.begin(), names.end()), c->stream)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&d_text), (size_t)std::max<int64_t>(total, 1))) != hipSuccess) {
-        std::free(out);
+        (e = grow_device(&c->text_buf, &c->text_cap, (size_t)std::max<int64_t>(total, 1))) != hipSuccess) {
         cleanup();
         return fail(c, PM_ERR_OOM, "FASTA buffers");
     }
+    d_text = static_cast<char*>(c->text_buf);
     f.seg_off = d_off;
     f.line_len = d_line;
     f.start = d_start;
@@ -508,14 +511,22 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     f.names = d_names;
     f.text = d_text;
     e = launch_fmt_write(c, f, L);
-    if (e == hipSuccess && total) e = hipMemcpyAsync(out, d_text, (size_t)total, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    clock.lap("fasta.text_kernel");
+    char* out = e == hipSuccess ? static_cast<char*>(host_alloc_large((size_t)total + 1)) : nullptr;
+    if (e == hipSuccess && !out) {
+        cleanup();
+        return fail(c, PM_ERR_OOM, "FASTA text");
+    }
+    // the text through pinned slots drained by host threads (pm_hostio.cpp), not one pageable copy
+    if (e == hipSuccess) e = d2h_large(c, out, d_text, (size_t)total);
     cleanup();
     if (e != hipSuccess) {
         std::free(out);
         return hip_fail(c, e, "FASTA write");
     }
     out[total] = 0;
+    clock.lap("fasta.download");
     *text = out;
     *length = total;
     return PM_OK;
@@ -523,7 +534,12 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
 
 int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* length) {
     int rc = pm_replay_prepare(c, p);
-    if (rc == PM_OK) rc = pm_replay_run(c);
+    if (rc == PM_OK) {
+        PhaseClock clock;
+        rc = pm_replay_run(c);
+        if (rc == PM_OK && c && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, PM_ERR_HIP, "replay");
+        clock.lap("replay.kernel");
+    }
     if (rc == PM_OK) rc = pm_replay_format(c, aligned, text, length);
     return rc;
 }
@@ -572,18 +588,36 @@ int pm_fasta_multi(const pm_panmat* p, int aligned, const int* devices, int num_
         }
         total += plen[g];
     }
-    char* out = static_cast<char*>(std::malloc((size_t)total + 1));
+    int nonempty = 0, only = -1;
+    for (int g = 0; g < G; ++g)
+        if (part[g]) {
+            ++nonempty;
+            only = g;
+        }
+    if (nonempty == 1) {   // one shard holds every leaf: its text is the result
+        for (int g = 0; g < G; ++g)
+            if (g != only) std::free(part[g]);
+        *text = part[only];
+        *length = plen[only];
+        return PM_OK;
+    }
+    char* out = static_cast<char*>(host_alloc_large((size_t)total + 1));
     if (!out) {
         for (char* x : part) std::free(x);
         set_err("FASTA text");
         return PM_ERR_OOM;
     }
-    int64_t at = 0;
-    for (int g = 0; g < G; ++g) {
-        if (plen[g]) std::memcpy(out + at, part[g], (size_t)plen[g]);
-        at += plen[g];
-        std::free(part[g]);
-    }
+    std::vector<int64_t> at(G + 1, 0);
+    for (int g = 0; g < G; ++g) at[g + 1] = at[g] + plen[g];
+    constexpr int64_t kPiece = (int64_t)8 << 20;   // concatenation by host threads, 8 MiB pieces
+    std::vector<std::pair<int, int64_t>> pieces;
+    for (int g = 0; g < G; ++g)
+        for (int64_t a = 0; a < plen[g]; a += kPiece) pieces.emplace_back(g, a);
+    host_parallel_for((int)pieces.size(), [&](int i) {
+        const auto [g, a] = pieces[i];
+        std::memcpy(out + at[g] + a, part[g] + a, (size_t)std::min(kPiece, plen[g] - a));
+    });
+    for (char* x : part) std::free(x);
     out[total] = 0;
     *text = out;
     *length = total;

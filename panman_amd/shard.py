@@ -46,8 +46,12 @@ def gather_site_results_device(engine, site_begin: int, sites: int, score_all: t
     world = dist.get_world_size(group)
     per = chunk_entries(sites, world)
     chunk = torch.empty(per, dtype=torch.int64, device=score_all.device)
-    engine.pack_site_results(site_begin, per, chunk.data_ptr())
+    engine.pack_site_results(site_begin, per, chunk.data_ptr())   # returns with the chunk written
     allc = gather_chunks(chunk, group)
+    # the collective ran on torch's stream, the unpack runs on the engine's: wait for it here
+    # (the unpack itself synchronises its stream before returning)
+    if allc.is_cuda:
+        torch.cuda.current_stream(allc.device).synchronize()
     engine.unpack_site_results(allc.data_ptr(), per, world, sites, score_all.data_ptr(), root_all.data_ptr())
 
 

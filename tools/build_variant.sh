@@ -21,5 +21,10 @@ for f in $src/*.cpp $src/*.hip; do
   objs+=("$o")
 done
 wait
-/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o "$out/libpanman_amd.so" "${objs[@]}" -l:liblzma.so.5
+# the variant's own build id: its (possibly patched) sources, headers and compile flags, so
+# PMC traffic stamped for another build is never reported against it
+id=$( (cat $(ls $src/*.cpp $src/*.hip $src/*.h | sort) include/panman_gpu.h; echo "variant $flags") | sha256sum | cut -c1-16)
+printf 'extern "C" const char* pm_build_id(void) { return "%s"; }\n' "$id" > "$out/pm_build_id.cpp"
+g++ -O2 -fPIC -c "$out/pm_build_id.cpp" -o "$out/pm_build_id.o"
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o "$out/libpanman_amd.so" "${objs[@]}" "$out/pm_build_id.o" -l:liblzma.so.5
 echo "$out/libpanman_amd.so"
