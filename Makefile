@@ -31,8 +31,9 @@ build/pm_build_id.o: $(SRC) $(HDR) Makefile build/flags.stamp
 	@printf 'extern "C" const char* pm_build_id(void) { return "%s"; }\n' $(BUILD_ID) > build/pm_build_id.cpp
 	g++ -O2 -fPIC -c build/pm_build_id.cpp -o $@
 
+# (linked to a temporary name and renamed: a snapshot of the tree never holds half a library)
 $(LIB): $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ) -l:liblzma.so.5
+	$(HIPCC) $(HIPFLAGS) -shared -o $@.tmp $(OBJ) -l:liblzma.so.5 && mv -f $@.tmp $@
 
 # panmanUtils-compatible CLI (host C++ over the C-ABI; finds the library next to the package)
 $(CLI): panman_amd/csrc/cli/panmanUtils.cpp include/panman_gpu.h $(LIB)

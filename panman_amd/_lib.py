@@ -117,13 +117,17 @@ def build_id() -> str:
 
 
 def phase_reset() -> None:
-    """Empty the library's phase log (pm_phase_reset)."""
-    load().pm_phase_reset()
+    """Empty the library's phase log (pm_phase_reset; a no-op on an older experiment build)."""
+    lib = load()
+    if hasattr(lib, "pm_phase_reset"):
+        lib.pm_phase_reset()
 
 
 def phase_report() -> list[tuple[str, float]]:
     """(phase, seconds) the library's drivers logged since the last phase_reset."""
     lib = load()
+    if not hasattr(lib, "pm_phase_report"):
+        return []
     need = lib.pm_phase_report(None, 0)
     buf = C.create_string_buffer(int(need))
     lib.pm_phase_report(buf, need)

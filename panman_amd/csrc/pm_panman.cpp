@@ -60,6 +60,29 @@ struct pm_lzma_stream {
 };
 int lzma_stream_decoder(pm_lzma_stream* strm, uint64_t memlimit, uint32_t flags);
 int lzma_easy_encoder(pm_lzma_stream* strm, uint32_t preset, int check);
+// lzma_mt (liblzma >= 5.2): the multi-threaded .xz encoder's options
+struct pm_lzma_mt {
+    uint32_t flags;
+    uint32_t threads;
+    uint64_t block_size;
+    uint32_t timeout;
+    uint32_t preset;
+    const void* filters;
+    int check;
+    int reserved_enum1, reserved_enum2, reserved_enum3;
+    uint32_t reserved_int1, reserved_int2, reserved_int3, reserved_int4;
+    uint64_t reserved_int5, reserved_int6, reserved_int7, reserved_int8;
+    void *reserved_ptr1, *reserved_ptr2, *reserved_ptr3, *reserved_ptr4;
+};
+int lzma_stream_encoder_mt(pm_lzma_stream* strm, const pm_lzma_mt* options);
+// lzma_filter, and the preset expansion into an lzma_options_lzma (whose first member is
+// dict_size; the rest is filled by liblzma and passed back opaque)
+struct pm_lzma_filter {
+    uint64_t id;
+    void* options;
+};
+unsigned char lzma_lzma_preset(void* options, uint32_t preset);
+int lzma_stream_encoder(pm_lzma_stream* strm, const pm_lzma_filter* filters, int check);
 int lzma_code(pm_lzma_stream* strm, int action);
 void lzma_end(pm_lzma_stream* strm);
 }
@@ -92,9 +115,41 @@ bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::s
     return true;
 }
 
+// xz level 9 as writePanMAN (src/panmanUtils.cpp:282-285): the preset's LZMA2 settings
+// (match finder, nice length, lc / lp / pb) with the dictionary cut to the data it can
+// reach -- a dictionary larger than the input (or than one block) finds nothing more, but
+// the level-9 encoder initialises all 64 MiB of it, which dominated writing a small PanMAN.
+// Messages above 256 KiB go through liblzma's multi-threaded encoder in independent blocks
+// (at least 256 KiB, at most one per host thread): still one standard .xz stream that any xz
+// decoder (the reference's boost lzma filter included) reads back to the same bytes.  PM_XZ_THREADS=1 forces one
+// block; PM_XZ_BLOCK sets the block size.
 bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string& err) {
     pm_lzma_stream s{};
-    if (lzma_easy_encoder(&s, 9, kLzmaCheckCrc64) != kLzmaOk) { err = "xz encoder init"; return false; }
+    int threads = host_threads();
+    if (const char* e = std::getenv("PM_XZ_THREADS")) threads = std::max(1, std::atoi(e));
+    uint64_t block = std::max<uint64_t>((uint64_t)256 << 10, (n + threads - 1) / std::max(threads, 1));
+    if (const char* e = std::getenv("PM_XZ_BLOCK")) block = std::max<uint64_t>(4096, std::strtoull(e, nullptr, 10));
+    threads = (int)std::min<uint64_t>((uint64_t)threads, (n + block - 1) / block);
+    const uint64_t reach = threads > 1 ? block : std::max<uint64_t>(n, 1);
+    uint32_t dict = 4096;
+    while (dict < reach && dict < ((uint32_t)64 << 20)) dict <<= 1;
+    alignas(16) unsigned char opt[512] = {0};   // lzma_options_lzma (opaque past dict_size)
+    if (lzma_lzma_preset(opt, 9)) { err = "xz preset"; return false; }
+    uint32_t* dict_size = reinterpret_cast<uint32_t*>(opt);
+    *dict_size = std::min(*dict_size, dict);
+    const pm_lzma_filter filters[2] = {{0x21 /* LZMA2 */, opt}, {UINT64_MAX, nullptr}};
+    if (threads > 1) {
+        pm_lzma_mt mt{};
+        mt.threads = (uint32_t)threads;
+        mt.block_size = block;
+        mt.preset = 9;
+        mt.filters = filters;
+        mt.check = kLzmaCheckCrc64;
+        if (lzma_stream_encoder_mt(&s, &mt) != kLzmaOk) { err = "xz encoder init"; return false; }
+    } else if (lzma_stream_encoder(&s, filters, kLzmaCheckCrc64) != kLzmaOk) {
+        err = "xz encoder init";
+        return false;
+    }
     out.resize(n / 2 + (1 << 16));
     s.next_in = in;
     s.avail_in = n;

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -46,11 +47,35 @@ hipError_t dput(T** dst, const std::vector<T>& v, hipStream_t s) {
 
 }  // namespace
 
-int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin, int64_t leaf_end) {
+
+namespace {
+
+struct FlatErr {
+    int code = PM_OK;
+    std::string msg;
+    int set(int c, const char* m) {
+        code = c;
+        msg = m;
+        return c;
+    }
+};
+
+}  // namespace
+
+// The host half of replay_prepare: canonical columns, per-node edits, per-leaf block state.
+// Per-node edit lists are independent and built by host threads (a C5 PanMAT carries ~18 M
+// edits); everything else is linear in blocks, nodes or leaves.
+int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t leaf_begin, int64_t leaf_end,
+                   std::string& err_msg) {
+    FlatErr ferr;
     PhaseClock clock;
+    auto fail_ = [&](int code, const char* msg) {
+        err_msg = msg;
+        return code;
+    };
     const int32_t N = p->num_nodes;
     if (N < 1 || p->root < 0 || p->root >= N || !p->child_offsets || !p->names)
-        return fail(c, PM_ERR_ARG, "bad PanMAT topology");
+        return fail_(PM_ERR_ARG, "bad PanMAT topology");
     r.num_nodes = N;
     r.names.resize(N);
     const char* nm = p->names;
@@ -63,39 +88,40 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     for (int32_t i = 0; i < N; ++i)
         for (int32_t e = p->child_offsets[i]; e < p->child_offsets[i + 1]; ++e) {
             const int32_t ch = p->child_index[e];
-            if (ch < 0 || ch >= N || r.parent[ch] != -2) return fail(c, PM_ERR_ARG, "bad child index");
+            if (ch < 0 || ch >= N || r.parent[ch] != -2) return fail_(PM_ERR_ARG, "bad child index");
             r.parent[ch] = i;
         }
     for (int32_t i = 0; i < N; ++i) {
-        if (r.parent[i] == -2) return fail(c, PM_ERR_ARG, "node unreachable from the root");
+        if (r.parent[i] == -2) return fail_(PM_ERR_ARG, "node unreachable from the root");
         if (p->child_offsets[i] == p->child_offsets[i + 1]) r.leaves.push_back(i);
     }
     if (leaf_begin >= 0 || leaf_end >= 0) {   // a shard of the leaves
         if (leaf_begin < 0 || leaf_end < leaf_begin || leaf_end > (int64_t)r.leaves.size())
-            return fail(c, PM_ERR_ARG, "leaf range outside [0, leaves]");
+            return fail_(PM_ERR_ARG, "leaf range outside [0, leaves]");
         r.leaves = std::vector<int32_t>(r.leaves.begin() + leaf_begin, r.leaves.begin() + leaf_end);
     }
 
     // ---- blocks (vector order defines blockLengths resets; ids must be unique)
     const int32_t B = p->num_blocks;
     for (int32_t b = 0; b < B; ++b) r.max_id = std::max(r.max_id, p->block_primary[b]);
-    if (B == 0) return fail(c, PM_ERR_ARG, "PanMAT has no blocks");
+    if (B == 0) return fail_(PM_ERR_ARG, "PanMAT has no blocks");
     const int32_t M = r.max_id + 1;
     r.is_block.assign(M, 0);
     std::vector<int32_t> len(M, 0);
-    std::vector<std::vector<uint8_t>> codes(M);
+    std::vector<int32_t> blk_of(M, -1);
     for (int32_t b = 0; b < B; ++b) {
         const int32_t id = p->block_primary[b];
-        if (id < 0 || r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "duplicate or negative primary block id");
+        if (id < 0 || r.is_block[id]) return fail_(PM_ERR_UNSUPPORTED, "duplicate or negative primary block id");
         r.is_block[id] = 1;
+        blk_of[id] = b;
+        int32_t n = 0;
         bool end = false;
         for (int64_t w = p->block_seq_offsets[b]; w < p->block_seq_offsets[b + 1] && !end; ++w)
             for (int k = 0; k < 8; ++k) {
-                const int code = (p->block_seq[w] >> (4 * (7 - k))) & 15;
-                if (code == 0) { end = true; break; }
-                codes[id].push_back((uint8_t)code);
+                if (((p->block_seq[w] >> (4 * (7 - k))) & 15) == 0) { end = true; break; }
+                ++n;
             }
-        len[id] = (int32_t)codes[id].size();
+        len[id] = n;
     }
     // gap slots: resize semantics (last entry wins) for present blocks; absent blocks
     // accumulate every listed length (src/fasta.cpp:2067-2088)
@@ -105,10 +131,10 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         if (r.is_block[id]) slots[id].assign(len[id] + 1, 0);
     for (int32_t g = 0; g < p->num_gaps; ++g) {
         const int32_t id = p->gap_primary[g];
-        if (id < 0 || id >= M || !r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "gap list for a missing block");
+        if (id < 0 || id >= M || !r.is_block[id]) return fail_(PM_ERR_UNSUPPORTED, "gap list for a missing block");
         for (int64_t k = p->gap_offsets[g]; k < p->gap_offsets[g + 1]; ++k) {
             const uint32_t pos = p->gap_position[k];
-            if (pos > (uint32_t)len[id]) return fail(c, PM_ERR_ARG, "gap position beyond the block");
+            if (pos > (uint32_t)len[id]) return fail_(PM_ERR_ARG, "gap position beyond the block");
             slots[id][pos] = (int32_t)p->gap_length[k];
             gap_sum[id] += p->gap_length[k];
         }
@@ -117,152 +143,255 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     r.width.assign(M, 0);
     r.absent_len.assign(M, 0);
     std::vector<std::vector<int64_t>> main_col(M), gap_col(M);   // column of main j / first slot of j
-    std::string cons;
+    int64_t cols = 0;
     for (int32_t id = 0; id < M; ++id) {
-        r.col_start[id] = (int64_t)cons.size();
+        r.col_start[id] = cols;
         if (!r.is_block[id]) continue;
-        main_col[id].resize(len[id] + 1);
-        gap_col[id].resize(len[id] + 1);
-        for (int32_t j = 0; j <= len[id]; ++j) {
-            gap_col[id][j] = (int64_t)cons.size();
-            cons.append((size_t)slots[id][j], '-');
-            main_col[id][j] = (int64_t)cons.size();
-            cons += j < len[id] ? nuc_char(codes[id][j]) : 'x';
-        }
-        r.width[id] = (int64_t)cons.size() - r.col_start[id];
+        for (int32_t j = 0; j <= len[id]; ++j) cols += slots[id][j] + 1;
+        r.width[id] = cols - r.col_start[id];
         r.absent_len[id] = len[id] + gap_sum[id];
     }
-    r.columns = (int64_t)cons.size();
-    r.cons = cons;
-    r.main_col = main_col;
-    r.gap_col = gap_col;
-    r.slots = slots;
-    if (r.columns >= ((int64_t)1 << 32)) return fail(c, PM_ERR_UNSUPPORTED, "more than 2^32 aligned columns");
+    r.columns = cols;
+    if (r.columns >= ((int64_t)1 << 32)) return fail_(PM_ERR_UNSUPPORTED, "more than 2^32 aligned columns");
+    std::string cons((size_t)cols, '-');
+    host_parallel_for(M, [&](int id) {   // blocks fill disjoint column ranges
+        if (!r.is_block[id]) return;
+        main_col[id].resize(len[id] + 1);
+        gap_col[id].resize(len[id] + 1);
+        const int32_t b = blk_of[id];
+        int64_t at = r.col_start[id];
+        int32_t j = 0;
+        for (int64_t w = p->block_seq_offsets[b]; w < p->block_seq_offsets[b + 1] && j < len[id]; ++w)
+            for (int k = 0; k < 8 && j < len[id]; ++k, ++j) {
+                gap_col[id][j] = at;
+                at += slots[id][j];
+                main_col[id][j] = at;
+                cons[(size_t)at++] = nuc_char((int)((p->block_seq[w] >> (4 * (7 - k))) & 15));
+            }
+        gap_col[id][len[id]] = at;
+        at += slots[id][len[id]];
+        main_col[id][len[id]] = at;
+        cons[(size_t)at] = 'x';
+    });
 
-    // ---- per-node edits (column, char, block), last write per column within a node wins
-    std::vector<int64_t> eoff(N + 1, 0);
-    std::vector<uint32_t> ecol;
-    std::vector<uint8_t> echr;
-    std::vector<int32_t> eblk;
-    std::vector<std::pair<uint32_t, size_t>> tmp;
-    for (int32_t v = 0; v < N; ++v) {
-        const size_t first = ecol.size();
-        for (int64_t k = p->nuc_mut_offsets[v]; k < p->nuc_mut_offsets[v + 1]; ++k) {
-            const int32_t id = p->nuc_mut_primary[k];
-            // secondary blocks (blockGaps, src/fasta.cpp:1230-1233) are never written by
-            // TreeGroup::writeToFile; refused rather than applied to the primary block
-            if (p->nuc_mut_secondary && p->nuc_mut_secondary[k] != -1)
-                return fail(c, PM_ERR_UNSUPPORTED, "mutation on a secondary block (blockGaps)");
-            const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
-            int32_t n = (int32_t)(info >> 4);
-            if (type > 5) continue;           // no-op types
-            if (type >= 3) n = 1;             // NSNPS / NSNPI / NSNPD: one code
-            if (id < 0 || id >= M || !r.is_block[id]) return fail(c, PM_ERR_UNSUPPORTED, "mutation on a missing block");
-            if (n > 6) return fail(c, PM_ERR_UNSUPPORTED, "nucleotide run longer than 6");
-            const int32_t pos = p->nuc_mut_position[k], gap = p->nuc_mut_gap_position[k];
-            for (int32_t j = 0; j < n; ++j) {
-                const int code = (p->nuc_mut_nucs[k] >> (4 * (5 - j))) & 15;
-                const bool del = type == 1 || type == 5;
-                int64_t col;
-                if (gap != -1) {
-                    if (pos < 0 || pos > len[id] || gap + j >= slots[id][pos] || gap < 0)
-                        return fail(c, PM_ERR_ARG, "gap-slot mutation outside the slot range");
-                    col = gap_col[id][pos] + gap + j;
-                } else {
-                    if (pos < 0 || pos + j > len[id]) return fail(c, PM_ERR_ARG, "mutation beyond the block");
-                    col = main_col[id][pos + j];   // pos + j == len rewrites the sentinel, as the reference does
+    clock.lap("replay.flat_blocks");
+    // ---- per-node edits (column, char), last write per column within a node wins.  Each
+    // node's list is written into its own slice of one array (sized from the mutations'
+    // lengths), sorted by column and deduplicated in place by host threads, then the slices
+    // are compacted in node order.
+    std::vector<int64_t> cap_off(N + 1, 0);
+    host_parallel_for((N + 15) / 16, [&](int task) {
+        for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
+            int64_t n = 0;
+            for (int64_t k = p->nuc_mut_offsets[v]; k < p->nuc_mut_offsets[v + 1]; ++k) {
+                const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
+                n += type > 5 ? 0 : type >= 3 ? 1 : std::min<int64_t>(info >> 4, 7);
+            }
+            cap_off[v + 1] = n;
+        }
+    });
+    for (int32_t v = 0; v < N; ++v) cap_off[v + 1] += cap_off[v];
+    // (column << 32) | (list index << 8) | char; uninitialised: the threads fault its pages in
+    std::unique_ptr<uint64_t[]> all(new uint64_t[(size_t)std::max<int64_t>(cap_off[N], 1)]);
+    std::vector<int64_t> kept(N, 0);
+    std::vector<int> node_err(N, PM_OK);
+    std::vector<const char*> node_msg(N, nullptr);
+    host_parallel_for((N + 15) / 16, [&](int task) {
+        for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
+            uint64_t* out = all.get() + cap_off[v];
+            int64_t cnt = 0;
+            auto bad = [&](int code, const char* msg) {
+                node_err[v] = code;
+                node_msg[v] = msg;
+            };
+            const int64_t k_end = p->nuc_mut_offsets[v + 1];
+            for (int64_t k = p->nuc_mut_offsets[v]; k < k_end && node_err[v] == PM_OK; ++k) {
+                if (k + 16 < k_end) {   // the column lookups are random accesses: prefetch ahead
+                    const int32_t pid = p->nuc_mut_primary[k + 16], ppos = p->nuc_mut_position[k + 16];
+                    if (pid >= 0 && pid < M && r.is_block[pid] && ppos >= 0 && ppos <= len[pid])
+                        __builtin_prefetch(p->nuc_mut_gap_position[k + 16] != -1 ? &gap_col[pid][ppos] : &main_col[pid][ppos]);
                 }
-                ecol.push_back((uint32_t)col);
-                echr.push_back((uint8_t)(del ? '-' : nuc_char(code)));
-                eblk.push_back(id);
+                const int32_t id = p->nuc_mut_primary[k];
+                // secondary blocks (blockGaps, src/fasta.cpp:1230-1233) are never written by
+                // TreeGroup::writeToFile; refused rather than applied to the primary block
+                if (p->nuc_mut_secondary && p->nuc_mut_secondary[k] != -1) {
+                    bad(PM_ERR_UNSUPPORTED, "mutation on a secondary block (blockGaps)");
+                    break;
+                }
+                const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
+                int32_t n = (int32_t)(info >> 4);
+                if (type > 5) continue;           // no-op types
+                if (type >= 3) n = 1;             // NSNPS / NSNPI / NSNPD: one code
+                if (id < 0 || id >= M || !r.is_block[id]) { bad(PM_ERR_UNSUPPORTED, "mutation on a missing block"); break; }
+                if (n > 6) { bad(PM_ERR_UNSUPPORTED, "nucleotide run longer than 6"); break; }
+                const int32_t pos = p->nuc_mut_position[k], gap = p->nuc_mut_gap_position[k];
+                const bool del = type == 1 || type == 5;
+                for (int32_t j = 0; j < n; ++j) {
+                    const int code = (p->nuc_mut_nucs[k] >> (4 * (5 - j))) & 15;
+                    int64_t col;
+                    if (gap != -1) {
+                        if (pos < 0 || pos > len[id] || gap + j >= slots[id][pos] || gap < 0) {
+                            bad(PM_ERR_ARG, "gap-slot mutation outside the slot range");
+                            break;
+                        }
+                        col = gap_col[id][pos] + gap + j;
+                    } else {
+                        if (pos < 0 || pos + j > len[id]) { bad(PM_ERR_ARG, "mutation beyond the block"); break; }
+                        col = main_col[id][pos + j];   // pos + j == len rewrites the sentinel, as the reference does
+                    }
+                    const uint64_t chr = (uint8_t)(del ? '-' : nuc_char(code));
+                    out[cnt] = ((uint64_t)col << 32) | ((uint64_t)cnt << 8) | chr;
+                    ++cnt;
+                }
+            }
+            if (node_err[v] != PM_OK) continue;
+            if (cnt >= ((int64_t)1 << 24)) {
+                bad(PM_ERR_UNSUPPORTED, "more than 2^24 column edits on one node");
+                continue;
+            }
+            // (column, list index) order; keep the last edit of each column
+            if (!std::is_sorted(out, out + cnt)) std::sort(out, out + cnt);
+            int64_t w = 0;
+            for (int64_t i = 0; i < cnt; ++i)
+                if (i + 1 == cnt || (out[i + 1] >> 32) != (out[i] >> 32)) out[w++] = out[i];
+            kept[v] = w;
+        }
+    });
+    for (int32_t v = 0; v < N; ++v)
+        if (node_err[v] != PM_OK) return fail_(node_err[v], node_msg[v]);
+    std::vector<int64_t>& eoff = h.eoff;
+    eoff.assign(N + 1, 0);
+    for (int32_t v = 0; v < N; ++v) eoff[v + 1] = eoff[v] + kept[v];
+    r.edits = eoff[N];
+    std::vector<uint32_t>& ecol = h.ecol;
+    std::vector<uint8_t>& echr = h.echr;
+    ecol.resize((size_t)r.edits);
+    echr.resize((size_t)r.edits);
+    host_parallel_for((N + 15) / 16, [&](int task) {
+        for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
+            const uint64_t* in = all.get() + cap_off[v];
+            for (int64_t i = 0, e = eoff[v]; i < kept[v]; ++i, ++e) {
+                ecol[e] = (uint32_t)(in[i] >> 32);
+                echr[e] = (uint8_t)(in[i] & 0xff);
             }
         }
-        // dedup within the node: keep the last edit per column
-        tmp.clear();
-        for (size_t e = first; e < ecol.size(); ++e) tmp.emplace_back(ecol[e], e);
-        std::stable_sort(tmp.begin(), tmp.end(), [](auto& a, auto& b) { return a.first < b.first; });
-        std::vector<uint32_t> c2;
-        std::vector<uint8_t> h2;
-        std::vector<int32_t> b2;
-        for (size_t i = 0; i < tmp.size(); ++i) {
-            if (i + 1 < tmp.size() && tmp[i + 1].first == tmp[i].first) continue;
-            c2.push_back(ecol[tmp[i].second]);
-            h2.push_back(echr[tmp[i].second]);
-            b2.push_back(eblk[tmp[i].second]);
+    });
+    all.reset();
+
+    clock.lap("replay.flat_edits");
+
+    // ---- column tiles: per node, the first (column-sorted) edit of every tile
+    const int64_t stride = (r.columns + 15) / 16 * 16;
+    const int32_t tiles = (int32_t)((stride + kReplayTile - 1) / kReplayTile);
+    std::vector<int64_t>& tile_edit = h.tile_edit;
+    tile_edit.resize((size_t)N * (tiles + 1));
+    host_parallel_for((N + 15) / 16, [&](int task) {
+        for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
+            int64_t e = eoff[v];
+            for (int32_t t = 0; t <= tiles; ++t) {
+                const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
+                while (e < eoff[v + 1] && (int64_t)ecol[e] < c0) ++e;
+                tile_edit[(size_t)v * (tiles + 1) + t] = e;
+            }
         }
-        ecol.resize(first);
-        echr.resize(first);
-        eblk.resize(first);
-        ecol.insert(ecol.end(), c2.begin(), c2.end());
-        echr.insert(echr.end(), h2.begin(), h2.end());
-        eblk.insert(eblk.end(), b2.begin(), b2.end());
-        eoff[v + 1] = (int64_t)ecol.size();
-    }
-    r.edits = (int64_t)ecol.size();
+    });
 
     // ---- edits that overwrite an ancestor's edit of the same column get kEditOverrides in
     // their character byte: the replay kernel writes the others in any order and only these
-    // in path order (k_replay_tile).  Depth-first walk with a count of the ancestors'
-    // edits per column.
+    // in path order (k_replay_tile).  A depth-first walk with a count of the ancestors' edits
+    // per column; the columns are split into ranges of tiles walked by host threads (each
+    // node's edits of a range are one slice of its column-sorted list, tile_edit).
     {
-        std::vector<int32_t> active(r.columns + 1, 0);
+        std::vector<std::pair<int32_t, bool>> walk;   // (node, leaving) in depth-first order
+        walk.reserve(2 * (size_t)N);
         std::vector<std::pair<int32_t, bool>> stack{{p->root, false}};
         while (!stack.empty()) {
-            const auto [v, leaving] = stack.back();
+            const auto ev = stack.back();
             stack.pop_back();
-            if (leaving) {
-                for (int64_t e = eoff[v]; e < eoff[v + 1]; ++e) --active[ecol[e]];
-                continue;
-            }
-            for (int64_t e = eoff[v]; e < eoff[v + 1]; ++e)
-                if (active[ecol[e]]++ > 0) echr[e] |= kEditOverrides;
-            stack.push_back({v, true});
-            for (int32_t e = p->child_offsets[v]; e < p->child_offsets[v + 1]; ++e)
+            walk.push_back(ev);
+            if (ev.second) continue;
+            stack.push_back({ev.first, true});
+            for (int32_t e = p->child_offsets[ev.first]; e < p->child_offsets[ev.first + 1]; ++e)
                 stack.push_back({p->child_index[e], false});
         }
+        const int T = std::max(1, std::min(host_threads() * 2, tiles));
+        host_parallel_for(T, [&](int task) {
+            const int32_t t0 = (int32_t)((int64_t)tiles * task / T), t1 = (int32_t)((int64_t)tiles * (task + 1) / T);
+            if (t1 <= t0) return;
+            const int64_t c0 = (int64_t)t0 * kReplayTile;
+            std::vector<int32_t> active((size_t)(t1 - t0) * kReplayTile, 0);
+            for (const auto& [v, leaving] : walk) {
+                const int64_t e0 = tile_edit[(size_t)v * (tiles + 1) + t0], e1 = tile_edit[(size_t)v * (tiles + 1) + t1];
+                if (leaving) {
+                    for (int64_t e = e0; e < e1; ++e) --active[ecol[e] - c0];
+                    continue;
+                }
+                for (int64_t e = e0; e < e1; ++e)
+                    if (active[ecol[e] - c0]++ > 0) echr[e] |= kEditOverrides;
+            }
+        });
     }
-
+    clock.lap("replay.flat_overrides");
     // ---- per-leaf block state (getBlockSequence + the block-mutation pass of the helper)
     const int32_t L = (int32_t)r.leaves.size();
     const int32_t words = (M + 31) / 32;
-    std::vector<uint32_t> presence((size_t)L * words, 0);
+    std::vector<uint32_t>& presence = h.presence;
+    presence.assign((size_t)L * words, 0);
     r.present.assign(L, {});
     r.exists.assign(L, {});
     r.strand.assign(L, {});
-    int32_t max_depth = 0;
-    std::vector<int64_t> path_off{0};
-    std::vector<int32_t> path_all;
-    const int64_t nb_slots = (int64_t)B + 1;   // blockSequence has blocks.size()+1 entries
+    std::vector<int64_t>& path_off = h.path_off;
+    std::vector<int32_t>& path_all = h.path_all;
+    path_off.assign(L + 1, 0);
     for (int32_t li = 0; li < L; ++li) {
-        std::vector<int32_t> path;
-        for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path.push_back(n);
-        std::reverse(path.begin(), path.end());
-        max_depth = std::max(max_depth, (int32_t)path.size());
-        path_all.insert(path_all.end(), path.begin(), path.end());   // root first
-        path_off.push_back((int64_t)path_all.size());
-        std::vector<uint8_t> pres(std::max<int64_t>(M, nb_slots), 0), ex(M, 0), st(M, 1);
-        for (int32_t n : path)
-            for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
-                const int32_t id = p->block_mut_primary[k];
-                if (id < 0 || id >= (int32_t)pres.size()) return fail(c, PM_ERR_ARG, "block mutation id out of range");
-                if (p->block_mut_info[k]) pres[id] = 1;
-                else if (!p->block_mut_inversion[k]) pres[id] = 0;
-            }
-        for (int32_t n : path)
-            for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
-                const int32_t id = p->block_mut_primary[k];
-                if (id >= M || !pres[id]) continue;
-                if (p->block_mut_info[k]) { ex[id] = 1; st[id] = !p->block_mut_inversion[k]; }
-                else if (p->block_mut_inversion[k]) st[id] = !st[id];
-                else { ex[id] = 0; st[id] = 1; }
-            }
-        pres.resize(M);
-        for (int32_t id = 0; id < M; ++id)
-            if (pres[id]) presence[(size_t)li * words + id / 32] |= 1u << (id % 32);
-        r.present[li] = std::move(pres);
-        r.exists[li] = std::move(ex);
-        r.strand[li] = std::move(st);
+        int32_t depth = 0;
+        for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) ++depth;
+        path_off[li + 1] = path_off[li] + depth;
+        h.max_depth = std::max(h.max_depth, depth);
     }
+    path_all.resize((size_t)path_off[L]);
+    const int64_t nb_slots = (int64_t)B + 1;   // blockSequence has blocks.size()+1 entries
+    std::vector<int> leaf_err(L, PM_OK);
+    host_parallel_for((L + 15) / 16, [&](int task) {
+        for (int32_t li = task * 16; li < std::min(L, task * 16 + 16); ++li) {
+            int32_t* path = path_all.data() + path_off[li];   // root first
+            const int32_t depth = (int32_t)(path_off[li + 1] - path_off[li]);
+            int32_t at = depth;
+            for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path[--at] = n;
+            std::vector<uint8_t> pres(std::max<int64_t>(M, nb_slots), 0), ex(M, 0), st(M, 1);
+            for (int32_t i = 0; i < depth; ++i) {
+                const int32_t n = path[i];
+                for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
+                    const int32_t id = p->block_mut_primary[k];
+                    if (id < 0 || id >= (int32_t)pres.size()) {
+                        leaf_err[li] = PM_ERR_ARG;
+                        break;
+                    }
+                    if (p->block_mut_info[k]) pres[id] = 1;
+                    else if (!p->block_mut_inversion[k]) pres[id] = 0;
+                }
+            }
+            if (leaf_err[li] != PM_OK) continue;
+            for (int32_t i = 0; i < depth; ++i) {
+                const int32_t n = path[i];
+                for (int64_t k = p->block_mut_offsets[n]; k < p->block_mut_offsets[n + 1]; ++k) {
+                    const int32_t id = p->block_mut_primary[k];
+                    if (id >= M || !pres[id]) continue;
+                    if (p->block_mut_info[k]) { ex[id] = 1; st[id] = !p->block_mut_inversion[k]; }
+                    else if (p->block_mut_inversion[k]) st[id] = !st[id];
+                    else { ex[id] = 0; st[id] = 1; }
+                }
+            }
+            pres.resize(M);
+            for (int32_t id = 0; id < M; ++id)
+                if (pres[id]) presence[(size_t)li * words + id / 32] |= 1u << (id % 32);
+            r.present[li] = std::move(pres);
+            r.exists[li] = std::move(ex);
+            r.strand[li] = std::move(st);
+        }
+    });
+    for (int32_t li = 0; li < L; ++li)
+        if (leaf_err[li] != PM_OK) return fail_(PM_ERR_ARG, "block mutation id out of range");
     r.circular.assign(L, -1);
     r.rotation.assign(L, 0);
     r.inverted.assign(L, 0);
@@ -273,56 +402,64 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         if (p->sequence_inverted) r.inverted[li] = p->sequence_inverted[v];
     }
 
-    // ---- column tiles: per node, the first (column-sorted) edit of every tile
-    const int64_t stride = (r.columns + 15) / 16 * 16;
-    const int32_t tiles = (int32_t)((stride + kReplayTile - 1) / kReplayTile);
-    std::vector<int64_t> tile_edit((size_t)N * (tiles + 1));
-    for (int32_t v = 0; v < N; ++v) {
-        int64_t e = eoff[v];
-        for (int32_t t = 0; t <= tiles; ++t) {
-            const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
-            while (e < eoff[v + 1] && (int64_t)ecol[e] < c0) ++e;
-            tile_edit[(size_t)v * (tiles + 1) + t] = e;
-        }
-    }
-    std::vector<int64_t> blk_lo(M), blk_hi(M);
+    clock.lap("replay.flat_leaves");
+    h.blk_lo.resize(M);
+    h.blk_hi.resize(M);
     for (int32_t id = 0; id < M; ++id) {
-        blk_lo[id] = r.col_start[id];
-        blk_hi[id] = r.col_start[id] + r.width[id];
+        h.blk_lo[id] = r.col_start[id];
+        h.blk_hi[id] = r.col_start[id] + r.width[id];
     }
-    std::vector<int32_t> tile_blk(tiles + 1);
+    h.tile_blk.resize(tiles + 1);
     for (int32_t t = 0, id = 0; t <= tiles; ++t) {
         const int64_t c0 = (int64_t)t * kReplayTile;
-        while (id < M && blk_hi[id] <= c0) ++id;
-        tile_blk[t] = id;
+        while (id < M && h.blk_hi[id] <= c0) ++id;
+        h.tile_blk[t] = id;
     }
+    h.cons_row.assign((size_t)stride, '-');
+    std::memcpy(h.cons_row.data(), cons.data(), cons.size());
+    h.words = words;
+    h.stride = stride;
+    h.tiles = tiles;
+    r.cons = std::move(cons);
+    r.main_col = std::move(main_col);
+    r.gap_col = std::move(gap_col);
+    r.slots = std::move(slots);
+    clock.lap("replay.flat_tiles");
+    (void)ferr;
+    return PM_OK;
+}
 
+int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin, int64_t leaf_end) {
+    PhaseClock clock;
+    ReplayHost h;
+    std::string msg;
+    const int rc = replay_flatten(p, r, h, leaf_begin, leaf_end, msg);
+    if (rc != PM_OK) return fail(c, rc, msg);
     clock.lap("replay.prepare_host");
-    // ---- device
-    std::vector<char> cons_row(stride, '-');
-    std::memcpy(cons_row.data(), cons.data(), cons.size());
+    const int32_t L = (int32_t)r.leaves.size();
+    const int32_t M = r.max_id + 1;
     hipError_t e;
     // (the rows live in the context's grow-only buffer: a 5 GB hipMalloc + hipFree per call
     // is not free, and pm_fasta prepares again on every call)
-    if ((e = grow_device(&c->rows_buf, &c->rows_cap, (size_t)std::max<int64_t>(L, 1) * stride)) != hipSuccess)
+    if ((e = grow_device(&c->rows_buf, &c->rows_cap, (size_t)std::max<int64_t>(L, 1) * h.stride)) != hipSuccess)
         return fail(c, PM_ERR_OOM, "replay rows");
     r.d_rows = static_cast<char*>(c->rows_buf);
-    if ((e = dput(&r.d_cons, cons_row, c->stream)) != hipSuccess || (e = dput(&r.d_parent, r.parent, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, presence, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_eoff, eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, ecol, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_echr, echr, c->stream)) != hipSuccess || (e = dput(&r.d_blk_lo, blk_lo, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_blk_hi, blk_hi, c->stream)) != hipSuccess || (e = dput(&r.d_tile_blk, tile_blk, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_tile_edit, tile_edit, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_path_off, path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, path_all, c->stream)) != hipSuccess ||
+    if ((e = dput(&r.d_cons, h.cons_row, c->stream)) != hipSuccess || (e = dput(&r.d_parent, r.parent, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_leaf, r.leaves, c->stream)) != hipSuccess || (e = dput(&r.d_presence, h.presence, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_eoff, h.eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, h.ecol, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_echr, h.echr, c->stream)) != hipSuccess || (e = dput(&r.d_blk_lo, h.blk_lo, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_blk_hi, h.blk_hi, c->stream)) != hipSuccess || (e = dput(&r.d_tile_blk, h.tile_blk, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_tile_edit, h.tile_edit, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_path_off, h.path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, h.path_all, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
     clock.lap("replay.upload");
     ReplayDev& d = r.dev;
     d.leaves = L;
-    d.row_stride = stride;
+    d.row_stride = h.stride;
     d.columns = r.columns;
-    d.max_depth = max_depth;
-    d.presence_words = words;
+    d.max_depth = h.max_depth;
+    d.presence_words = h.words;
     d.rows = r.d_rows;
     d.cons_row = r.d_cons;
     d.parent = r.d_parent;
@@ -335,7 +472,7 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     d.blk_lo = r.d_blk_lo;
     d.blk_hi = r.d_blk_hi;
     d.tile_blk = r.d_tile_blk;
-    d.tiles = tiles;
+    d.tiles = h.tiles;
     d.tile_edit = r.d_tile_edit;
     d.path_off = r.d_path_off;
     d.path = r.d_path;

@@ -55,5 +55,20 @@ struct ReplayState {
 // and upload it; the rows are produced by launch_replay(c, r.dev).
 // Leaves [leaf_begin, leaf_end) of the PanMAT's leaves in node-id order (-1, -1: all).
 int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_begin = -1, int64_t leaf_end = -1);
+// Host arrays of a flattened PanMAT that the replay kernels read (uploaded by replay_prepare).
+struct ReplayHost {
+    std::vector<char> cons_row;
+    std::vector<uint32_t> presence;
+    std::vector<int64_t> eoff;
+    std::vector<uint32_t> ecol;
+    std::vector<uint8_t> echr;
+    std::vector<int64_t> blk_lo, blk_hi, tile_edit, path_off;
+    std::vector<int32_t> tile_blk, path_all;
+    int32_t max_depth = 0, words = 0, tiles = 0;
+    int64_t stride = 0;
+};
+// Its host half (no device call): fills r and the arrays replay_prepare uploads.
+int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t leaf_begin, int64_t leaf_end,
+                   std::string& err_msg);
 
 }  // namespace pm
