@@ -141,7 +141,11 @@ __global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 #ifdef PM_UP_LDS_PAD   // occupancy experiments only: caps the resident workgroups per CU
     __shared__ uint32_t occ_pad[PM_UP_LDS_PAD / 4];
-    if (a.count < 0) occ_pad[threadIdx.x] = 0;
+    if (a.count < 0) {   // never taken; a read keeps the array (and its LDS allocation)
+        occ_pad[threadIdx.x] = threadIdx.x;
+        __syncthreads();
+        a.cmask[threadIdx.x] = occ_pad[(threadIdx.x * 7) % (PM_UP_LDS_PAD / 4)];
+    }
 #endif
     int32_t item;
     int tile;
