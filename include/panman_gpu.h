@@ -221,6 +221,10 @@ int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_s
  * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
  * words, finals written, tail items.  `n` >= 5.  Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
+/* FETCH_SIZE calibration for scattered reads: `lanes` threads each read 4 x 16 B, one 16-B
+ * slot every `stride_bytes` (16 = a coalesced stream), and write 16 B coalesced; `reps`
+ * launches, *ms_per_launch their average (profile it with rocprofv3 --pmc FETCH_SIZE). */
+int pm_gather_probe(int device, int64_t lanes, int stride_bytes, int reps, double* ms_per_launch);
 /* Device bytes the context holds now (n entries of): out[0] total, [1] leaf rows (code planes,
  * presence, flags), [2] the S2 / S3 side-by-side leaf copy, [3] state-set records, [4] record
  * masks, [5] Sankoff part counters, [6] mutation-record shards, [7] the flattened tree

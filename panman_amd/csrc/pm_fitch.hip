@@ -236,6 +236,14 @@ __device__ __forceinline__ void wide_fold(const UpArgs& a, int32_t e0, int32_t e
         const int4 vl = my < e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask]
                                                                    : make_int4(-1, -1, -1, -1);
         const int cnt = min(kWave, (e1 - base + NW - 1) / NW);
+        // AP: every record child's (x, s) masks, one child per lane, loaded once for the whole
+        // batch -- a pair's record loads then wait on nothing but themselves
+        uint64_t cmx = 0, cms = 0;
+        if (AP && my < e1 && materialised(enc)) {
+            const uint64_t* q = a.cmask + kMaskWords * ((size_t)enc * a.tiles + tile);
+            cmx = q[0];
+            cms = q[1];
+        }
         for (int k = 0; k < cnt; k += 2) {
             const int32_t c0 = __builtin_amdgcn_readlane(enc, k);
             const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
@@ -245,8 +253,8 @@ __device__ __forceinline__ void wide_fold(const UpArgs& a, int32_t e0, int32_t e
                                 : make_int4(-1, -1, -1, -1);
             if constexpr (AP) {   // both children's loads in flight together (see k_fitch_up)
                 ChildFetch f0, f1;
-                fetch_child_ap(a, c0, v0, tile, lane, word, f0);
-                if (two) fetch_child_ap(a, c1, v1, tile, lane, word, f1);
+                fetch_child_ap_m(a, c0, v0, readlane64(cmx, k), readlane64(cms, k), tile, lane, word, f0);
+                if (two) fetch_child_ap_m(a, c1, v1, readlane64(cmx, k + 1), readlane64(cms, k + 1), tile, lane, word, f1);
                 __builtin_amdgcn_sched_barrier(0);
                 fold_child_ap(c0, v0, f0, both, either, vd);
                 if (two) fold_child_ap(c1, v1, f1, both, either, vd);

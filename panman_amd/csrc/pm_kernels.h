@@ -532,6 +532,31 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
     }
 }
 
+// fetch_child_ap for a child whose record masks (x, s) the caller already holds (wide nodes:
+// every child's masks are loaded up front, one per lane, so a child's record loads wait for
+// no mask load of their own)
+template <int REC = kFitchRec>
+__device__ __forceinline__ void fetch_child_ap_m(const UpArgs& a, int32_t c, int4 vl, uint64_t mx, uint64_t ms, int tile,
+                                                 int lane, int64_t word, ChildFetch& f) {
+    if (c < 0 || (c & kVirtualBit)) {
+        fetch_child_ap<REC, false, false>(a, c, vl, tile, lane, word, f);
+        return;
+    }
+    const size_t rec = (size_t)c * a.tiles + tile;
+    const RecMask m{mx, ms, 0, 0, 0};
+    const uint4* p = a.sets + rec * REC;
+    f.cx = (m.x >> lane) & 1ull;
+    f.code = rec_code_all(p, m, lane, a.cons, word);
+    const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
+    const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
 __device__ __forceinline__ uint32_t code_ne(const uint4& p, const uint4& q) {
     return (p.x ^ q.x) | (p.y ^ q.y) | (p.z ^ q.z) | (p.w ^ q.w);
 }

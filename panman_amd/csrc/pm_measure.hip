@@ -36,6 +36,24 @@ __global__ __launch_bounds__(kBlock) void k_stream_copy(const uint4* __restrict_
     }
 }
 
+// FETCH_SIZE calibration for scattered 16-B-per-lane reads (the pre-order's parent finals and
+// dirty-lane leaf words): thread i reads 16 B at i * stride, (i + n) * stride, ... (kGather
+// reads, each lane its own 16 B of a stride-spaced slot) and writes one coalesced 16-B XOR.
+constexpr int kGather = 4;
+
+__global__ __launch_bounds__(kBlock) void k_gather_probe(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         int64_t n, int64_t stride_q) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kGather; ++u) {
+        const uint4 v = src[(i + (int64_t)u * n) * stride_q];
+        acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+    dst[i] = acc;
+}
+
 inline int popc(uint64_t x) { return __builtin_popcountll(x); }
 
 }  // namespace
@@ -71,6 +89,42 @@ int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs) {
             rc = PM_ERR_HIP;
         else
             *gbs = 2.0 * (double)n * sizeof(uint4) * reps / (ms * 1e-3) / 1e9;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    return rc;
+}
+
+int pm_gather_probe(int device, int64_t lanes, int stride_bytes, int reps, double* ms_per_launch) {
+    if (!ms_per_launch || lanes < kBlock || stride_bytes < 16 || stride_bytes % 16 || reps < 1) return PM_ERR_ARG;
+    *ms_per_launch = 0.0;
+    if (hipSetDevice(device) != hipSuccess) return PM_ERR_HIP;
+    const int64_t sq = stride_bytes / 16, n = lanes;
+    const size_t src_q = (size_t)(n * kGather) * sq;
+    uint4 *a = nullptr, *b = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = PM_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&a), src_q * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&b), n * sizeof(uint4)) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess) {
+        rc = PM_ERR_OOM;
+    } else {
+        const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+        (void)hipMemsetAsync(a, 1, src_q * sizeof(uint4), s);
+        hipLaunchKernelGGL(k_gather_probe, grid, dim3(kBlock), 0, s, a, b, n, sq);   // warm-up
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_gather_probe, grid, dim3(kBlock), 0, s, a, b, n, sq);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.f)
+            rc = PM_ERR_HIP;
+        else
+            *ms_per_launch = (double)ms / reps;
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
