@@ -6,8 +6,8 @@
 // nucleotide mutations of each node on its root->leaf path in order, only for blocks that
 // are present at the leaf (blockSequence, :1766-1787, :1842).
 //
-//   k_replay_tile   one workgroup per (leaf, 16 KiB column tile): consensus tile -> LDS,
-//                   the path nodes' edits inside the tile applied root first by one wave
+//   k_replay_piped  one workgroup per (leaf, 8 column tiles of 16 KiB): consensus tile -> LDS,
+//                   the path nodes' edits inside the tile applied root first by all waves
 //                   (edits of one node are unique per column and sorted by column on the
 //                   host, so a per-(node, tile) offset table bounds each node's slice),
 //                   absent blocks restored, one coalesced write of the tile: 1 B per
@@ -134,6 +134,50 @@ __device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_
     }
 }
 
+// edit_write in two halves for the all-wave editor below: the round's edits that overwrite
+// no ancestor's edit (returns whether the round holds any overriding one, wave-uniform) ...
+__device__ __forceinline__ bool edit_write_plain(const EditRound& r, char* buf, int64_t c0) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        const bool ok = r.node8[j] != kNoEdit;
+        const bool ovr = ok && (r.chr[j] & kEditOverrides);
+        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
+        any |= __ballot(ovr) != 0;
+    }
+    return any;
+}
+
+// ... and its overriding ones, node by node in path order (as edit_write)
+__device__ __forceinline__ void edit_write_overrides(const EditRound& r, char* buf, int64_t c0) {
+    const int lane = (int)threadIdx.x & (kWave - 1);
+    uint64_t pend[kEditsPerLane];
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        pend[j] = __ballot(r.node8[j] != kNoEdit && (r.chr[j] & kEditOverrides));
+        any |= pend[j] != 0;
+    }
+    while (any) {
+        uint32_t k = 0;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < kEditsPerLane; ++j)
+            if (!found && pend[j]) {
+                k = __builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                found = true;
+            }
+        any = false;
+#pragma unroll
+        for (int j = 0; j < kEditsPerLane; ++j) {
+            const bool mine = ((pend[j] >> lane) & 1ull) && (r.node8[j] >> 8) == k;
+            if (mine) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
+            pend[j] &= ~__ballot(mine);
+            any |= pend[j] != 0;
+        }
+    }
+}
+
 // Any path (deep ones too): the edits of tile t, chunk by chunk, each round loaded then
 // written (no prefetch).
 __device__ __forceinline__ void apply_path_edits(const ReplayDev& d, char* buf, int32_t leaf, int32_t t, int64_t c0) {
@@ -214,22 +258,17 @@ __device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf,
 
 // One workgroup = (leaf, group of kReplayGroup column tiles), tile after tile: the tile of
 // the leaf's row is assembled in LDS -- consensus copy (all waves), the path nodes' edits
-// (wave 0, apply order above), blocks absent at the leaf restored (waves 1-3) -- and
-// leaves as one coalesced write; each row byte is written to HBM once.  For a path of at
-// most 64 nodes (each lane holds one), wave 0 loads the slice bounds of the whole group at
-// the start and the NEXT tile's edits while the other waves restore, write out and copy in,
-// and waves 1-3 look up the next tile's absent blocks the same way, so only the
-// consensus copy's latency stays on each tile's critical path.
+// (wave 0, apply order above), blocks absent at the leaf restored (waves 1-3) -- and leaves
+// as one coalesced write; each row byte is written to HBM once.  This is the general form
+// (paths deeper than 64 nodes); k_replay_piped below is the one for every other tree.
 #ifndef PM_REPLAY_GROUP
 #define PM_REPLAY_GROUP 8
 #endif
 constexpr int kReplayGroup = PM_REPLAY_GROUP;   // column tiles per workgroup
 
-// PIPED: every path has at most 64 nodes (launch_replay checks max_depth).
 #ifndef PM_REPLAY_WAVES
 #define PM_REPLAY_WAVES 7
 #endif
-template <bool PIPED>
 __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev d) {
     __shared__ uint4 tile_buf[kReplayTile / 16];
     __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
@@ -239,71 +278,100 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
     const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
     const int tid = (int)threadIdx.x;
     const bool editor = tid < kWave;
+    if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
+    for (int32_t t = t_begin; t < t_end; ++t) {
+        const int64_t c0 = (int64_t)t * kReplayTile;
+        const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
+        const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
+        const int wv = tid >> 6;
+        for (int64_t b = (int64_t)wv * kWave; b < n / 16; b += 4 * kWave) {
+            const int64_t k = b + (tid & (kWave - 1));
+            if (k < n / 16)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                                 (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0, 0);
+        }
+        __syncthreads();
+        if (editor) apply_path_edits(d, buf, leaf, t, c0);
+        __syncthreads();
+        if (!editor) restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
+        __syncthreads();
+        if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
+        uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
+        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
+        __syncthreads();   // the tile buffer is refilled next
+    }
+}
+
+#ifndef PM_REPLAY_PIPED_WAVES
+#define PM_REPLAY_PIPED_WAVES 6
+#endif
+// Every path at most 64 nodes (launch_replay checks max_depth): all four waves edit.  Every
+// wave holds the path's slice bounds (lane = path node) and takes every fourth round of the
+// tile's edits (a super-round = 4 x kEditsPerLane x 64 edits; a C5 tile has ~800).  Edits
+// that overwrite no ancestor's edit touch distinct columns along the path, so the waves write
+// them in any order; the overriding ones (kEditOverrides, rare) follow wave by wave -- the
+// rounds are in path order -- with a barrier between, and only in a super-round that has
+// any.  Each wave prefetches its first round of the next tile while the tile is restored and
+// written out, so a tile's edits cost LDS writes, not a chain of memory round trips in one
+// wave (the single-editor kernel above: ~10 us per 16 KiB tile at C5).
+__global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(ReplayDev d) {
+    __shared__ uint4 tile_buf[kReplayTile / 16];
+    __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
+    char* buf = reinterpret_cast<char*>(tile_buf);
+    const int32_t leaf = blockIdx.x;
+    const int32_t t_begin = (int32_t)blockIdx.y * kReplayGroup;
+    const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
+    const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & (kWave - 1);
+    constexpr int32_t R = kEditsPerLane * kWave;   // edits per wave-round
     const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
-    constexpr bool piped = PIPED;
     const int cnt = (int)min((int64_t)kWave, p1 - p0);
-    // wave 0, piped: this lane's path node's slice bounds for the current tile and ahead
     const int64_t* te = nullptr;
     int64_t te_next = 0, te_next2 = 0;   // this lane's node: slice starts of tiles t+1, t+2
     EditChunk ch{};
     EditRound r{};
-    if (editor && piped && cnt > 0) {
-        const int32_t node = tid < cnt ? d.path[p0 + tid] : d.path[p0];
+    if (cnt > 0) {
+        const int32_t node = lane < cnt ? d.path[p0 + lane] : d.path[p0];
         te = d.tile_edit + (size_t)node * (d.tiles + 1);
         const int64_t te_cur = te[t_begin];
         te_next = te[t_begin + 1];
         if (t_begin + 2 <= d.tiles) te_next2 = te[t_begin + 2];
-        ch = edit_chunk_from(cnt, te_cur, te_next, tid);
-        if (ch.total > 0) edit_round(d, ch, 0, (int64_t)t_begin * kReplayTile, tid, r);
+        ch = edit_chunk_from(cnt, te_cur, te_next, lane);
+        if (wave * R < ch.total) edit_round(d, ch, wave * R, (int64_t)t_begin * kReplayTile, lane, r);
     }
     if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
     for (int32_t t = t_begin; t < t_end; ++t) {
         const int64_t c0 = (int64_t)t * kReplayTile;
         const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
         const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
-        {
-            // LDS-DMA copy-in (1 KiB per wave-instruction, every one in flight at once); in
-            // the group's first tile waves 0 and 1 are walking their lookup chains, so
-            // waves 2-3 copy the whole tile
-            const int wv = tid >> 6;
-            const bool first = t == t_begin;
-            if (!first || wv >= 2) {
-                const int w0 = first ? 2 : 0, nw = first ? 2 : 4;
-                for (int64_t b = (int64_t)(wv - w0) * kWave; b < n / 16; b += (int64_t)nw * kWave) {
-                    const int64_t k = b + (tid & (kWave - 1));
-                    if (k < n / 16)
-                        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
-                                                         (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0,
-                                                         0);
+        // LDS-DMA copy-in of the consensus tile (1 KiB per wave-instruction, all in flight)
+        for (int64_t b = (int64_t)wave * kWave; b < n / 16; b += 4 * kWave) {
+            const int64_t k = b + lane;
+            if (k < n / 16)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                                 (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0, 0);
+        }
+        __syncthreads();
+        for (int32_t sr = 0; sr < ch.total; sr += 4 * R) {   // (uniform: every wave holds the same chunk)
+            const int32_t base = sr + wave * R;
+            if (sr > 0 && base < ch.total) edit_round(d, ch, base, c0, lane, r);   // (super-round 0: prefetched)
+            const bool ovr = base < ch.total && edit_write_plain(r, buf, c0);
+            if (__syncthreads_or(ovr)) {
+                for (int w = 0; w < 4; ++w) {
+                    if (wave == w && base < ch.total) edit_write_overrides(r, buf, c0);
+                    __syncthreads();
                 }
             }
         }
-        __syncthreads();
-        if (editor) {
-            if (!piped) {
-                apply_path_edits(d, buf, leaf, t, c0);
-            } else if (cnt > 0) {
-                // this tile: the prefetched round, then any further rounds (long slices)
-                if (ch.total > 0) edit_write(r, buf, c0);
-                for (int32_t base = kEditsPerLane * kWave; base < ch.total; base += kEditsPerLane * kWave) {
-                    edit_round(d, ch, base, c0, tid, r);
-                    edit_write(r, buf, c0);
-                }
-            }
-        }
-        __syncthreads();
-        if (!editor) {
-            restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
-        } else if (piped && cnt > 0 && t + 1 < t_end) {
-            // the next tile's first round, in flight through the restore / write / copy
-            // slice bounds loaded a tile ago; the next ones' load goes out now
-            ch = edit_chunk_from(cnt, te_next, te_next2, tid);
+        restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid, blockDim.x);
+        if (cnt > 0 && t + 1 < t_end) {
+            // the next tile's first rounds, in flight through the restore / write / copy
+            ch = edit_chunk_from(cnt, te_next, te_next2, lane);
             te_next = te_next2;
             if (t + 3 <= d.tiles) te_next2 = te[t + 3];
-            if (ch.total > 0) edit_round(d, ch, 0, c0 + kReplayTile, tid, r);
+            if (wave * R < ch.total) edit_round(d, ch, wave * R, c0 + kReplayTile, lane, r);
         }
-        __syncthreads();
         if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
+        __syncthreads();
         uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
         for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
         __syncthreads();   // the tile buffer is refilled next
@@ -460,9 +528,9 @@ hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     timer_begin(c, 3);
     const unsigned groups = (unsigned)((d.tiles + kReplayGroup - 1) / kReplayGroup);
     if (d.max_depth <= kWave)
-        hipLaunchKernelGGL(k_replay_tile<true>, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
+        hipLaunchKernelGGL(k_replay_piped, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
     else
-        hipLaunchKernelGGL(k_replay_tile<false>, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
+        hipLaunchKernelGGL(k_replay_tile, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
     timer_end(c, 3);
     return hipGetLastError();
 }
