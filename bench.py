@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--group-levels", type=int, default=4, help="PM_OPT_GROUP_LEVELS (2 to 4)")
     p.add_argument("--no-up-group", action="store_true",
                    help="Fitch: post-order launches by height (PM_OPT_UP_GROUP off)")
+    p.add_argument("--sub-down", type=int, default=-1,
+                   help="Fitch: PM_OPT_SUB_DOWN, S2 / S3 records from the parent's pre-order wave (1) or "
+                        "the tail (0); -1: library default")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -127,6 +130,8 @@ def main():
         eng.set_narrow(args.narrow)
     if args.no_up_group:
         eng.set_up_group(False)
+    if args.sub_down >= 0:
+        eng.set_sub_down(bool(args.sub_down))
     if args.group >= 0 or args.group_levels != 4:
         eng.set_group(args.group if args.group >= 0 else 32768, args.group_levels)
 

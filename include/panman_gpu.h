@@ -103,6 +103,9 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_UP_GROUP (default 1): Fitch, subtree form -- a node of out-degree <= 3 whose
  *                  latest children have out-degree <= 3 runs in their post-order launch,
  *                  recomputing them, instead of one launch per height; 0 = by height.
+ *   PM_OPT_SUB_DOWN (default 0): Fitch, subtree form -- a three- or four-leaf subtree's
+ *                  finals and records come from its parent's pre-order wave instead of a
+ *                  wave of their own after the levels.
  *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the
  *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
  *                  re-run with a larger buffer when its results are read (pm_mutation_count,
@@ -118,6 +121,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_GROUP_LEVELS 9
 #define PM_OPT_UP_GROUP 10
 #define PM_OPT_RECORD_CAP 12
+#define PM_OPT_SUB_DOWN 13
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

@@ -448,7 +448,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     // subtree form: grouped post-order launches (PM_OPT_UP_GROUP) or one launch per height
     const bool grp = sub && c->up_group;
     const NodeDesc* up_desc = grp ? dt.up_desc_g : sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
-    const NodeDesc* down_desc = sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
+    // PM_OPT_SUB_DOWN: S2 / S3 children stay in their parent's pre-order descriptor (k_down<..,
+    // SUB>) and leave the tail
+    const bool sub_down = sub && c->sub_down;
+    const NodeDesc* down_desc = sub_down ? dt.down_desc_ks : sub ? dt.down_desc_k : virt ? dt.down_desc_v : dt.down_desc;
     const std::vector<int32_t>& up_off = grp ? ht.up_level_off_g : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off;
     const std::vector<int32_t>& down_off = sub ? ht.down_level_off_k : virt ? ht.down_level_off_v : ht.down_level_off;
 
@@ -585,6 +588,12 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     dn.vinner = dt.vinner;
+    if (sub_down) {   // the S children's leaf words and node ids (their tail descriptors)
+        dn.tail = dt.tail_desc_k;
+        dn.num_s = ht.num_tail_s;
+        dn.sbase = ht.sbase;
+        dn.sub_planes = c->sub_planes;
+    }
     const int D = (int)down_off.size() - 1;
     for (int d = 0; d < D; ++d) {
         if (c->narrow_max > 0 && down_off[d + 1] - down_off[d] <= c->narrow_max) {
@@ -600,6 +609,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
                 if (block && ap) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (block) hipLaunchKernelGGL((k_down_band<Mode::kBlockFitch, false>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 // (level groups inside the band when PM_OPT_GROUP_WAVES is on)
+                else if (sub_down && c->group_waves > 0) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true, true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
+                else if (sub_down) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (ap && c->group_waves > 0) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (ap) hipLaunchKernelGGL((k_down_band<Mode::kFitch, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
                 else if (c->group_waves > 0) hipLaunchKernelGGL((k_down_band<Mode::kFitch, false, false, true>), dim3(tiles), dim3(kBandBlock), 0, c->stream, dn, tab, base, d, d1);
@@ -636,7 +647,9 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             dn.count = (int32_t)items;
             const dim3 grid = wave_grid(dn.count, tiles);
             timer_begin(c, 1);
-            if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            if (sub_down && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else if (sub_down) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+            else if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
             else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
             else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
             timer_end(c, 1);
@@ -649,6 +662,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
         // from the tail launch, so the lean kernels run every level)
         if (block && ap) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (block) hipLaunchKernelGGL((k_down<Mode::kBlockFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (sub_down && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
+        else if (sub_down) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (ap && dense) hipLaunchKernelGGL((k_down<Mode::kFitch, true, true>), grid, dim3(kBlock), 0, c->stream, dn);
         else if (ap) hipLaunchKernelGGL((k_down<Mode::kFitch, true, false>), grid, dim3(kBlock), 0, c->stream, dn);
         else hipLaunchKernelGGL((k_down<Mode::kFitch, false, false>), grid, dim3(kBlock), 0, c->stream, dn);
@@ -656,12 +671,14 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     }
     // The tail (children beyond the second, S2 / S3 subtrees) needs only its parents'
     // finals: one flat launch after the levels.
-    const int32_t tail_total = sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail;
+    // (PM_OPT_SUB_DOWN: the S2 / S3 items, the first num_tail_s, were done by the levels)
+    const int32_t tail_skip = sub_down ? ht.num_tail_s : 0;
+    const int32_t tail_total = (sub ? ht.num_tail_k : virt ? ht.num_tail_v : ht.num_tail) - tail_skip;
     if (tail_total > 0) {
         DownArgs t = dn;
-        t.tail = sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc;
+        t.tail = (sub ? dt.tail_desc_k : virt ? dt.tail_desc_v : dt.tail_desc) + tail_skip;
         t.count = tail_total;
-        t.num_s = sub ? ht.num_tail_s : 0;
+        t.num_s = sub && !sub_down ? ht.num_tail_s : 0;
         t.sbase = ht.sbase;
         t.sub_planes = c->sub_planes;
         const dim3 grid = wave_grid(t.count, tiles);

@@ -79,6 +79,7 @@ void free_tree(DevTree& t) {
     dev_free(t.up_desc_g);
     dev_free(t.up_desc_gs);
     dev_free(t.down_desc_k);
+    dev_free(t.down_desc_ks);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
     dev_free(t.lvl);
@@ -202,6 +203,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
                               (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
+                              (uint64_t)c->sub_down,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -446,6 +448,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     }
     if (option == PM_OPT_UP_GROUP) {
         c->up_group = value != 0;
+        return PM_OK;
+    }
+    if (option == PM_OPT_SUB_DOWN) {
+        c->sub_down = value != 0;
         return PM_OK;
     }
     if (option == PM_OPT_GROUP_WAVES) {
@@ -943,6 +949,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)
     std::vector<NodeDesc> down_desc_k = with_gp(make_desc(down_order_k, child_enc_k));
+    const std::vector<NodeDesc> down_desc_ks = down_desc_k;   // (PM_OPT_SUB_DOWN: S children kept)
     for (NodeDesc& x : down_desc_k) {
         const int32_t deg = x.e1 - x.e0;
         if (deg > 2) continue;   // S2 / S3 nodes have parents of out-degree <= 2
@@ -1103,6 +1110,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.up_desc_g, up_desc_g)) != hipSuccess ||
         (e = up(&dt.up_desc_gs, up_desc_gs)) != hipSuccess ||
         (e = up(&dt.down_desc_k, down_desc_k)) != hipSuccess ||
+        (e = up(&dt.down_desc_ks, down_desc_ks)) != hipSuccess ||
         (e = up(&dt.vinner, vinner)) != hipSuccess ||
         (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
         (e = up(&dt.lvl, lvl)) != hipSuccess) {

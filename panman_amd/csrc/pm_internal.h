@@ -122,6 +122,7 @@ struct DevTree {
     NodeDesc* up_desc_g = nullptr;     // grouped post-order launches of the subtree form
     NodeDesc* up_desc_gs = nullptr;    // ... Sankoff's (binary recomputed children; pad0 = first part above 255 children)
     NodeDesc* down_desc_k = nullptr;
+    NodeDesc* down_desc_ks = nullptr;  // ... with their S2 / S3 children kept (PM_OPT_SUB_DOWN)
     int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
     // level tables on the device (the narrow-band launches walk several levels): the host
@@ -207,6 +208,7 @@ struct pm_ctx {
     int64_t group_waves = 32768;      // Fitch: pre-order levels grouped into one launch up to this many waves (PM_OPT_GROUP_WAVES)
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
+    bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
 
     // column shard
     int64_t num_sites = 0;

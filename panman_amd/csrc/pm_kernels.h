@@ -1046,6 +1046,22 @@ __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 v
     }
 }
 
+// An S2 / S3 child fetched for its parent's pre-order wave (PM_OPT_SUB_DOWN): its leaves'
+// words side by side (sub_planes, one 64-B sector per dirty lane), as the tail reads them.
+__device__ __forceinline__ void kid_fetch_s(const DownArgs& a, int32_t enc, int64_t word, bool dirty, Kid& k) {
+    k.enc = enc;
+    k.L0 = k.L1 = k.L2 = k.L3 = make_uint4(0, 0, 0, 0);
+    k.m0 = k.m1 = 0;
+    const uint4* q = sub_word(a.sub_planes, (enc & kDenseMask) - a.sbase, a.wpad, word);
+    if (dirty) {
+        k.L0 = q[0];
+        k.L1 = q[1];
+        k.L2 = q[2];
+        k.m0 = k.m1 = ~0u;
+    }
+    if (dirty && kid_shape(enc) == 2) k.L3 = q[3];
+}
+
 // Fold one leaf into a virtual node's union / lowest code / "parent code present" masks.
 __device__ __forceinline__ void virt_fold(const uint4& L, uint32_t m, const uint32_t* Fn, uint32_t* low, uint32_t& have,
                                           uint32_t& hit) {
@@ -1314,7 +1330,7 @@ __device__ __forceinline__ void resolve_final(const DownArgs& a, bool is_root, i
 // SUB: subtree form (Fitch, every leaf present) -- the first two children may be S2 / S3
 // subtrees, whose inner finals and records this wave produces (subtree_prepare).
 #ifndef PM_SUB_DOWN_WAVES
-#define PM_SUB_DOWN_WAVES 4
+#define PM_SUB_DOWN_WAVES 5
 #endif
 // One pre-order wave: node `n` (its descriptor d) x tile; `salt` spreads the waves over the
 // record shards; `stage` is the wave's LDS entry area (kEntryQuads, see emit_stream).
@@ -1382,16 +1398,24 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     // complex lanes, a virtual child only there and where its own leaves disagree (mask
     // words 6, 7: store_kid_masks) -- not at the lanes another child made dirty
     uint64_t k0 = m.d, k1 = m.d;
+    // SUB (PM_OPT_SUB_DOWN): the descriptor keeps S2 / S3 children, done here instead of in
+    // the tail: an S child's lanes are the ones its parent's post-order wave pushed into its
+    // own mask record (word 5); words 6 / 7 follow the descriptor without S children
+    // (fitch_up_node's store_kid_masks), so a second child's are word 6 after an S first one
+    const bool s0 = SUB && kid_shape(d.c0) != 0, s1 = SUB && e1 - e0 > 1 && kid_shape(d.c1) != 0;
     if constexpr (M == Mode::kFitch && AP) {
         const uint64_t* q = a.cmask + kMaskWords * rec;
-        k0 = d.c0 < 0 ? m.x : q[6];
-        k1 = d.c1 < 0 ? m.x : q[7];
+        auto sub_lanes = [&](int32_t c) { return a.cmask[kMaskWords * ((size_t)(c & kDenseMask) * a.tiles + tile) + 5]; };
+        k0 = d.c0 < 0 ? m.x : s0 ? sub_lanes(d.c0) : q[6];
+        k1 = d.c1 < 0 ? m.x : s1 ? sub_lanes(d.c1) : s0 ? q[6] : q[7];
     }
     const bool dirty0 = is_root || ((k0 >> lane) & 1ull);
     const bool dirty1 = is_root || ((k1 >> lane) & 1ull);
     Kid kids[2];
-    kid_fetch<M, AP, SUB>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty0, kids[0]);
-    if (e1 - e0 > 1) kid_fetch<M, AP, SUB>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty1, kids[1]);
+    if (s0) kid_fetch_s(a, d.c0, word, dirty0, kids[0]);
+    else kid_fetch<M, AP, false>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word, dirty0, kids[0]);
+    if (s1) kid_fetch_s(a, d.c1, word, dirty1, kids[1]);
+    else if (e1 - e0 > 1) kid_fetch<M, AP, false>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word, dirty1, kids[1]);
     uint32_t z1[16];
     if constexpr (M == Mode::kSankoff) {
         load_sankoff(p, m, a.cons, lane, word, own, z1, !is_root);
@@ -1418,8 +1442,19 @@ __device__ __forceinline__ void down_node(const DownArgs& a, const NodeDesc& d, 
     Emit em{stage, shard_of(salt, tile), 0u, 0u};
     const uint32_t site0 = (uint32_t)(word * 32);
     emit_stream(a, em, lane, node_id, self_diff, site0, F[0], F[1], F[2], F[3], pc);
-    kid_emit<M>(a, em, lane, kids[0], kids[0].id0, kids[0].id1, kids[0].id2, valid, F, site0);
-    if (e1 - e0 > 1) kid_emit<M>(a, em, lane, kids[1], kids[1].id0, kids[1].id1, kids[1].id2, valid, F, site0);
+    // (an S child's node ids come with its tail descriptor: item = dense index - sbase)
+    if (s0) {
+        const TailDesc& t = a.tail[(d.c0 & kDenseMask) - a.sbase];
+        subtree_emit<M>(a, em, lane, t.id, t.ix, t.iy, kids[0], kid_shape(d.c0), valid, F, site0);
+    } else {
+        kid_emit<M>(a, em, lane, kids[0], kids[0].id0, kids[0].id1, kids[0].id2, valid, F, site0);
+    }
+    if (s1) {
+        const TailDesc& t = a.tail[(d.c1 & kDenseMask) - a.sbase];
+        subtree_emit<M>(a, em, lane, t.id, t.ix, t.iy, kids[1], kid_shape(d.c1), valid, F, site0);
+    } else if (e1 - e0 > 1) {
+        kid_emit<M>(a, em, lane, kids[1], kids[1].id0, kids[1].id1, kids[1].id2, valid, F, site0);
+    }
     emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
@@ -1435,7 +1470,7 @@ template <Mode M, bool AP, bool DENSE, bool SUB = false, bool GROUP = false>
 #ifndef PM_SK_DOWN_WAVES
 #define PM_SK_DOWN_WAVES 6
 #endif
-__global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? PM_DOWN_WAVES : (M == Mode::kSankoff && AP) ? PM_SK_DOWN_WAVES : 1) void k_down(DownArgs a) {
+__global__ __launch_bounds__(kBlock, GROUP ? (M == Mode::kSankoff ? PM_SK_GROUP_WAVES : SUB ? PM_SUB_DOWN_WAVES : 8) : SUB ? PM_SUB_DOWN_WAVES : (M == Mode::kFitch && AP) ? PM_DOWN_WAVES : (M == Mode::kSankoff && AP) ? PM_SK_DOWN_WAVES : 1) void k_down(DownArgs a) {
     __shared__ uint4 stage[kWavesPerBlock][kEntryQuads];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
