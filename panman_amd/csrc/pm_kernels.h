@@ -64,7 +64,10 @@ inline dim3 block_grid(int32_t count, int32_t tiles) {
 #endif
 constexpr int64_t kMixedMaxWaves = PM_MIXED_MAX_WAVES;
 // Narrow-level band launches (PM_OPT_NARROW): one workgroup of 16 waves per tile.
-constexpr int kBandWaves = 16;
+#ifndef PM_BAND_WAVES
+#define PM_BAND_WAVES 16
+#endif
+constexpr int kBandWaves = PM_BAND_WAVES;
 constexpr int kBandBlock = kBandWaves * kWave;
 
 struct UpArgs {
