@@ -85,6 +85,7 @@ unsigned char lzma_lzma_preset(void* options, uint32_t preset);
 int lzma_stream_encoder(pm_lzma_stream* strm, const pm_lzma_filter* filters, int check);
 int lzma_code(pm_lzma_stream* strm, int action);
 void lzma_end(pm_lzma_stream* strm);
+uint32_t lzma_crc32(const uint8_t* buf, size_t size, uint32_t crc);
 }
 
 namespace pm {
@@ -93,7 +94,122 @@ namespace {
 constexpr int kLzmaOk = 0, kLzmaStreamEnd = 1, kLzmaFinish = 3, kLzmaCheckCrc64 = 4;
 constexpr uint32_t kLzmaConcatenated = 0x08;
 
+bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err);
+
+// ---- multi-block .xz in parallel --------------------------------------------------------
+// The writer (xz_encode) emits one stream of independent blocks; its index (at the end of the
+// stream) gives every block's compressed and uncompressed size, so each block can be decoded
+// on its own host thread: re-wrapped as a one-block stream (the original stream header, the
+// block, a one-record index and a footer, CRCs by liblzma) and decoded into its slice of the
+// output.  Anything else -- one block (what the reference writes), several streams, stream
+// padding, a malformed index -- takes the single-threaded decoder.
+struct XzBlock {
+    size_t offset;       // in the input
+    uint64_t unpadded;   // block header + data + check (index "unpadded size")
+    uint64_t size;       // uncompressed
+    size_t out;          // offset of its output
+};
+
+bool vli_read(const uint8_t*& p, const uint8_t* end, uint64_t& v) {
+    v = 0;
+    for (int i = 0; i < 9 && p < end; ++i) {
+        const uint8_t b = *p++;
+        v |= (uint64_t)(b & 0x7f) << (7 * i);
+        if (!(b & 0x80)) return i == 0 || b != 0;
+    }
+    return false;
+}
+
+void vli_write(std::vector<uint8_t>& o, uint64_t v) {
+    while (v >= 0x80) {
+        o.push_back((uint8_t)(v | 0x80));
+        v >>= 7;
+    }
+    o.push_back((uint8_t)v);
+}
+
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+void wr32(std::vector<uint8_t>& o, uint32_t v) {
+    for (int i = 0; i < 4; ++i) o.push_back((uint8_t)(v >> (8 * i)));
+}
+
+bool xz_blocks(const std::vector<uint8_t>& in, std::vector<XzBlock>& blocks) {
+    const size_t n = in.size();
+    if (n < 32 || in[n - 2] != 'Y' || in[n - 1] != 'Z') return false;
+    const uint8_t* foot = in.data() + n - 12;
+    if (lzma_crc32(foot + 4, 6, 0) != rd32(foot)) return false;
+    if (foot[8] != in[6] || foot[9] != in[7]) return false;   // stream flags as in the header
+    const uint64_t index_size = ((uint64_t)rd32(foot + 4) + 1) * 4;
+    if (index_size + 24 > n) return false;
+    const uint8_t* idx = foot - index_size;
+    if (idx[0] != 0 || lzma_crc32(idx, index_size - 4, 0) != rd32(foot - 4)) return false;
+    const uint8_t* p = idx + 1;
+    uint64_t count = 0;
+    if (!vli_read(p, foot - 4, count) || count < 2 || count > (1u << 20)) return false;
+    size_t off = 12, out = 0;
+    for (uint64_t k = 0; k < count; ++k) {
+        XzBlock b{};
+        if (!vli_read(p, foot - 4, b.unpadded) || !vli_read(p, foot - 4, b.size) || b.unpadded < 5) return false;
+        b.offset = off;
+        b.out = out;
+        off += (size_t)((b.unpadded + 3) & ~(uint64_t)3);
+        out += (size_t)b.size;
+        blocks.push_back(b);
+    }
+    return off == (size_t)(idx - in.data());   // one stream: the blocks end where the index starts
+}
+
 bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
+    std::vector<XzBlock> blocks;
+    if (!xz_blocks(in, blocks)) return xz_decode_serial(in, out, err);
+    out.resize(blocks.back().out + (size_t)blocks.back().size);
+    std::vector<int> ok(blocks.size(), 0);
+    host_parallel_for((int)blocks.size(), [&](int k) {
+        const XzBlock& b = blocks[(size_t)k];
+        const size_t padded = (size_t)((b.unpadded + 3) & ~(uint64_t)3);
+        std::vector<uint8_t> one(in.begin(), in.begin() + 12);   // stream header
+        one.insert(one.end(), in.begin() + (ptrdiff_t)b.offset, in.begin() + (ptrdiff_t)(b.offset + padded));
+        std::vector<uint8_t> index{0};
+        vli_write(index, 1);
+        vli_write(index, b.unpadded);
+        vli_write(index, b.size);
+        while (index.size() % 4) index.push_back(0);
+        wr32(index, lzma_crc32(index.data(), index.size(), 0));
+        one.insert(one.end(), index.begin(), index.end());
+        std::vector<uint8_t> tail;
+        wr32(tail, (uint32_t)(index.size() / 4 - 1));
+        tail.push_back(in[6]);
+        tail.push_back(in[7]);
+        std::vector<uint8_t> foot;
+        wr32(foot, lzma_crc32(tail.data(), tail.size(), 0));
+        foot.insert(foot.end(), tail.begin(), tail.end());
+        foot.push_back('Y');
+        foot.push_back('Z');
+        one.insert(one.end(), foot.begin(), foot.end());
+        pm_lzma_stream s{};
+        if (lzma_stream_decoder(&s, UINT64_MAX, 0) != kLzmaOk) return;
+        s.next_in = one.data();
+        s.avail_in = one.size();
+        uint8_t extra = 0;
+        s.next_out = b.size ? out.data() + b.out : &extra;
+        s.avail_out = (size_t)b.size;
+        int rc = lzma_code(&s, kLzmaFinish);
+        if (rc == kLzmaOk && s.avail_out == 0) {   // the end of stream needs one more call
+            s.next_out = &extra;
+            s.avail_out = 1;
+            rc = lzma_code(&s, kLzmaFinish);
+            ok[(size_t)k] = rc == kLzmaStreamEnd && s.avail_out == 1;
+        } else {
+            ok[(size_t)k] = rc == kLzmaStreamEnd && s.avail_out == 0;
+        }
+        lzma_end(&s);
+    });
+    for (int v : ok)
+        if (!v) return xz_decode_serial(in, out, err);   // (a block that does not decode alone)
+    return true;
+}
+
+bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
     pm_lzma_stream s{};
     if (lzma_stream_decoder(&s, UINT64_MAX, kLzmaConcatenated) != kLzmaOk) { err = "xz decoder init"; return false; }
     out.resize(std::max<size_t>(in.size() * 4, 1 << 20));

@@ -128,3 +128,29 @@ def test_newick_lengths_follow_reference_rules(tmp_path, newick, want):
     again = g.to_panmat(0)
     g.close()
     assert np.array_equal(again.branch_length, pm.branch_length)
+
+
+def test_multi_block_xz_round_trip(tmp_path, monkeypatch, oracle):
+    """A message above the xz block size is written as one .xz stream of independent blocks
+    (decoded block-parallel by the reader) and as one block (PM_XZ_THREADS=1, what the
+    reference writes, decoded serially): both decode with Python's lzma to the same bytes and
+    load back to PanMATs that replay identically."""
+    import lzma
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=60, blocks=40, mean_len=4000, seed=5)
+    paths = {}
+    for threads, block in (("4", "65536"), ("1", None)):
+        monkeypatch.setenv("PM_XZ_THREADS", threads)
+        if block:
+            monkeypatch.setenv("PM_XZ_BLOCK", block)
+        else:
+            monkeypatch.delenv("PM_XZ_BLOCK", raising=False)
+        paths[threads] = str(tmp_path / f"x{threads}.panman")
+        write_panman(paths[threads], [pm])
+    multi, single = (open(paths[k], "rb").read() for k in ("4", "1"))
+    assert multi != single                                   # several blocks vs one
+    assert lzma.decompress(multi) == lzma.decompress(single)
+    back = [PanmanFile(paths[k]).to_panmat(0) for k in ("4", "1")]
+    want = parse_records(oracle.fasta(pm, True))
+    for b in back:
+        assert parse_records(oracle.fasta(b, True)) == want
