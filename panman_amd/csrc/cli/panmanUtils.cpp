@@ -364,9 +364,9 @@ int from_panman(const Options& o, const std::vector<int>& devices) {
     const int trees = pm_panman_tree_count(file);
     const bool to_file = o.has("output-file");
     auto sink = [&](const char* ext, int i, const char* data, size_t n) -> bool {
-        if (!to_file) {
-            std::cout.write(data, (std::streamsize)n);
-            return true;
+        if (!to_file) {   // (stdio straight to fd 1: a 5 GB FASTA text through iostream costs seconds)
+            std::cout.flush();
+            return std::fwrite(data, 1, n, stdout) == n && std::fflush(stdout) == 0;
         }
         const std::string p = "./info/" + o.get("output-file") + "_" + std::to_string(i) + ext;
         std::ofstream f(p, std::ios::binary);
