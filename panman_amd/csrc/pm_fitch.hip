@@ -65,26 +65,10 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         cw = a.cons[word];
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
-#ifdef PM_EXP_PAIR
-        child_set_ap<SUB>(d.c0, vl0, f0, both, vd0);
-        if (e1 - e0 > 1) {
-            child_set_ap<SUB>(d.c1, vl1, f1, either, vd1);
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const uint32_t x = both[v], y = either[v];
-                both[v] = x & y;
-                either[v] = x | y;
-            }
-        } else {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) either[v] = both[v];
-        }
-#else
         child_set_ap<SUB>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
         if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd1);
-#endif
         vd = vd0 | vd1;
         split = true;
     } else {
@@ -94,9 +78,6 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         if (e1 - e0 > 1) fold_child<AP>(a, d.c1, vl1, tile, lane, word, both, either, vd);
         cw = a.cons[word];
     }
-#ifdef PM_EXP_BIN_ONLY
-    if (false)
-#endif
     for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
