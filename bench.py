@@ -797,11 +797,11 @@ def replay_block(args, world, rank, local):
                "sample": f"first {k} leaves by name, aligned FASTA, oracle printFASTAUltraFast restatement "
                          f"({secs:.1f}s on {threads} threads, leaves in parallel as the reference's "
                          f"tbb::parallel_for_each over leaves, src/fasta.cpp:1993)"}
-    # PMC-measured HBM bytes per k_replay_tile launch (tools/pmc_traffic.py, key replay:LxC)
+    # PMC-measured HBM bytes per k_replay_piped launch (tools/pmc_traffic.py, key replay:LxC)
     traffic, traffic_note = None, "no PMC traffic for this workload"
     if os.path.exists(args.traffic):
         try:
-            entry = json.load(open(args.traffic)).get("k_replay_tile", {})
+            entry = json.load(open(args.traffic)).get("k_replay_piped", {})
             key = f"replay:{leaves}x{cols}"
             if key in entry and entry.get(key + ":build") == panman_amd.build_id():
                 traffic = entry[key]
@@ -822,7 +822,7 @@ def replay_block(args, world, rank, local):
                    "leaves": total_leaves, "leaves_per_gpu": leaves, "columns": cols,
                    "path_mutation_records_rank0": path_recs,
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
-        "roofline": {"bound": "hbm", "kernel": "k_replay_tile", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": "k_replay_piped", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_note": traffic_note, "design_bytes_per_launch": alg_bytes,
                      "bytes_model": "row bytes written once + consensus row once + 5 B per path edit",
