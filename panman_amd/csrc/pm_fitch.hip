@@ -41,10 +41,15 @@ namespace {
 // leaves each, evaluated in registers: subtree_set_ap).
 // GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
 // launch, recomputed here (child_recompute) instead of loaded.
+// gi: the node's index in the descriptor array (up slots, UpArgs::upm).
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
-__device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
+__device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
+    // subtree form: the children's masks from this node's up slots, its own into its parent's
+    UpSlots sl{0, 0, 0, 0};
+    if constexpr (SUB && !LEAFY) sl = load_up_slots(a, gi, tile);
+    const int32_t ps = SUB ? a.pslot[gi] : -1;
 
     uint4 cw;   // consensus word for the store; loaded after the children's loads (see below)
     // vd0 / vd1: the first / second child's disagreeing-leaf sites (vd: every child's)
@@ -53,12 +58,13 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && !LEAFY), "grouped launches: all leaves present, non-leafy levels");
-        fold_first_two<SUB, kUpGroupDepth, kFitchRec>(a, d, tile, lane, word, both, either, vd);
+        fold_first_two<SUB, kUpGroupDepth, kFitchRec>(a, d, gi, tile, lane, word, both, either, vd);
         cw = a.cons[word];
     } else if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;
-        fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c0, vl0, tile, lane, word, f0);
-        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB>(a, d.c1, vl1, tile, lane, word, f1);
+        constexpr bool SLOT = SUB && !LEAFY;
+        fetch_child_ap<kFitchRec, LEAFY, SUB, SLOT>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
+        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB, SLOT>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
         __builtin_amdgcn_sched_barrier(0);
         // after the children's consensus loads: loaded before them, the compiler reuses it
         // for them through register copies that wait on every outstanding load
@@ -102,6 +108,7 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     // leaf is absent somewhere (an empty leaf set can make a single code by the OR)
     uint64_t mx, ms, md;
     store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
+    push_up_slot(a, ps, tile, lane, mx, ms);
     // The first / second child's own dirty lanes (mask words 6 / 7 for the pre-order
     // descriptor's first / second child; an S2 / S3 child's pushed into its record): this node's complex lanes plus the lanes where that child's
     // leaves disagree.  Elsewhere every site's set is one code c, which all the child's
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? 
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    fitch_up_node<AP, LEAFY, SUB, GROUP>(a, a.desc[item], tile, lane);
+    fitch_up_node<AP, LEAFY, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
@@ -252,8 +259,8 @@ __device__ __forceinline__ void wide_fold(const UpArgs& a, int32_t e0, int32_t e
 
 // AND if non-empty else OR, forced root, store and mask pushes of a wide node (one wave).
 template <bool AP>
-__device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
-                                            uint32_t* both, const uint32_t* either, uint32_t vd) {
+__device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane,
+                                            int64_t word, uint32_t* both, const uint32_t* either, uint32_t vd) {
     const uint32_t nz = any_plane(both);
 #pragma unroll
     for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
@@ -263,13 +270,14 @@ __device__ __forceinline__ void wide_finish(const UpArgs& a, const NodeDesc& d, 
     }
     uint64_t mx, ms, md;
     store_fitch_set(a.sets, a.cmask, a.cons[word], d.node, a.tiles, tile, lane, both, !AP || vd != 0u, mx, ms, md);
+    if (a.upm != nullptr) push_up_slot(a, a.pslot[gi], tile, lane, mx, ms);   // (subtree form)
     push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms);
     store_kid_masks(a.cmask, (size_t)d.node * a.tiles + tile, lane, md, md);
 }
 
 // One workgroup = one wide node x tile.
 template <bool AP>
-__device__ __forceinline__ void wide_node(const UpArgs& a, const NodeDesc& d, int tile, int wave, int lane,
+__device__ __forceinline__ void wide_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int wave, int lane,
                                           uint32_t (*part)[33][kWave]) {
     const int64_t word = (int64_t)tile * kWave + lane;
     uint32_t both[16], either[16], vd;
@@ -293,7 +301,7 @@ __device__ __forceinline__ void wide_node(const UpArgs& a, const NodeDesc& d, in
         }
         vd |= part[w][32][lane];
     }
-    wide_finish<AP>(a, d, tile, lane, word, both, either, vd);
+    wide_finish<AP>(a, d, gi, tile, lane, word, both, either, vd);
 }
 
 template <bool AP>
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_wide(UpArgs a) {
     int32_t item;
     int tile;
     block_item(a.tiles, item, tile);
-    wide_node<AP>(a, a.desc[item], tile, wave, lane, part);
+    wide_node<AP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, wave, lane, part);
 }
 
 // A level holding nodes of both kinds (polytomies, deep trees) in ONE launch instead of two
@@ -318,12 +326,12 @@ __global__ __launch_bounds__(kBlock) void k_fitch_up_mixed(UpArgs a, const NodeD
         int32_t item;
         int tile;
         wave_item(wave, a.tiles, item, tile);
-        if (item < a.count) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[item], tile, lane);
+        if (item < a.count) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
         return;
     }
     const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
     const int32_t item = b / a.tiles;
-    wide_node<AP>(a, wdesc[item], b - item * a.tiles, wave, lane, part);
+    wide_node<AP>(a, wdesc[item], (int32_t)(wdesc - a.desc_all) + item, b - item * a.tiles, wave, lane, part);
 }
 
 // Narrow levels (PM_OPT_NARROW): a run of consecutive post-order levels with few nodes each
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
     for (int32_t h = h0; h < h1; ++h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
                       e = class_off[(h + 1) * kDegreeClasses];
-        for (int32_t i = b + wave; i < m; i += kBandWaves) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[i], tile, lane);
+        for (int32_t i = b + wave; i < m; i += kBandWaves) fitch_up_node<AP, false, SUB, GROUP>(a, a.desc[i], i, tile, lane);
         for (int32_t i = m; i < e; ++i) {   // out-degree > 3
             if (wave == 0) {
 #pragma unroll
@@ -364,7 +372,7 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
             if (wave == 0) {
 #pragma unroll
                 for (int v = 0; v < 16; ++v) { both[v] = acc[v][lane]; either[v] = acc[16 + v][lane]; }
-                wide_finish<AP>(a, d, tile, lane, word, both, either, acc[32][lane]);
+                wide_finish<AP>(a, d, i, tile, lane, word, both, either, acc[32][lane]);
             }
         }
         __syncthreads();
@@ -457,6 +465,10 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const int form = sub ? 2 : virt ? 1 : 0;   // pre-order level tables (lvl_down)
     const int up_form = grp ? 3 : form;        // post-order ones (lvl_up)
     up.desc_all = up_desc;
+    // up slots: the subtree form's kernels (alloc_work sizes them for its two up orders)
+    if (sub && c->upm == nullptr) return hipErrorInvalidValue;
+    up.upm = sub ? c->upm : nullptr;
+    up.pslot = grp ? dt.pslot_g : dt.pslot_k;
     const int H = (int)up_off.size() - 1;
     // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
     auto narrow_up = [&](int h) {

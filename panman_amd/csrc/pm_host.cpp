@@ -80,6 +80,8 @@ void free_tree(DevTree& t) {
     dev_free(t.up_desc_gs);
     dev_free(t.down_desc_k);
     dev_free(t.down_desc_ks);
+    dev_free(t.pslot_k);
+    dev_free(t.pslot_g);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
     dev_free(t.lvl);
@@ -113,6 +115,8 @@ void free_work(pm_ctx* c) {
     drop_graph(c);
     dev_free(c->sets);
     dev_free(c->cmask);
+    dev_free(c->upm);
+    c->upm_bytes = 0;
     dev_free(c->finals);
     dev_free(c->sk_parts);
     dev_free(c->recs);
@@ -165,6 +169,17 @@ int alloc_work(pm_ctx* c, int mode) {
             return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));
         c->cmask_bytes = need_mask;
     }
+    // up slots: Fitch, subtree form (every leaf present, some S2 / S3 node)
+    if (mode == PM_MODE_FITCH && c->subtree_form && c->ht.num_sshape > 0) {
+        const size_t need = (size_t)std::max(c->ht.up_items_k, c->ht.up_items_g) * (wpad / kWave) * 4 * sizeof(uint64_t);
+        if (need > c->upm_bytes) {
+            dev_free(c->upm);
+            c->upm_bytes = 0;
+            if ((e = hipMalloc(reinterpret_cast<void**>(&c->upm), need)) != hipSuccess)
+                return fail(c, PM_ERR_OOM, std::string("up slots: ") + hipGetErrorString(e));
+            c->upm_bytes = need;
+        }
+    }
     if (!fitch) {   // Sankoff nodes of out-degree > 255: part counters
         const size_t parts = (size_t)std::max(c->ht.part_off.empty() ? 0 : c->ht.part_off.back(),
                                               std::max(c->ht.part_off_v.empty() ? 0 : c->ht.part_off_v.back(),
@@ -203,7 +218,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
                               (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
-                              (uint64_t)c->sub_down,
+                              (uint64_t)c->sub_down, (uint64_t)(uintptr_t)c->upm,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -939,8 +954,23 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
         return std::make_pair(desc, order);
     };
-    const std::vector<NodeDesc> up_desc_g =
-        make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g).first;
+    const auto groups_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g);
+    const std::vector<NodeDesc>& up_desc_g = groups_g.first;
+    // up slots: each descriptor's parent item and child slot (the parent's first / second
+    // child) in the same array, for the subtree form's two up orders
+    auto make_pslot = [&](const std::vector<int32_t>& order, const std::vector<NodeDesc>& desc) {
+        std::vector<int32_t> pos(I, -1), ps(order.size(), -1);
+        for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (int32_t)k;
+        for (size_t k = 0; k < desc.size(); ++k)
+            for (int j = 0; j < 2 && j < desc[k].e1 - desc[k].e0; ++j) {
+                const int32_t x = j == 0 ? desc[k].c0 : desc[k].c1;
+                if (x >= 0 && !(x & kVirtualBit) && pos[x] >= 0) ps[pos[x]] = (int32_t)k * 2 + j;
+            }
+        return ps;
+    };
+    const std::vector<int32_t> pslot_k = make_pslot(up_order_k, up_desc_k), pslot_g = make_pslot(groups_g.second, up_desc_g);
+    ht.up_items_k = (int32_t)up_desc_k.size();
+    ht.up_items_g = (int32_t)up_desc_g.size();
     // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
     // above 255 children never group), so pad0 / pad1 here index the grouped array only
     std::vector<NodeDesc> up_desc_gs =
@@ -1111,6 +1141,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.up_desc_gs, up_desc_gs)) != hipSuccess ||
         (e = up(&dt.down_desc_k, down_desc_k)) != hipSuccess ||
         (e = up(&dt.down_desc_ks, down_desc_ks)) != hipSuccess ||
+        (e = up(&dt.pslot_k, pslot_k)) != hipSuccess ||
+        (e = up(&dt.pslot_g, pslot_g)) != hipSuccess ||
         (e = up(&dt.vinner, vinner)) != hipSuccess ||
         (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
         (e = up(&dt.lvl, lvl)) != hipSuccess) {

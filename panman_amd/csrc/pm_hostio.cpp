@@ -266,7 +266,7 @@ int pm_memory_footprint(pm_ctx* c, int64_t* out, int n) {
     if (c->leaf_present) v[1] += L * wpad * (int64_t)sizeof(uint32_t);
     v[2] = (int64_t)c->sub_planes_bytes;
     v[3] = (int64_t)c->sets_bytes;
-    v[4] = (int64_t)c->cmask_bytes;
+    v[4] = (int64_t)(c->cmask_bytes + c->upm_bytes);   // (mask records + up slots)
     v[5] = (int64_t)c->sk_parts_bytes;
     if (c->recs) v[6] = c->shard_cap * pm::kShards * (int64_t)sizeof(pm_mut) + pm::kShards * 4;
     v[7] = (int64_t)c->tree_bytes;

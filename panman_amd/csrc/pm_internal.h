@@ -124,6 +124,9 @@ struct DevTree {
     NodeDesc* down_desc_k = nullptr;
     NodeDesc* down_desc_ks = nullptr;  // ... with their S2 / S3 children kept (PM_OPT_SUB_DOWN)
     int32_t* vinner = nullptr;        // [I][2] an S2 / S3 node's cherries (dense), -1 padded
+    // up slots (UpArgs::upm): per up_desc_k / up_desc_g item, parent item * 2 + slot, or -1
+    int32_t* pslot_k = nullptr;
+    int32_t* pslot_g = nullptr;
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
     // level tables on the device (the narrow-band launches walk several levels): the host
     // arrays up_class_off{,_v,_k}, down_level_off{,_v,_k}, down_dense_base_k back to back
@@ -170,6 +173,7 @@ struct HostTree {
     std::vector<int32_t> up_level_off_gs, up_class_off_gs;
     std::vector<uint8_t> up_leafy_gs, up_recomp_gs;
     bool down_dense_k = false;
+    int32_t up_items_k = 0, up_items_g = 0;   // descriptor counts (up slot storage)
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;
@@ -228,6 +232,8 @@ struct pm_ctx {
     size_t sets_bytes = 0;
     uint64_t* cmask = nullptr;        // Fitch: [I][tile] complex-lane masks
     size_t cmask_bytes = 0;
+    uint64_t* upm = nullptr;          // Fitch subtree form: [up items][tile][4] up slots (UpArgs::upm)
+    size_t upm_bytes = 0;
     uint4* finals = nullptr;          // [I][W] synthetic generator scratch (internal sequences)
     size_t finals_bytes = 0;
     uint32_t* sk_parts = nullptr;     // Sankoff part counters [parts][kPartPlanes][wpad]

@@ -90,7 +90,34 @@ struct UpArgs {
     int64_t wpad;
     bool absent_code0;     // block Sankoff: a leaf missing from the column is state 0
     bool all_present;      // every leaf present at every site (dirty-lane rules)
+    // Up slots (Fitch subtree form; null otherwise): per (descriptor item, tile) the (x, s)
+    // masks of the item's first two children, {c0.x, c0.s, c1.x, c1.s}, written by each child's
+    // own post-order wave (pslot[item] = parent item * 2 + slot, or -1).  A node's wave loads
+    // them beside its descriptor -- both addressed by its item index alone -- so its children's
+    // record loads wait for one round trip instead of two (descriptor, then the children's
+    // mask records).
+    uint64_t* upm;
+    const int32_t* pslot;
 };
+
+struct UpSlots {
+    uint64_t x0, s0, x1, s1;
+};
+
+// Item gi's up slots, loaded from nothing but gi (no dependence on its descriptor).
+__device__ __forceinline__ UpSlots load_up_slots(const UpArgs& a, int32_t gi, int tile) {
+    const uint64_t* q = a.upm + ((size_t)gi * a.tiles + tile) * 4;
+    return UpSlots{q[0], q[1], q[2], q[3]};
+}
+
+// A node's (x, s) masks into its parent's slot (lane 0; ps = pslot[gi], loaded early).
+__device__ __forceinline__ void push_up_slot(const UpArgs& a, int32_t ps, int tile, int lane, uint64_t mx, uint64_t ms) {
+    if (ps >= 0 && lane == 0) {
+        uint64_t* q = a.upm + ((size_t)(ps >> 1) * a.tiles + tile) * 4 + (ps & 1) * 2;
+        q[0] = mx;
+        q[1] = ms;
+    }
+}
 
 // The leaf words of S2 / S3 node `item` (dense index sbase + item) at one word: vl[0..3]'s
 // words in four consecutive uint4 (pm_ctx::sub_planes).
@@ -504,9 +531,10 @@ struct ChildFetch {
 // LEAFY: the caller knows c is a leaf or a virtual leaf-parent (no record, fewer registers).
 // SUB: subtree form -- a virtual child may be an S2 / S3 subtree (three or four leaves, in
 // code, v[0], v[1], v[2]).
-template <int REC = kFitchRec, bool LEAFY = false, bool SUB = false>
+// SLOT: a record child's (x, s) masks are (sx, ss), from its parent's up slot (UpArgs::upm).
+template <int REC = kFitchRec, bool LEAFY = false, bool SUB = false, bool SLOT = false>
 __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 vl, int tile, int lane, int64_t word,
-                                               ChildFetch& f) {
+                                               ChildFetch& f, uint64_t sx = 0, uint64_t ss = 0) {
     f.cx = false;
     if (c < 0) {
         f.code = a.leaf_planes[(size_t)(-c - 1) * a.wpad + word];
@@ -524,7 +552,7 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         }
     } else if (!LEAFY) {
         const size_t rec = (size_t)c * a.tiles + tile;
-        const RecMask m = rec_mask(a.cmask, rec);
+        const RecMask m = SLOT ? RecMask{sx, ss, 0, 0, 0} : rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * REC;   // Sankoff: the Z0 planes
         f.cx = (m.x >> lane) & 1ull;
         f.code = rec_code_all(p, m, lane, a.cons, word);
@@ -670,14 +698,14 @@ __device__ __forceinline__ void virtual_set16(const Args& a, int32_t v, int64_t 
 // stride (Fitch sets, or Sankoff's whose first 16 planes are Z0; a recomputed Sankoff child is
 // binary, so its Z0 is this same AND-else-OR of its children's Z0).
 template <bool SUB, int D, int REC>
-__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
-                                               uint32_t* both, uint32_t* either, uint32_t& vd);
+__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane,
+                                               int64_t word, uint32_t* both, uint32_t* either, uint32_t& vd);
 
 template <bool SUB, int D, int REC>
-__device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc& cd, int tile, int lane, int64_t word,
-                                                uint32_t* x) {
+__device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc& cd, int32_t gi, int tile, int lane,
+                                                int64_t word, uint32_t* x) {
     uint32_t both[16], either[16], vd = 0;
-    fold_first_two<SUB, D, REC>(a, cd, tile, lane, word, both, either, vd);
+    fold_first_two<SUB, D, REC>(a, cd, gi, tile, lane, word, both, either, vd);
     for (int32_t e = cd.e0 + 2; e < cd.e1; ++e) {
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
@@ -689,16 +717,20 @@ __device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc&
 }
 
 template <bool SUB, int D, int REC>
-__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int tile, int lane, int64_t word,
-                                               uint32_t* both, uint32_t* either, uint32_t& vd) {
+__device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane,
+                                               int64_t word, uint32_t* both, uint32_t* either, uint32_t& vd) {
+    constexpr bool SLOT = SUB && REC == kFitchRec;   // (Fitch subtree form: up slots)
+    UpSlots sl{0, 0, 0, 0};
+    if constexpr (SLOT) sl = load_up_slots(a, gi, tile);
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
     const bool two = d.e1 - d.e0 > 1;
     if (D > 0 && (d.pad0 >= 0 || d.pad1 >= 0)) {
         uint32_t x0[16];
-        child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[d.pad0 >= 0 ? d.pad0 : d.pad1], tile, lane, word, x0);
+        const int32_t r0 = d.pad0 >= 0 ? d.pad0 : d.pad1;
+        child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[r0], r0, tile, lane, word, x0);
         if (d.pad0 >= 0 && d.pad1 >= 0) {
             uint32_t x1[16];
-            child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[d.pad1], tile, lane, word, x1);
+            child_recompute<SUB, (D > 0 ? D - 1 : 0), REC>(a, a.desc_all[d.pad1], d.pad1, tile, lane, word, x1);
 #pragma unroll
             for (int v = 0; v < 16; ++v) { both[v] = x0[v] & x1[v]; either[v] = x0[v] | x1[v]; }
             return;
@@ -710,7 +742,7 @@ __device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& 
             const int32_t c = first ? d.c0 : d.c1;
             const int4 vl = first ? vl0 : vl1;
             ChildFetch f;
-            fetch_child_ap<REC, false, SUB>(a, c, vl, tile, lane, word, f);
+            fetch_child_ap<REC, false, SUB, SLOT>(a, c, vl, tile, lane, word, f, first ? sl.x0 : sl.x1, first ? sl.s0 : sl.s1);
             fold_child_ap<SUB>(c, vl, f, both, either, vd);
         }
         return;
@@ -718,8 +750,8 @@ __device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& 
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
     ChildFetch f0, f1;
-    fetch_child_ap<REC, false, SUB>(a, d.c0, vl0, tile, lane, word, f0);
-    if (two) fetch_child_ap<REC, false, SUB>(a, d.c1, vl1, tile, lane, word, f1);
+    fetch_child_ap<REC, false, SUB, SLOT>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
+    if (two) fetch_child_ap<REC, false, SUB, SLOT>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
     __builtin_amdgcn_sched_barrier(0);
     fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
     if (two) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);

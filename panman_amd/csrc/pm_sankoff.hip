@@ -76,7 +76,7 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && SUB && B >= 2), "grouped launches: subtree form, narrow nodes");
         uint32_t both[16], either[16], vd = 0;
-        fold_first_two<SUB, kUpGroupDepth, kSankoffRec>(a, d, tile, lane, word, both, either, vd);
+        fold_first_two<SUB, kUpGroupDepth, kSankoffRec>(a, d, -1, tile, lane, word, both, either, vd);
         const bool two = e1 - e0 > 1;
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
