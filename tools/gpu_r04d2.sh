@@ -2,7 +2,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_variants.sh fitch 2 default base || exit 4
+BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_variants.sh fitch 2 default noslots base || exit 4
 BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_args.sh 2 "--sub-down 0" "--sub-down 1" || exit 8
 bash tools/replay_variants.sh base rp_e4w5 rp_e8w5 rp_e16w4 || exit 6
 bash tools/fetch_calibrate.sh || exit 5
