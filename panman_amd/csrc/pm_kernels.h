@@ -584,8 +584,12 @@ __device__ __forceinline__ void fetch_child_ap_m(const UpArgs& a, int32_t c, int
     for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
 }
 
+// (the builtin returns int: each half goes through uint32_t, or the low half's bit 31 would
+// sign-extend over the high half)
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t code_ne(const uint4& p, const uint4& q) {

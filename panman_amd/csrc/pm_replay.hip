@@ -120,7 +120,7 @@ __device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j)
             if (!found && pend[j]) {
-                k = __builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                k = (uint32_t)__builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
                 found = true;
             }
         any = false;
@@ -164,7 +164,7 @@ __device__ __forceinline__ void edit_write_overrides(const EditRound& r, char* b
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j)
             if (!found && pend[j]) {
-                k = __builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                k = (uint32_t)__builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
                 found = true;
             }
         any = false;
