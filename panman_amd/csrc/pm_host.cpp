@@ -82,6 +82,7 @@ void free_tree(DevTree& t) {
     dev_free(t.down_desc_ks);
     dev_free(t.pslot_k);
     dev_free(t.pslot_g);
+    dev_free(t.pslot_gs);
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
     dev_free(t.lvl);
@@ -169,9 +170,10 @@ int alloc_work(pm_ctx* c, int mode) {
             return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));
         c->cmask_bytes = need_mask;
     }
-    // up slots: Fitch, subtree form (every leaf present, some S2 / S3 node)
-    if (mode == PM_MODE_FITCH && c->subtree_form && c->ht.num_sshape > 0) {
-        const size_t need = (size_t)std::max(c->ht.up_items_k, c->ht.up_items_g) * (wpad / kWave) * 4 * sizeof(uint64_t);
+    // up slots: Fitch / Sankoff, subtree form (every leaf present, some S2 / S3 node)
+    if ((mode == PM_MODE_FITCH || mode == PM_MODE_SANKOFF) && c->subtree_form && c->ht.num_sshape > 0) {
+        const size_t items = (size_t)std::max(c->ht.up_items_k, std::max(c->ht.up_items_g, c->ht.up_items_gs));
+        const size_t need = items * (wpad / kWave) * 4 * sizeof(uint64_t);
         if (need > c->upm_bytes) {
             dev_free(c->upm);
             c->upm_bytes = 0;
@@ -973,8 +975,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.up_items_g = (int32_t)up_desc_g.size();
     // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
     // above 255 children never group), so pad0 / pad1 here index the grouped array only
-    std::vector<NodeDesc> up_desc_gs =
-        make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs).first;
+    auto groups_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs);
+    std::vector<NodeDesc> up_desc_gs = groups_gs.first;
+    const std::vector<int32_t> pslot_gs = make_pslot(groups_gs.second, up_desc_gs);
+    ht.up_items_gs = (int32_t)up_desc_gs.size();
     // subtree-form pre-order descriptors list only the children the level kernel handles:
     // S2 / S3 children are tail items (k_tail<.., SUB>); a node left with none gets a
     // materialised placeholder (c0 = 0, no loads, no records)
@@ -1143,6 +1147,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.down_desc_ks, down_desc_ks)) != hipSuccess ||
         (e = up(&dt.pslot_k, pslot_k)) != hipSuccess ||
         (e = up(&dt.pslot_g, pslot_g)) != hipSuccess ||
+        (e = up(&dt.pslot_gs, pslot_gs)) != hipSuccess ||
         (e = up(&dt.vinner, vinner)) != hipSuccess ||
         (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
         (e = up(&dt.lvl, lvl)) != hipSuccess) {

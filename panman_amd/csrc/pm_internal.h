@@ -127,6 +127,7 @@ struct DevTree {
     // up slots (UpArgs::upm): per up_desc_k / up_desc_g item, parent item * 2 + slot, or -1
     int32_t* pslot_k = nullptr;
     int32_t* pslot_g = nullptr;
+    int32_t* pslot_gs = nullptr;      // ... of up_desc_gs (Sankoff's groups)
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
     // level tables on the device (the narrow-band launches walk several levels): the host
     // arrays up_class_off{,_v,_k}, down_level_off{,_v,_k}, down_dense_base_k back to back
@@ -173,7 +174,7 @@ struct HostTree {
     std::vector<int32_t> up_level_off_gs, up_class_off_gs;
     std::vector<uint8_t> up_leafy_gs, up_recomp_gs;
     bool down_dense_k = false;
-    int32_t up_items_k = 0, up_items_g = 0;   // descriptor counts (up slot storage)
+    int32_t up_items_k = 0, up_items_g = 0, up_items_gs = 0;   // descriptor counts (up slot storage)
     int64_t num_sshape = 0;
     std::vector<uint8_t> sshape;          // [I] 1: S2, 2: S3 (subtree form), else 0
     int32_t num_tail_k = 0;

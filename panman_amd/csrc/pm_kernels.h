@@ -723,7 +723,7 @@ __device__ __forceinline__ void child_recompute(const UpArgs& a, const NodeDesc&
 template <bool SUB, int D, int REC>
 __device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane,
                                                int64_t word, uint32_t* both, uint32_t* either, uint32_t& vd) {
-    constexpr bool SLOT = SUB && REC == kFitchRec;   // (Fitch subtree form: up slots)
+    constexpr bool SLOT = SUB;   // (subtree form: up slots)
     UpSlots sl{0, 0, 0, 0};
     if constexpr (SLOT) sl = load_up_slots(a, gi, tile);
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);

@@ -60,10 +60,14 @@ __device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& fi
 // first / second children of this same launch -- binary, so their Z0 is the AND-else-OR of
 // their children's Z0 -- recomputed in registers (fold_first_two) instead of loaded; the
 // first two children's counts then follow from their AND (count 2) and OR (count >= 1).
+// gi: the node's index in the descriptor array; SUB: up slots (UpArgs::upm), as fitch_up_node.
 template <int B, bool AP, bool SUB = false, bool GROUP = false>
-__device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int tile, int lane) {
+__device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane) {
     const int32_t n = d.node;
     const int64_t word = (int64_t)tile * kWave + lane;
+    UpSlots sl{0, 0, 0, 0};
+    if constexpr (SUB) sl = load_up_slots(a, gi, tile);
+    const int32_t ps = SUB ? a.pslot[gi] : -1;
 
     uint32_t cnt[16][B];
 #pragma unroll
@@ -76,7 +80,7 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     if (GROUP && (d.pad0 >= 0 || d.pad1 >= 0)) {
         static_assert(!GROUP || (AP && SUB && B >= 2), "grouped launches: subtree form, narrow nodes");
         uint32_t both[16], either[16], vd = 0;
-        fold_first_two<SUB, kUpGroupDepth, kSankoffRec>(a, d, -1, tile, lane, word, both, either, vd);
+        fold_first_two<SUB, kUpGroupDepth, kSankoffRec>(a, d, gi, tile, lane, word, both, either, vd);
         const bool two = e1 - e0 > 1;
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
@@ -90,8 +94,8 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
         const int4 vl0 = SUB ? make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]) : make_int4(d.vl0[0], d.vl0[1], -1, -1);
         const int4 vl1 = SUB ? make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]) : make_int4(d.vl1[0], d.vl1[1], -1, -1);
         ChildFetch f0, f1;
-        fetch_child_ap<kSankoffRec, false, SUB>(a, d.c0, vl0, tile, lane, word, f0);
-        if (e1 - e0 > 1) fetch_child_ap<kSankoffRec, false, SUB>(a, d.c1, vl1, tile, lane, word, f1);
+        fetch_child_ap<kSankoffRec, false, SUB, SUB>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
+        if (e1 - e0 > 1) fetch_child_ap<kSankoffRec, false, SUB, SUB>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t vd = 0;
         child_set_ap<SUB>(d.c0, vl0, f0, z, vd);
@@ -149,6 +153,7 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
     uint64_t rx, rs, rd;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1,
                   !a.all_present || e1 - e0 > 2 || sd != 0u, rx, rs, rd);
+    push_up_slot(a, ps, tile, lane, rx, rs);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs, rd, n == a.root_dense);
 }
 
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? PM_SK_GROUP_UP_WAVES : PM_SK_UP_WAV
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    sankoff_up_node<B, AP, SUB, GROUP>(a, a.desc[item], tile, lane);
+    sankoff_up_node<B, AP, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
@@ -175,8 +180,8 @@ __global__ __launch_bounds__(kBlock, GROUP ? PM_SK_GROUP_UP_WAVES : PM_SK_UP_WAV
 // per-wave counts is the node's count: src/fitchSankoff.cpp:391-402 is a sum over
 // children), then Z0 / Z1 as in k_sankoff_up.
 template <int B>
-__device__ __forceinline__ void sankoff_wide_node(const UpArgs& a, const NodeDesc& d, int tile, int wave, int lane,
-                                                  uint32_t (*part)[kWave]) {
+__device__ __forceinline__ void sankoff_wide_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int wave,
+                                                  int lane, uint32_t (*part)[kWave]) {
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     uint32_t cnt[16][B];
@@ -260,6 +265,7 @@ __device__ __forceinline__ void sankoff_wide_node(const UpArgs& a, const NodeDes
     }
     uint64_t rx, rs, rd;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs, rd);
+    if (a.upm != nullptr) push_up_slot(a, a.pslot[gi], tile, lane, rx, rs);   // (subtree form)
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_wide(UpArgs a) {
     int32_t item;
     int tile;
     block_item(a.tiles, item, tile);
-    sankoff_wide_node<B>(a, a.desc[item], tile, wave, lane, part);
+    sankoff_wide_node<B>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, wave, lane, part);
 }
 
 // A small level holding nodes of out-degree <= 3 and 4..255 in ONE launch instead of two or
@@ -286,12 +292,12 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_up_mixed(UpArgs a, const Nod
         int32_t item;
         int tile;
         wave_item(wave, a.tiles, item, tile);
-        if (item < a.count) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[item], tile, lane);
+        if (item < a.count) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
         return;
     }
     const int32_t b = (int32_t)blockIdx.x - narrow_blocks;
     const int32_t item = b / a.tiles;
-    sankoff_wide_node<BW>(a, wdesc[item], b - item * a.tiles, wave, lane, part);
+    sankoff_wide_node<BW>(a, wdesc[item], (int32_t)(wdesc - a.desc_all) + item, b - item * a.tiles, wave, lane, part);
 }
 
 // Narrow post-order levels (PM_OPT_NARROW, see k_fitch_up_band): a run of levels whose
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(kBandBlock) void k_sankoff_up_band(UpArgs a, const 
     const int tile = blockIdx.x;
     for (int32_t h = h0; h < h1; ++h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1];
-        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[i], tile, lane);
+        for (int32_t i = b + wave; i < m; i += kBandWaves) sankoff_up_node<2, AP, SUB, GROUP>(a, a.desc[i], i, tile, lane);
         __syncthreads();
     }
 }
@@ -436,6 +442,7 @@ __global__ __launch_bounds__(kBlock) void k_sankoff_merge(UpArgs a, const uint32
     }
     uint64_t rx, rs, rd;
     store_sankoff(a.sets, a.cmask, a.cons, n, a.tiles, tile, lane, word, z0, z1, true, rx, rs, rd);
+    if (a.upm != nullptr) push_up_slot(a, a.pslot[(int32_t)(a.desc - a.desc_all) + item], tile, lane, rx, rs);
     push_children(a, tile, lane, e0, e1, d.c0, d.c1, rx, rs);
 }
 
@@ -479,6 +486,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     up.tiles = tiles;
     up.wpad = wpad;
     up.desc_all = up_desc;   // grouped launches: pad0 / pad1 index the whole array
+    // up slots: the subtree form's kernels (alloc_work sizes them for its up orders)
+    if (sub && c->upm == nullptr) return hipErrorInvalidValue;
+    up.upm = sub ? c->upm : nullptr;
+    up.pslot = grp ? dt.pslot_gs : dt.pslot_k;
     const int H = (int)(grp ? ht.up_level_off_gs : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off).size() - 1;
     // nodes [b, e) of one level with more than 255 children: parts, then the merge
     auto launch_parts = [&](int32_t b, int32_t e, hipStream_t s) {
