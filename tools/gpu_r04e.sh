@@ -4,6 +4,8 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+bash tools/fetch_calibrate.sh || exit 5
+(cd /tmp && timeout -k 5 60 rocprofv3 -L > $GRAFT_REPO_ROOT/gpurun_out/rocprof_counters.txt 2>&1) || true
 bash tools/pmc_variants.sh FETCH_SIZE base nodirty nopfinal || exit 2
 bash tools/ab_variants.sh fitch 1 default nodirty nopfinal || exit 3
 timeout -k 10 600 python bench.py --no-cpu --with none --leaves 8000000 --sites 3750 --steps 5 --warmup 2 > gpurun_out/c4share_r04e.json 2> gpurun_out/c4share_r04e.err || { tail -5 gpurun_out/c4share_r04e.err; exit 4; }
