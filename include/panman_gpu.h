@@ -106,6 +106,9 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_SUB_DOWN (default 0): Fitch, subtree form -- a three- or four-leaf subtree's
  *                  finals and records come from its parent's pre-order wave instead of a
  *                  wave of their own after the levels.
+ *   PM_OPT_PLAIN_UP (default 1): Fitch, grouped subtree form -- a post-order launch's binary
+ *                  nodes with no three- / four-leaf subtree child and nothing recomputed run in
+ *                  a lean kernel (fewer registers, more waves in flight) before the rest.
  *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the
  *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
  *                  re-run with a larger buffer when its results are read (pm_mutation_count,
@@ -122,6 +125,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_UP_GROUP 10
 #define PM_OPT_RECORD_CAP 12
 #define PM_OPT_SUB_DOWN 13
+#define PM_OPT_PLAIN_UP 14
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

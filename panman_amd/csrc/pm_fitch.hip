@@ -42,8 +42,12 @@ namespace {
 // GROUP: the descriptor's pad0 / pad1 (>= 0) name first / second children of this same
 // launch, recomputed here (child_recompute) instead of loaded.
 // gi: the node's index in the descriptor array (up slots, UpArgs::upm).
-template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
+// PLAIN (subtree form, grouped order's plain prefix: pm_host.cpp make_groups): binary, neither
+// child an S2 / S3 subtree -- the S-subtree code and the polytomy loop compiled out, 78 VGPRs
+// instead of 117, so 6 waves per SIMD instead of 4.
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false, bool PLAIN = false>
 __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane) {
+    constexpr bool SS = SUB && !PLAIN;   // S2 / S3 children possible
     const int32_t n = d.node, e0 = d.e0, e1 = d.e1;
     const int64_t word = (int64_t)tile * kWave + lane;
     // subtree form: the children's masks from this node's up slots, its own into its parent's
@@ -63,18 +67,18 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     } else if constexpr (AP) {   // both children's loads in flight together
         ChildFetch f0, f1;
         constexpr bool SLOT = SUB && !LEAFY;
-        fetch_child_ap<kFitchRec, LEAFY, SUB, SLOT>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
-        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SUB, SLOT>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
+        fetch_child_ap<kFitchRec, LEAFY, SS, SLOT>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
+        if (e1 - e0 > 1) fetch_child_ap<kFitchRec, LEAFY, SS, SLOT>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
         __builtin_amdgcn_sched_barrier(0);
         // after the children's consensus loads: loaded before them, the compiler reuses it
         // for them through register copies that wait on every outstanding load
         cw = a.cons[word];
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
-        child_set_ap<SUB>(d.c0, vl0, f0, both, vd0);
+        child_set_ap<SS>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
-        if (e1 - e0 > 1) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd1);
+        if (e1 - e0 > 1) fold_child_ap<SS>(d.c1, vl1, f1, both, either, vd1);
         vd = vd0 | vd1;
         split = true;
     } else {
@@ -84,7 +88,7 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         if (e1 - e0 > 1) fold_child<AP>(a, d.c1, vl1, tile, lane, word, both, either, vd);
         cw = a.cons[word];
     }
-    for (int32_t e = e0 + 2; e < e1; ++e) {   // polytomies
+    for (int32_t e = e0 + 2; !PLAIN && e < e1; ++e) {   // polytomies
         const int32_t c = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
         const int4 vl = c >= 0 && (c & kVirtualBit) ? a.vleaf[c & kDenseMask] : make_int4(-1, -1, -1, -1);
         if constexpr (LEAFY) {
@@ -124,8 +128,11 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
     store_kid_masks(a.cmask, (size_t)n * a.tiles + tile, lane, sub_shaped(d.c0) ? md1 : md0, md1);
 }
 
-template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false>
-__global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
+#ifndef PM_PLAIN_UP_WAVES
+#define PM_PLAIN_UP_WAVES 6
+#endif
+template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false, bool PLAIN = false>
+__global__ __launch_bounds__(kBlock, PLAIN ? PM_PLAIN_UP_WAVES : GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? PM_SUB_LEAFY_WAVES : PM_SUB_UP_WAVES) : LEAFY ? PM_LEAFY_WAVES : AP ? 5 : 1) void k_fitch_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 #ifdef PM_UP_LDS_PAD   // occupancy experiments only: caps the resident workgroups per CU
     __shared__ uint32_t occ_pad[PM_UP_LDS_PAD / 4];
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(kBlock, GROUP ? PM_GROUP_UP_WAVES : SUB ? (LEAFY ? 
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    fitch_up_node<AP, LEAFY, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
+    fitch_up_node<AP, LEAFY, SUB, GROUP, PLAIN>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), the children dealt
@@ -532,11 +539,27 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             if (!fork) timer_end(c, 0);
         }
         if (m > b) {
-            up.desc = up_desc + b;
-            up.count = m - b;
-            const dim3 grid = wave_grid(up.count, tiles);
             const bool leafy = grp ? ht.up_leafy_g[h] : sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
+            // the grouped order's plain prefix (binary, no S2 / S3 child, nothing recomputed):
+            // the lean kernel, then the rest of the class
+            const int32_t np = grp && !leafy && c->plain_up ? std::min(ht.up_plain_g[h], m - b) : 0;
             timer_begin(c, 0);
+            if (np > 0) {
+                up.desc = up_desc + b;
+                up.count = np;
+                hipLaunchKernelGGL((k_fitch_up<true, false, true, false, true>), wave_grid(np, tiles), dim3(kBlock), 0, c->stream, up);
+            }
+            up.desc = up_desc + b + np;
+            up.count = m - b - np;
+            const dim3 grid = wave_grid(up.count, tiles);
+            if (up.count == 0) {
+                if (fork) {
+                    const hipError_t je = side_join(c);
+                    if (je != hipSuccess) return je;
+                }
+                timer_end(c, 0);
+                continue;
+            }
             if (sub && leafy) hipLaunchKernelGGL((k_fitch_up<true, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (grp && ht.up_recomp_g[h]) hipLaunchKernelGGL((k_fitch_up<true, false, true, true>), grid, dim3(kBlock), 0, c->stream, up);
             else if (sub) hipLaunchKernelGGL((k_fitch_up<true, false, true>), grid, dim3(kBlock), 0, c->stream, up);

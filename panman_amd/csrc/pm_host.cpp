@@ -220,7 +220,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
                               (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
-                              (uint64_t)c->sub_down, (uint64_t)(uintptr_t)c->upm,
+                              (uint64_t)c->sub_down, (uint64_t)c->plain_up, (uint64_t)(uintptr_t)c->upm,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -465,6 +465,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     }
     if (option == PM_OPT_UP_GROUP) {
         c->up_group = value != 0;
+        return PM_OK;
+    }
+    if (option == PM_OPT_PLAIN_UP) {
+        c->plain_up = value != 0;
         return PM_OK;
     }
     if (option == PM_OPT_SUB_DOWN) {
@@ -890,7 +894,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     // launch: big levels fill the chip by themselves and pay for the recomputation (measured
     // at N*).
     auto make_groups = [&](int32_t max_rc, std::vector<int32_t>& level_off, std::vector<int32_t>& class_off,
-                           std::vector<uint8_t>& leafy_out, std::vector<uint8_t>& recomp_out) {
+                           std::vector<uint8_t>& leafy_out, std::vector<uint8_t>& recomp_out,
+                           std::vector<int32_t>& plain_out) {
         auto is_mat = [](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
         auto narrow = [&](int32_t d) { return degree_class(ht.child_off[d + 1] - ht.child_off[d]) == 0; };
         auto recomputable = [&](int32_t d) { return ht.child_off[d + 1] - ht.child_off[d] <= max_rc; };
@@ -926,16 +931,29 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             }
             G = std::max(G, lv[d] + 1);
         }
-        // bucket by (launch, degree class), children-first order kept inside a bucket
+        // bucket by (launch, degree class), children-first order kept inside a bucket; in the
+        // out-degree <= 3 class the plain nodes first (binary, neither of the children an S2 / S3
+        // subtree nor recomputed here): one launch of the lean kernel covers them
         class_off.assign((size_t)G * kDegreeClasses + 1, 0);
         auto key = [&](int32_t d) { return lv[d] * kDegreeClasses + degree_class(ht.child_off[d + 1] - ht.child_off[d]); };
+        auto sub_shaped_enc = [](int32_t x) { return x >= 0 && (x & kVirtualBit) && ((x >> kShapeShift) & 3); };
+        auto plain = [&](int32_t d) {
+            if (ht.child_off[d + 1] - ht.child_off[d] > 2 || inl[(size_t)d * 2] >= 0 || inl[(size_t)d * 2 + 1] >= 0) return false;
+            for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e)
+                if (sub_shaped_enc(child_enc_k[e])) return false;
+            return true;
+        };
         for (int32_t d : up_order_k) ++class_off[key(d) + 1];
         for (size_t k = 0; k + 1 < class_off.size(); ++k) class_off[k + 1] += class_off[k];
         std::vector<int32_t> order(up_order_k.size()), cur(class_off.begin(), class_off.end() - 1), pos(I, -1);
-        for (int32_t d : up_order_k) {
-            pos[d] = cur[key(d)]++;
-            order[pos[d]] = d;
-        }
+        plain_out.assign(G, 0);
+        for (int pass = 0; pass < 2; ++pass)
+            for (int32_t d : up_order_k) {
+                if (plain(d) != (pass == 0)) continue;
+                pos[d] = cur[key(d)]++;
+                order[pos[d]] = d;
+                if (pass == 0) ++plain_out[lv[d]];
+            }
         level_off.assign(G + 1, 0);
         for (int32_t l = 0; l <= G; ++l) level_off[l] = class_off[(size_t)l * kDegreeClasses];
         leafy_out.assign(G, 0);
@@ -956,7 +974,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
         return std::make_pair(desc, order);
     };
-    const auto groups_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g);
+    const auto groups_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g, ht.up_plain_g);
     const std::vector<NodeDesc>& up_desc_g = groups_g.first;
     // up slots: each descriptor's parent item and child slot (the parent's first / second
     // child) in the same array, for the subtree form's two up orders
@@ -975,7 +993,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.up_items_g = (int32_t)up_desc_g.size();
     // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
     // above 255 children never group), so pad0 / pad1 here index the grouped array only
-    auto groups_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs);
+    auto groups_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs, ht.up_plain_gs);
     std::vector<NodeDesc> up_desc_gs = groups_gs.first;
     const std::vector<int32_t> pslot_gs = make_pslot(groups_gs.second, up_desc_gs);
     ht.up_items_gs = (int32_t)up_desc_gs.size();

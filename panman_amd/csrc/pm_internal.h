@@ -170,6 +170,9 @@ struct HostTree {
     // subtree form, grouped post-order launches (PM_OPT_UP_GROUP): launch l's nodes by class
     std::vector<int32_t> up_level_off_g, up_class_off_g;
     std::vector<uint8_t> up_leafy_g, up_recomp_g;   // (recomp: some node of the launch recomputes a child)
+    // ... and each launch's "plain" nodes at the front of its out-degree <= 3 class: binary, no
+    // S2 / S3 child, no recomputed child -- the lean, higher-occupancy kernel (k_fitch_up<.., PLAIN>)
+    std::vector<int32_t> up_plain_g, up_plain_gs;
     // ... and Sankoff's (a recomputed child must be binary)
     std::vector<int32_t> up_level_off_gs, up_class_off_gs;
     std::vector<uint8_t> up_leafy_gs, up_recomp_gs;
@@ -214,6 +217,7 @@ struct pm_ctx {
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
     bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
+    bool plain_up = true;             // Fitch grouped subtree form: plain nodes in the lean post-order kernel (PM_OPT_PLAIN_UP)
 
     // column shard
     int64_t num_sites = 0;

@@ -118,6 +118,34 @@ def test_up_groups_equal_heights(engine, narrow, tree, mode):
     assert (gs == ws).all() and (gr == wr).all()
 
 
+@pytest.mark.parametrize("narrow", [0, 16])
+@pytest.mark.parametrize("tree", ["sars-like", "random-join", "polytomy"])
+def test_plain_up_equals_general_kernel(engine, narrow, tree):
+    """PM_OPT_PLAIN_UP: the grouped post-order's plain prefix (binary, no S2 / S3 child,
+    nothing recomputed) in the lean kernel gives the general kernel's records."""
+    if tree == "sars-like":
+        off, idx, root = panman_amd.sars_like_tree(6000, seed=41)
+    elif tree == "random-join":
+        off, idx, root = panman_amd.random_join_tree(6000, seed=42)
+    else:
+        off, idx, root = random_tree(3000, np.random.default_rng(43), max_children=3, unary=0.05)
+    _variant(engine, "virtual")
+    engine.tree_upload(off, idx, root)
+    engine.synth_columns(0, 4500, seed=7)
+    res = []
+    try:
+        for on in (False, True):
+            engine.set_plain_up(on)
+            res.append(_run(engine, 32768, narrow))
+    finally:
+        engine.set_plain_up(True)
+        engine.set_narrow(16)
+    (w, ws, wr), (g, gs, gr) = res
+    assert w.shape[0] > 0
+    assert g.shape == w.shape and (g == w).all()
+    assert (gs == ws).all() and (gr == wr).all()
+
+
 @pytest.mark.parametrize("mode", [panman_amd.MODE_SANKOFF, panman_amd.MODE_BLOCK_SANKOFF])
 @pytest.mark.parametrize("levels", [2, 3, 4])
 @pytest.mark.parametrize("narrow", [0, 16])
