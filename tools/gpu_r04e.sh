@@ -1,12 +1,10 @@
 #!/bin/bash
-# Pre-order traffic attribution (PMC per variant, timing-only variants) and the C4 rank share's
-# footprint.
+# C3 A/Bs (slots / wide prefetch, Sankoff slots, sub-down), replay variants, FETCH calibration
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_variants.sh fitch 2 default noslots base || exit 4
+BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_variants.sh sankoff 1 default noslots || exit 10
+BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_args.sh 2 "--sub-down 0" "--sub-down 1" || exit 8
+bash tools/replay_variants.sh base rp_e4w5 rp_e8w5 rp_e16w4 || exit 6
 bash tools/fetch_calibrate.sh || exit 5
-(cd /tmp && timeout -k 5 60 rocprofv3 -L > $GRAFT_REPO_ROOT/gpurun_out/rocprof_counters.txt 2>&1) || true
-bash tools/pmc_variants.sh FETCH_SIZE base nodirty nopfinal || exit 2
-bash tools/ab_variants.sh fitch 1 default nodirty nopfinal || exit 3
-timeout -k 10 600 python bench.py --no-cpu --with none --leaves 8000000 --sites 3750 --steps 5 --warmup 2 > gpurun_out/c4share_r04e.json 2> gpurun_out/c4share_r04e.err || { tail -5 gpurun_out/c4share_r04e.err; exit 4; }
-python3 -c "import json;d=json.load(open('gpurun_out/c4share_r04e.json'));print('C4 share', round(d['ms_per_step'],3), json.dumps(d['footprint']))"
