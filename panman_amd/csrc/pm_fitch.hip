@@ -43,7 +43,8 @@ namespace {
 // launch, recomputed here (child_recompute) instead of loaded.
 // gi: the node's index in the descriptor array (up slots, UpArgs::upm).
 // PLAIN (subtree form, grouped order's plain prefix: pm_host.cpp make_groups): binary, neither
-// child an S2 / S3 subtree -- the S-subtree code and the polytomy loop compiled out, 78 VGPRs
+// child an S2 / S3 subtree -- the S-subtree code and the polytomy loop compiled out, the child
+// sets branch-free (child_set_plain): 79 VGPRs
 // instead of 117, so 6 waves per SIMD instead of 4.
 template <bool AP, bool LEAFY, bool SUB = false, bool GROUP = false, bool PLAIN = false>
 __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane) {
@@ -75,10 +76,20 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         cw = a.cons[word];
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
-        child_set_ap<SS>(d.c0, vl0, f0, both, vd0);
+        if constexpr (PLAIN) child_set_plain(d.c0, vl0, f0, both, vd0);
+        else child_set_ap<SS>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
-        if (e1 - e0 > 1) fold_child_ap<SS>(d.c1, vl1, f1, both, either, vd1);
+        if constexpr (PLAIN) {
+            if (e1 - e0 > 1) {
+                uint32_t y[16];
+                child_set_plain(d.c1, vl1, f1, y, vd1);
+#pragma unroll
+                for (int v = 0; v < 16; ++v) { either[v] = both[v] | y[v]; both[v] &= y[v]; }
+            }
+        } else if (e1 - e0 > 1) {
+            fold_child_ap<SS>(d.c1, vl1, f1, both, either, vd1);
+        }
         vd = vd0 | vd1;
         split = true;
     } else {

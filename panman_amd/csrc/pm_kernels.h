@@ -647,6 +647,27 @@ __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetc
     }
 }
 
+// A child of a plain node (leaf, leaf-parent of one or two leaves, or record), branch-free over
+// its kind (wave-uniform) and the lane's complex flag: one select per plane.
+__device__ __forceinline__ void child_set_plain(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
+    const bool virt2 = c >= 0 && (c & kVirtualBit) && __builtin_amdgcn_readfirstlane(vl.y) >= 0;
+    const bool rec_cx = c >= 0 && !(c & kVirtualBit) && f.cx;
+    const uint32_t m2 = virt2 ? ~0u : 0u;
+    const uint4 L1 = f.v[0];
+    vd |= m2 & code_ne(f.code, L1);
+    const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u), u = lohi_of(L1.x, L1.y, L1.z, L1.w, m2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t w[4] = {f.v[q].x, f.v[q].y, f.v[q].z, f.v[q].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int v = 4 * q + k;
+            const uint32_t y = (t.lo[v & 3] & t.hi[v >> 2]) | (u.lo[v & 3] & u.hi[v >> 2]);
+            x[v] = rec_cx ? w[k] : y;
+        }
+    }
+}
+
 template <bool SUB = false>
 __device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
                                               uint32_t& vd) {
