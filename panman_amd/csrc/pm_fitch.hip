@@ -25,13 +25,11 @@ namespace {
 #ifndef PM_LEAFY_WAVES
 #define PM_LEAFY_WAVES 6
 #endif
-// (subtree form, leafy level: branch-free child sets, child_set_leafy -- 83 VGPRs; at 6 waves
-// it would spill)
 #ifndef PM_SUB_LEAFY_WAVES
-#define PM_SUB_LEAFY_WAVES 5
+#define PM_SUB_LEAFY_WAVES 4
 #endif
 #ifndef PM_SUB_UP_WAVES
-#define PM_SUB_UP_WAVES 5
+#define PM_SUB_UP_WAVES 4
 #endif
 // GROUP: 4 waves per SIMD, where the recomputation spills ~80 B/lane to scratch; 3 waves
 // (~150 VGPRs, no scratch) cost C3 2 %.  A spilling build of this kernel once gave wrong sets
@@ -79,15 +77,13 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
         if constexpr (PLAIN) child_set_plain(d.c0, vl0, f0, both, vd0);
-        else if constexpr (LEAFY && SUB) child_set_leafy(d.c0, vl0, f0, both, vd0);
         else child_set_ap<SS>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
-        if constexpr (PLAIN || (LEAFY && SUB)) {
+        if constexpr (PLAIN) {
             if (e1 - e0 > 1) {
                 uint32_t y[16];
-                if constexpr (PLAIN) child_set_plain(d.c1, vl1, f1, y, vd1);
-                else child_set_leafy(d.c1, vl1, f1, y, vd1);
+                child_set_plain(d.c1, vl1, f1, y, vd1);
 #pragma unroll
                 for (int v = 0; v < 16; ++v) { either[v] = both[v] | y[v]; both[v] &= y[v]; }
             }

@@ -624,6 +624,28 @@ __device__ __forceinline__ void subtree_set_ap(int shape, const ChildFetch& f, u
 }
 
 // A fetched child's 16-plane set (Fitch) / optimal set Z0 (Sankoff); vd as fold_child's.
+template <bool SUB = false>
+__device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
+    const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = t.lo[v & 3] & t.hi[v >> 2];
+    if (SUB && c >= 0 && (c & kVirtualBit) && ((c >> kShapeShift) & 3)) {
+        subtree_set_ap((c >> kShapeShift) & 3, f, x, vd);
+    } else if (c >= 0 && (c & kVirtualBit)) {
+        if (__builtin_amdgcn_readfirstlane(vl.y) >= 0) {
+            const uint4 L1 = f.v[0];
+            vd |= (f.code.x ^ L1.x) | (f.code.y ^ L1.y) | (f.code.z ^ L1.z) | (f.code.w ^ L1.w);
+            const LoHi u = lohi_of(L1.x, L1.y, L1.z, L1.w, ~0u);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];
+        }
+    } else if (c >= 0 && f.cx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            x[4 * q] = f.v[q].x; x[4 * q + 1] = f.v[q].y; x[4 * q + 2] = f.v[q].z; x[4 * q + 3] = f.v[q].w;
+        }
+    }
+}
 
 // A child of a plain node (leaf, leaf-parent of one or two leaves, or record), branch-free over
 // its kind (wave-uniform) and the lane's complex flag: one select per plane.
@@ -644,64 +666,6 @@ __device__ __forceinline__ void child_set_plain(int32_t c, int4 vl, const ChildF
             x[v] = rec_cx ? w[k] : y;
         }
     }
-}
-
-// A child of a leafy subtree-form node -- a leaf, a leaf-parent of one or two leaves, or an
-// S2 / S3 subtree -- branch-free over its kind: with P = {a, b} (its first cherry, or its
-// leaves) and Q = {c, d} (the rest; empty but for S2 / S3), the set is P & Q where they meet,
-// else P | Q (src/fitchSankoff.cpp:39-55 on the cherries), which is subtree_set_ap's.
-__device__ __forceinline__ void child_set_leafy(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
-    const bool virt = c >= 0;
-    const uint32_t mb = virt && __builtin_amdgcn_readfirstlane(vl.y) >= 0 ? ~0u : 0u;
-    const uint32_t mc = virt && __builtin_amdgcn_readfirstlane(vl.z) >= 0 ? ~0u : 0u;
-    const uint32_t md = virt && __builtin_amdgcn_readfirstlane(vl.w) >= 0 ? ~0u : 0u;
-    const uint4 A = f.code, B = f.v[0], C = f.v[1], D = f.v[2];
-    vd |= (mb & code_ne(A, B)) | (mc & code_ne(A, C)) | (md & code_ne(A, D));
-    const uint32_t nz = (mc & (~code_ne(A, C) | (mb & ~code_ne(B, C)))) | (md & (~code_ne(A, D) | (mb & ~code_ne(B, D))));
-    const LoHi ta = lohi_of(A.x, A.y, A.z, A.w, ~0u), tb = lohi_of(B.x, B.y, B.z, B.w, mb);
-    const LoHi tc = lohi_of(C.x, C.y, C.z, C.w, mc), td = lohi_of(D.x, D.y, D.z, D.w, md);
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        const uint32_t p = (ta.lo[v & 3] & ta.hi[v >> 2]) | (tb.lo[v & 3] & tb.hi[v >> 2]);
-        const uint32_t q = (tc.lo[v & 3] & tc.hi[v >> 2]) | (td.lo[v & 3] & td.hi[v >> 2]);
-        x[v] = (p & q) | ((p | q) & ~nz);
-    }
-}
-
-// Any child of a subtree-form node (leaf, leaf-parent, S2 / S3, or record), branch-free:
-// child_set_leafy's formula over its leaf codes (a record's code planes as the one leaf),
-// then a record's complex lanes take their stored planes.
-__device__ __forceinline__ void child_set_any(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
-    const bool virt = c >= 0 && (c & kVirtualBit);
-    const bool rec_cx = c >= 0 && !(c & kVirtualBit) && f.cx;
-    const uint32_t mb = virt && __builtin_amdgcn_readfirstlane(vl.y) >= 0 ? ~0u : 0u;
-    const uint32_t mc = virt && __builtin_amdgcn_readfirstlane(vl.z) >= 0 ? ~0u : 0u;
-    const uint32_t md = virt && __builtin_amdgcn_readfirstlane(vl.w) >= 0 ? ~0u : 0u;
-    const uint4 A = f.code, B = f.v[0], C = f.v[1], D = f.v[2];
-    vd |= (mb & code_ne(A, B)) | (mc & code_ne(A, C)) | (md & code_ne(A, D));
-    const uint32_t nz = (mc & (~code_ne(A, C) | (mb & ~code_ne(B, C)))) | (md & (~code_ne(A, D) | (mb & ~code_ne(B, D))));
-    const LoHi ta = lohi_of(A.x, A.y, A.z, A.w, ~0u), tb = lohi_of(B.x, B.y, B.z, B.w, mb);
-    const LoHi tc = lohi_of(C.x, C.y, C.z, C.w, mc), td = lohi_of(D.x, D.y, D.z, D.w, md);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t w[4] = {f.v[q].x, f.v[q].y, f.v[q].z, f.v[q].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int v = 4 * q + k;
-            const uint32_t p = (ta.lo[v & 3] & ta.hi[v >> 2]) | (tb.lo[v & 3] & tb.hi[v >> 2]);
-            const uint32_t r = (tc.lo[v & 3] & tc.hi[v >> 2]) | (td.lo[v & 3] & td.hi[v >> 2]);
-            x[v] = rec_cx ? w[k] : (p & r) | ((p | r) & ~nz);
-        }
-    }
-}
-
-// A fetched child's 16-plane set (Fitch) / optimal set Z0 (Sankoff), branch-free (round 4: the
-// per-kind branches' join copies held both the computed and the loaded planes -- 117 VGPRs in
-// the subtree form's level kernel, 92 now; the grouped kernels stopped spilling).
-template <bool SUB = false>
-__device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
-    if constexpr (SUB) child_set_any(c, vl, f, x, vd);
-    else child_set_plain(c, vl, f, x, vd);
 }
 
 template <bool SUB = false>
