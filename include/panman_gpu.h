@@ -106,7 +106,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *   PM_OPT_SUB_DOWN (default 0): Fitch, subtree form -- a three- or four-leaf subtree's
  *                  finals and records come from its parent's pre-order wave instead of a
  *                  wave of their own after the levels.
- *   PM_OPT_PLAIN_UP (default 1): Fitch, grouped subtree form -- a post-order launch's binary
+ *   PM_OPT_PLAIN_UP (default 1): Fitch / Sankoff, grouped subtree form -- a post-order launch's binary
  *                  nodes with no three- / four-leaf subtree child and nothing recomputed run in
  *                  a lean kernel (fewer registers, more waves in flight) before the rest.
  *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the

@@ -217,7 +217,7 @@ struct pm_ctx {
     int32_t group_levels = 4;         // ... and up to this many levels (PM_OPT_GROUP_LEVELS)
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
     bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
-    bool plain_up = true;             // Fitch grouped subtree form: plain nodes in the lean post-order kernel (PM_OPT_PLAIN_UP)
+    bool plain_up = true;             // grouped subtree form: plain nodes in the lean post-order kernels (PM_OPT_PLAIN_UP)
 
     // column shard
     int64_t num_sites = 0;

@@ -61,7 +61,9 @@ __device__ __forceinline__ void count_child(uint32_t (&cnt)[16][B], uint32_t& fi
 // their children's Z0 -- recomputed in registers (fold_first_two) instead of loaded; the
 // first two children's counts then follow from their AND (count 2) and OR (count >= 1).
 // gi: the node's index in the descriptor array; SUB: up slots (UpArgs::upm), as fitch_up_node.
-template <int B, bool AP, bool SUB = false, bool GROUP = false>
+// PLAIN: the grouped order's plain prefix (binary, no S2 / S3 child, nothing recomputed; see
+// fitch_up_node): branch-free child sets, no polytomy loop -- fewer registers, more waves.
+template <int B, bool AP, bool SUB = false, bool GROUP = false, bool PLAIN = false>
 __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc& d, int32_t gi, int tile, int lane) {
     const int32_t n = d.node;
     const int64_t word = (int64_t)tile * kWave + lane;
@@ -98,18 +100,20 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
         if (e1 - e0 > 1) fetch_child_ap<kSankoffRec, false, SUB, SUB>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t vd = 0;
-        child_set_ap<SUB>(d.c0, vl0, f0, z, vd);
-        if (SUB && kid_shape(d.c0)) sd |= vd;
+        if constexpr (PLAIN) child_set_plain(d.c0, vl0, f0, z, vd);
+        else child_set_ap<SUB>(d.c0, vl0, f0, z, vd);
+        if (SUB && !PLAIN && kid_shape(d.c0)) sd |= vd;
         count_child<B>(cnt, finite, z);
         if (e1 - e0 > 1) {
             vd = 0;
-            child_set_ap<SUB>(d.c1, vl1, f1, z, vd);
-            if (SUB && kid_shape(d.c1)) sd |= vd;
+            if constexpr (PLAIN) child_set_plain(d.c1, vl1, f1, z, vd);
+            else child_set_ap<SUB>(d.c1, vl1, f1, z, vd);
+            if (SUB && !PLAIN && kid_shape(d.c1)) sd |= vd;
             count_child<B>(cnt, finite, z);
         }
         first = e0 + 2;
     }
-    for (int32_t e = first; e < e1; ++e) {   // one or two leaves: Z0 = their codes (:376-402)
+    for (int32_t e = first; !PLAIN && e < e1; ++e) {   // one or two leaves: Z0 = their codes (:376-402)
         const int32_t c = e == e0 ? d.c0 : (e == e0 + 1 ? d.c1 : __builtin_amdgcn_readfirstlane(a.child_enc[e]));
         const int4 vl = !(c >= 0 && (c & kVirtualBit)) ? make_int4(-1, -1, -1, -1)
                         : e == e0                       ? make_int4(d.vl0[0], d.vl0[1], -1, -1)
@@ -160,18 +164,21 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
 #ifndef PM_SK_UP_WAVES
 #define PM_SK_UP_WAVES 1
 #endif
+#ifndef PM_SK_PLAIN_UP_WAVES
+#define PM_SK_PLAIN_UP_WAVES 7
+#endif
 // GROUP: 4 waves per SIMD (3: no scratch spills, C3 Sankoff 2-3 % slower; see PM_GROUP_UP_WAVES)
 #ifndef PM_SK_GROUP_UP_WAVES
 #define PM_SK_GROUP_UP_WAVES 4
 #endif
-template <int B, bool AP, bool SUB = false, bool GROUP = false>
-__global__ __launch_bounds__(kBlock, GROUP ? PM_SK_GROUP_UP_WAVES : PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
+template <int B, bool AP, bool SUB = false, bool GROUP = false, bool PLAIN = false>
+__global__ __launch_bounds__(kBlock, PLAIN ? PM_SK_PLAIN_UP_WAVES : GROUP ? PM_SK_GROUP_UP_WAVES : PM_SK_UP_WAVES) void k_sankoff_up(UpArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int32_t item;
     int tile;
     wave_item(wave, a.tiles, item, tile);
     if (item >= a.count) return;
-    sankoff_up_node<B, AP, SUB, GROUP>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
+    sankoff_up_node<B, AP, SUB, GROUP, PLAIN>(a, a.desc[item], (int32_t)(a.desc - a.desc_all) + item, tile, lane);
 }
 
 // Wide nodes (out-degree > 3): one workgroup per (node, tile), children dealt round-robin
@@ -571,8 +578,18 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             const int32_t e = class_off[h * kDegreeClasses + k + 1];
             if (e == b) continue;
             hipStream_t s = fork && k > 0 ? c->side : c->stream;
-            up.desc = up_desc + b;
-            up.count = e - b;
+            // the grouped order's plain prefix of the narrow class: the lean kernel first
+            const int32_t np = k == 0 && grp && c->plain_up ? std::min(ht.up_plain_gs[h], e - b) : 0;
+            if (np > 0) {
+                up.desc = up_desc + b;
+                up.count = np;
+                timer_begin(c, 0);
+                hipLaunchKernelGGL((k_sankoff_up<2, true, true, false, true>), wave_grid(np, tiles), dim3(kBlock), 0, s, up);
+                timer_end(c, 0);
+                if (np == e - b) continue;
+            }
+            up.desc = up_desc + b + np;
+            up.count = e - b - np;
             const dim3 grid = wave_grid(up.count, tiles), wide = block_grid(up.count, tiles);
             timer_begin(c, 0);
             if (k == 0 && grp && ht.up_recomp_gs[h]) hipLaunchKernelGGL((k_sankoff_up<2, true, true, true>), grid, dim3(kBlock), 0, s, up);

@@ -120,9 +120,11 @@ def test_up_groups_equal_heights(engine, narrow, tree, mode):
 
 @pytest.mark.parametrize("narrow", [0, 16])
 @pytest.mark.parametrize("tree", ["sars-like", "random-join", "polytomy"])
-def test_plain_up_equals_general_kernel(engine, narrow, tree):
+@pytest.mark.parametrize("mode", [panman_amd.MODE_FITCH, panman_amd.MODE_SANKOFF])
+def test_plain_up_equals_general_kernel(engine, narrow, tree, mode):
     """PM_OPT_PLAIN_UP: the grouped post-order's plain prefix (binary, no S2 / S3 child,
-    nothing recomputed) in the lean kernel gives the general kernel's records."""
+    nothing recomputed) in the lean kernel gives the general kernel's records (Fitch and
+    Sankoff)."""
     if tree == "sars-like":
         off, idx, root = panman_amd.sars_like_tree(6000, seed=41)
     elif tree == "random-join":
@@ -136,7 +138,7 @@ def test_plain_up_equals_general_kernel(engine, narrow, tree):
     try:
         for on in (False, True):
             engine.set_plain_up(on)
-            res.append(_run(engine, 32768, narrow))
+            res.append(_run(engine, 32768, narrow, mode=mode))
     finally:
         engine.set_plain_up(True)
         engine.set_narrow(16)
