@@ -553,7 +553,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             const bool leafy = grp ? ht.up_leafy_g[h] : sub ? ht.up_leafy_k[h] : virt && ht.up_leafy_v[h];
             // the grouped order's plain prefix (binary, no S2 / S3 child, nothing recomputed):
             // the lean kernel, then the rest of the class
-            const int32_t np = grp && !leafy && c->plain_up ? std::min(ht.up_plain_g[h], m - b) : 0;
+            int32_t np = grp && !leafy && c->plain_up ? std::min(ht.up_plain_g[h], m - b) : 0;
+            if ((int64_t)np * tiles < kPlainMinWaves) np = 0;
             timer_begin(c, 0);
             if (np > 0) {
                 up.desc = up_desc + b;

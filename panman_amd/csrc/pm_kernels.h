@@ -68,6 +68,14 @@ constexpr int64_t kMixedMaxWaves = PM_MIXED_MAX_WAVES;
 #define PM_BAND_WAVES 16
 #endif
 constexpr int kBandWaves = PM_BAND_WAVES;
+// Plain post-order prefixes (PM_OPT_PLAIN_UP) get a launch of their own only from this many
+// (node, tile) waves: the lean kernel's higher occupancy pays on levels that fill the chip
+// many times over, a second dependent launch costs more on smaller ones (C3 with a split at
+// every level: +0.2 ms).
+#ifndef PM_PLAIN_MIN_WAVES
+#define PM_PLAIN_MIN_WAVES 65536
+#endif
+constexpr int64_t kPlainMinWaves = PM_PLAIN_MIN_WAVES;
 constexpr int kBandBlock = kBandWaves * kWave;
 
 struct UpArgs {

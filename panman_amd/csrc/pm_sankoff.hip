@@ -579,7 +579,8 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             if (e == b) continue;
             hipStream_t s = fork && k > 0 ? c->side : c->stream;
             // the grouped order's plain prefix of the narrow class: the lean kernel first
-            const int32_t np = k == 0 && grp && c->plain_up ? std::min(ht.up_plain_gs[h], e - b) : 0;
+            int32_t np = k == 0 && grp && c->plain_up ? std::min(ht.up_plain_gs[h], e - b) : 0;
+            if ((int64_t)np * tiles < kPlainMinWaves) np = 0;
             if (np > 0) {
                 up.desc = up_desc + b;
                 up.count = np;
