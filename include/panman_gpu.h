@@ -108,7 +108,9 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  wave of their own after the levels.
  *   PM_OPT_PLAIN_UP (default 1): Fitch / Sankoff, grouped subtree form -- a post-order launch's binary
  *                  nodes with no three- / four-leaf subtree child and nothing recomputed run in
- *                  a lean kernel (fewer registers, more waves in flight) before the rest.
+ *                  a lean kernel (fewer registers, more waves in flight) before the rest, when
+ *                  they are at least 65536 (node, tile) waves; a value >= 2 sets that threshold;
+ *                  0 = off.
  *   PM_OPT_RECORD_CAP: the record buffer's capacity per shard (1024 shards), replacing the
  *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
  *                  re-run with a larger buffer when its results are read (pm_mutation_count,

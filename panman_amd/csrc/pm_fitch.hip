@@ -554,7 +554,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
             // the grouped order's plain prefix (binary, no S2 / S3 child, nothing recomputed):
             // the lean kernel, then the rest of the class
             int32_t np = grp && !leafy && c->plain_up ? std::min(ht.up_plain_g[h], m - b) : 0;
-            if ((int64_t)np * tiles < kPlainMinWaves) np = 0;
+            if ((int64_t)np * tiles < (c->plain_min_waves > 0 ? c->plain_min_waves : kPlainMinWaves)) np = 0;
             timer_begin(c, 0);
             if (np > 0) {
                 up.desc = up_desc + b;

@@ -220,7 +220,8 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
                               (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
-                              (uint64_t)c->sub_down, (uint64_t)c->plain_up, (uint64_t)(uintptr_t)c->upm,
+                              (uint64_t)c->sub_down, (uint64_t)c->plain_up, (uint64_t)c->plain_min_waves,
+                              (uint64_t)(uintptr_t)c->upm,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
                               (uint64_t)c->shard_cap, (uint64_t)(uintptr_t)c->recs, (uint64_t)(uintptr_t)c->sets,
@@ -467,8 +468,10 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->up_group = value != 0;
         return PM_OK;
     }
-    if (option == PM_OPT_PLAIN_UP) {
+    if (option == PM_OPT_PLAIN_UP) {   // 0 off, 1 on (default threshold), >= 2: on from that many waves
+        if (value < 0) return fail(c, PM_ERR_ARG, "PM_OPT_PLAIN_UP: 0, 1 or a wave threshold >= 2");
         c->plain_up = value != 0;
+        c->plain_min_waves = value >= 2 ? value : 0;
         return PM_OK;
     }
     if (option == PM_OPT_SUB_DOWN) {

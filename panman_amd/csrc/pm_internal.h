@@ -218,6 +218,7 @@ struct pm_ctx {
     bool up_group = true;             // Fitch subtree form: grouped post-order launches (PM_OPT_UP_GROUP)
     bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
     bool plain_up = true;             // grouped subtree form: plain nodes in the lean post-order kernels (PM_OPT_PLAIN_UP)
+    int64_t plain_min_waves = 0;      // ... from this many (node, tile) waves (0: kPlainMinWaves)
 
     // column shard
     int64_t num_sites = 0;

@@ -580,7 +580,7 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
             hipStream_t s = fork && k > 0 ? c->side : c->stream;
             // the grouped order's plain prefix of the narrow class: the lean kernel first
             int32_t np = k == 0 && grp && c->plain_up ? std::min(ht.up_plain_gs[h], e - b) : 0;
-            if ((int64_t)np * tiles < kPlainMinWaves) np = 0;
+            if ((int64_t)np * tiles < (c->plain_min_waves > 0 ? c->plain_min_waves : kPlainMinWaves)) np = 0;
             if (np > 0) {
                 up.desc = up_desc + b;
                 up.count = np;

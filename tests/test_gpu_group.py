@@ -137,7 +137,7 @@ def test_plain_up_equals_general_kernel(engine, narrow, tree, mode):
     res = []
     try:
         for on in (False, True):
-            engine.set_plain_up(on)
+            engine.set_plain_up(on, min_waves=2)   # (every plain prefix split off, small trees too)
             res.append(_run(engine, 32768, narrow, mode=mode))
     finally:
         engine.set_plain_up(True)
