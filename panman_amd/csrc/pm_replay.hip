@@ -305,6 +305,26 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
 #ifndef PM_REPLAY_PIPED_WAVES
 #define PM_REPLAY_PIPED_WAVES 6
 #endif
+// PM_REPLAY_DB: two LDS tile buffers -- tile t + 1's consensus copy-in is issued as tile t's
+// edits start, so it lands behind them instead of heading tile t + 1's critical path.
+#ifndef PM_REPLAY_DB
+#define PM_REPLAY_DB 1
+#endif
+constexpr int kReplayBufs = PM_REPLAY_DB ? 2 : 1;
+
+// LDS-DMA copy-in of the consensus tile t (1 KiB per wave-instruction, all in flight).
+__device__ __forceinline__ void tile_copy_in(const ReplayDev& d, int32_t t, uint4* dst, int wave, int lane) {
+    const int64_t c0 = (int64_t)t * kReplayTile;
+    const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
+    const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
+    for (int64_t b = (int64_t)wave * kWave; b < n / 16; b += 4 * kWave) {
+        const int64_t k = b + lane;
+        if (k < n / 16)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                             (__attribute__((address_space(3))) void*)(dst + b), 16, 0, 0);
+    }
+}
+
 // Every path at most 64 nodes (launch_replay checks max_depth): all four waves edit.  Every
 // wave holds the path's slice bounds (lane = path node) and takes every fourth round of the
 // tile's edits (a super-round = 4 x kEditsPerLane x 64 edits; a C5 tile has ~800).  Edits
@@ -315,9 +335,8 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
 // written out, so a tile's edits cost LDS writes, not a chain of memory round trips in one
 // wave (the single-editor kernel above: ~10 us per 16 KiB tile at C5).
 __global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(ReplayDev d) {
-    __shared__ uint4 tile_buf[kReplayTile / 16];
+    __shared__ uint4 tile_buf[kReplayBufs][kReplayTile / 16];
     __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
-    char* buf = reinterpret_cast<char*>(tile_buf);
     const int32_t leaf = blockIdx.x;
     const int32_t t_begin = (int32_t)blockIdx.y * kReplayGroup;
     const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
@@ -339,18 +358,15 @@ __global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(Rep
         if (wave * R < ch.total) edit_round(d, ch, wave * R, (int64_t)t_begin * kReplayTile, lane, r);
     }
     if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
+    if (kReplayBufs == 2) tile_copy_in(d, t_begin, tile_buf[0], wave, lane);
     for (int32_t t = t_begin; t < t_end; ++t) {
         const int64_t c0 = (int64_t)t * kReplayTile;
         const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
-        const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
-        // LDS-DMA copy-in of the consensus tile (1 KiB per wave-instruction, all in flight)
-        for (int64_t b = (int64_t)wave * kWave; b < n / 16; b += 4 * kWave) {
-            const int64_t k = b + lane;
-            if (k < n / 16)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
-                                                 (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0, 0);
-        }
-        __syncthreads();
+        uint4* cur = tile_buf[kReplayBufs == 2 ? (t - t_begin) & 1 : 0];
+        char* buf = reinterpret_cast<char*>(cur);
+        if (kReplayBufs == 1) tile_copy_in(d, t, cur, wave, lane);
+        __syncthreads();   // tile t's copy-in landed; (two buffers) tile t - 1's write-out read its buffer
+        if (kReplayBufs == 2 && t + 1 < t_end) tile_copy_in(d, t + 1, tile_buf[(t + 1 - t_begin) & 1], wave, lane);
         for (int32_t sr = 0; sr < ch.total; sr += 4 * R) {   // (uniform: every wave holds the same chunk)
             const int32_t base = sr + wave * R;
             if (sr > 0 && base < ch.total) edit_round(d, ch, base, c0, lane, r);   // (super-round 0: prefetched)
@@ -373,8 +389,8 @@ __global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(Rep
         if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
         __syncthreads();
         uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
-        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
-        __syncthreads();   // the tile buffer is refilled next
+        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = cur[k];
+        if (kReplayBufs == 1) __syncthreads();   // the tile buffer is refilled next
     }
 }
 
