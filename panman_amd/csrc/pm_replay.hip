@@ -306,9 +306,11 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev 
 #define PM_REPLAY_PIPED_WAVES 6
 #endif
 // PM_REPLAY_DB: two LDS tile buffers -- tile t + 1's consensus copy-in is issued as tile t's
-// edits start, so it lands behind them instead of heading tile t + 1's critical path.
+// edits start, so it lands behind them instead of heading tile t + 1's critical path.  Off:
+// the second 16 KiB buffer takes the kernel from 6 to 4 workgroups per CU (LDS), and C5 went
+// 1.75 -> 2.04 ms (r04i, interleaved).
 #ifndef PM_REPLAY_DB
-#define PM_REPLAY_DB 1
+#define PM_REPLAY_DB 0
 #endif
 constexpr int kReplayBufs = PM_REPLAY_DB ? 2 : 1;
 

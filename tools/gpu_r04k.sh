@@ -1,12 +1,12 @@
 #!/bin/bash
-# The round's Sankoff / C3 / C2 / replay evidence, then plain and C3 A/Bs
+# The round's evidence on the final build: N* Fitch and Sankoff profiles (stats + FETCH / WRITE /
+# SQ), C3 / C3 Sankoff / C2 traces, replay PMC
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+bash tools/profile_fitch.sh r04 || exit 2
 bash tools/profile_fitch.sh r04_sankoff --mode sankoff || exit 3
 bash tools/trace_stats.sh r04_c3 --tree sars-like --leaves 100000 --steps 5 --warmup 2 || exit 4
 bash tools/trace_stats.sh r04_c3_sankoff --tree sars-like --leaves 100000 --mode sankoff --steps 5 --warmup 2 || exit 5
 bash tools/trace_stats.sh r04_c2 --leaves 4096 --sites 15000 --steps 10 --warmup 3 || exit 6
 bash tools/profile_replay.sh r04 || exit 7
-bash tools/ab_args.sh 1 "--plain-up 0" "--plain-up 1" || exit 8
-BENCH_ARGS="--tree sars-like --leaves 100000" bash tools/ab_variants.sh fitch 1 default noslots || exit 9
