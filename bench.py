@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
     p.add_argument("--replay-leaves", type=int, default=1000)
+    p.add_argument("--replay-tree", choices=["random-join", "sars-like"], default="random-join",
+                   help="C5 replay tree: T1 random-join (paths <= ~30 nodes) or T2 sars-like (deep paths, "
+                        "several 64-node edit chunks per tile)")
     p.add_argument("--replay-blocks", type=int, default=500)
     p.add_argument("--replay-block-len", type=int, default=10_000)
     p.add_argument("--cpu-leaves", type=int, default=128, help="leaves replayed on the CPU baseline (~10 s)")
@@ -208,9 +211,7 @@ def main():
             "data": f"synthetic (seeded on-device tree-evolved columns, {args.tree} tree)",
             "build_id": panman_amd.build_id(),
             "config": {
-                "workload": (f"N* {args.mode}: {L} leaves x {S} sites random-join tree (C4 weak scaling at N>1)"
-                             if args.tree == "random-join" else
-                             f"{args.mode}: {L} leaves x {S} sites sars-like tree (T2; C3 at 100k leaves)"),
+                "workload": workload_label(args.mode, args.tree, L, S, world),
                 "tree": args.tree,
                 "leaves": L, "nodes": n_nodes, "sites": S, "sites_per_gpu": s_local,
                 "parallelism": f"column shards x{world}, one all-gather of per-site score/root",
@@ -239,6 +240,25 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def workload_label(mode: str, tree: str, L: int, S: int, world: int) -> str:
+    """Which BASELINE.json config a run measures (SURVEY.md §8d names): N* (1M x 30k, one
+    GPU), C4 (N x 1M leaves x 30k sites over N GPUs) and its one-rank share (8M x 3750), C3
+    (T2 100k x 30k), C2 (RSV-like ~4k x 15k); anything else is labelled by its shape only."""
+    shape = f"{L} leaves x {S} sites {tree} tree"
+    if tree == "random-join":
+        if world == 1 and (L, S) == (1_000_000, 30_000):
+            return f"N* {mode}: {shape} (one MI355X, north-star size)"
+        if world > 1 and L == world * 1_000_000 and S == 30_000:
+            return f"C4 {mode} weak scaling: {shape}, columns over {world} GPUs"
+        if world == 1 and (L, S) == (8_000_000, 3_750):
+            return f"C4 rank share {mode}: {shape} (one rank of --gpus 8)"
+        if world == 1 and L <= 5_000 and S == 15_000:
+            return f"C2 {mode}: {shape} (RSV-like size)"
+    elif world == 1 and (L, S) == (100_000, 30_000):
+        return f"C3 {mode}: {shape} (T2, SARS-like)"
+    return f"{mode}: {shape} (not a BASELINE config size)"
 
 
 def parsimony_block(args, eng, mode, ctx):
@@ -307,7 +327,7 @@ def parsimony_block(args, eng, mode, ctx):
     return {"metric": f"Fitch-Sankoff site*node updates/sec ({name} mode)", "value": value,
             "unit": "site*node updates/s", "ms_per_step": ms_step, "mutations_total": muts_total,
             "roofline": roofline,
-            "config": {"workload": f"{name}: {L} leaves x {S} sites ({args.tree} tree)", "sites_per_gpu": s_local}}
+            "config": {"workload": workload_label(name, args.tree, L, S, world), "sites_per_gpu": s_local}}
 
 
 def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
@@ -716,7 +736,11 @@ def replay_block(args, world, rank, local):
     # weak scaling over leaves: N x replay-leaves leaves, rank r replays
     # its contiguous share; tree and mutations are replicated, no collective
     total_leaves = args.replay_leaves * world
-    pm = c5_panmat(leaves=total_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len)
+    tree = None
+    if args.replay_tree == "sars-like":
+        from panman_amd.engine import sars_like_tree
+        tree = sars_like_tree(total_leaves, seed=1)
+    pm = c5_panmat(leaves=total_leaves, blocks=args.replay_blocks, mean_len=args.replay_block_len, tree=tree)
     off = pm.child_offsets
     leaf_nodes = [i for i in range(pm.num_nodes) if off[i] == off[i + 1]]
     lo, hi = shard_range(rank, world, len(leaf_nodes))
@@ -821,9 +845,9 @@ def replay_block(args, world, rank, local):
         "value": value, "unit": "leaf*column/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8 (ASCII IUPAC)",
-        "data": "synthetic C5-like PanMAT (seeded: random-join tree, blocks, gap slots, block and nuc mutations)",
+        "data": f"synthetic C5-like PanMAT (seeded: {args.replay_tree} tree, blocks, gap slots, block and nuc mutations)",
         "config": {"workload": f"C5 replay: {total_leaves} leaves x {cols} aligned columns, "
-                               f"{args.replay_blocks} blocks, {edits} edits",
+                               f"{args.replay_blocks} blocks, {edits} edits, {args.replay_tree} tree",
                    "leaves": total_leaves, "leaves_per_gpu": leaves, "columns": cols,
                    "path_mutation_records_rank0": path_recs,
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},

@@ -316,7 +316,13 @@ typedef struct pm_panmat {
  * record per leaf, ">name\n" + 70-column lines + "\n", leaves in node-id order (the
  * reference's order is TBB-scheduled).  `*text` is malloc'd (release with pm_free).
  * Replay runs on the GPU (consensus expansion + path mutations per leaf); block order,
- * strands, rotation, circular offset and line wrapping are applied by the host formatter. */
+ * strands, rotation, circular offset and line wrapping are applied by the host formatter.
+ * A nucleotide mutation's secondary block id is ignored (applied to its primary block), as
+ * printFASTAUltraFastHelper does (src/fasta.cpp:1838-1842).
+ * Memory: the replayed rows (leaves x columns bytes) and the text stay on the device in
+ * grow-only per-context buffers until pm_destroy, so the next pm_fasta on the context does not
+ * allocate again; a later large allocation on the context that fails releases them and
+ * retries once. */
 int pm_fasta(pm_ctx* ctx, const pm_panmat* panmat, int aligned, char** text, int64_t* length);
 /* pm_fasta over several devices: leaves split into contiguous ranges, one host thread and
  * context per entry of `devices` (entries may repeat), texts concatenated in leaf order --

@@ -135,7 +135,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
     c->words = (int32_t)((sites + 31) / 32);
     const int64_t wpad = wpad_of(c);
     hipError_t e;
-    if ((e = dev_alloc(&c->leaf_planes, (size_t)c->dt.num_leaves * wpad)) != hipSuccess ||
+    if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->leaf_planes), sizeof(uint4) * (size_t)c->dt.num_leaves * wpad)) != hipSuccess ||
         (e = dev_alloc(&c->leaf_flag, (size_t)c->dt.num_leaves)) != hipSuccess ||
         (e = dev_alloc(&c->cons, (size_t)std::max<int64_t>(wpad, 4 * kWave))) != hipSuccess ||   // cx_base reads 4 tiles
         (e = dev_alloc(&c->forced, (size_t)wpad)) != hipSuccess ||
@@ -160,13 +160,13 @@ int alloc_work(pm_ctx* c, int mode) {
     hipError_t e;
     if (need_sets > c->sets_bytes) {
         dev_free(c->sets);
-        if ((e = hipMalloc(reinterpret_cast<void**>(&c->sets), need_sets)) != hipSuccess)
+        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->sets), need_sets)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("state sets: ") + hipGetErrorString(e));
         c->sets_bytes = need_sets;
     }
     if (need_mask > c->cmask_bytes) {
         dev_free(c->cmask);
-        if ((e = hipMalloc(reinterpret_cast<void**>(&c->cmask), need_mask)) != hipSuccess)
+        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->cmask), need_mask)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("set masks: ") + hipGetErrorString(e));
         c->cmask_bytes = need_mask;
     }
@@ -177,7 +177,7 @@ int alloc_work(pm_ctx* c, int mode) {
         if (need > c->upm_bytes) {
             dev_free(c->upm);
             c->upm_bytes = 0;
-            if ((e = hipMalloc(reinterpret_cast<void**>(&c->upm), need)) != hipSuccess)
+            if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->upm), need)) != hipSuccess)
                 return fail(c, PM_ERR_OOM, std::string("up slots: ") + hipGetErrorString(e));
             c->upm_bytes = need;
         }
@@ -190,7 +190,7 @@ int alloc_work(pm_ctx* c, int mode) {
         const size_t need = parts * kPartPlanes * wpad * sizeof(uint32_t);
         if (need > c->sk_parts_bytes) {
             dev_free(c->sk_parts);
-            if ((e = hipMalloc(reinterpret_cast<void**>(&c->sk_parts), need)) != hipSuccess)
+            if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->sk_parts), need)) != hipSuccess)
                 return fail(c, PM_ERR_OOM, std::string("Sankoff part counters: ") + hipGetErrorString(e));
             c->sk_parts_bytes = need;
         }
@@ -201,7 +201,7 @@ int alloc_work(pm_ctx* c, int mode) {
         const double nodes = (double)c->dt.num_internal + c->dt.num_leaves;
         const double guess = std::max(65536.0, 0.01 * nodes * (double)c->num_sites);
         const int64_t cap = c->record_cap > 0 ? c->record_cap : (int64_t)(guess * 1.5 / kShards) + 256;
-        if ((e = dev_alloc(&c->recs, (size_t)cap * kShards)) != hipSuccess)
+        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->recs), sizeof(pm_mut) * (size_t)cap * kShards)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("mutation records: ") + hipGetErrorString(e));
         c->shard_cap = cap;
     }
@@ -286,7 +286,7 @@ int settle(pm_ctx* c, std::vector<uint32_t>& counts) {
         if ((int64_t)worst <= c->shard_cap) return PM_OK;
         dev_free(c->recs);
         const int64_t cap = (int64_t)worst + worst / 8 + 256;
-        if ((e = dev_alloc(&c->recs, (size_t)cap * kShards)) != hipSuccess)
+        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->recs), sizeof(pm_mut) * (size_t)cap * kShards)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("mutation records: ") + hipGetErrorString(e));
         c->shard_cap = cap;
         int rc = run_once(c, c->last_mode);
@@ -348,7 +348,7 @@ int build_sub_planes(pm_ctx* c) {
     if (need > c->sub_planes_bytes) {
         dev_free(c->sub_planes);
         c->sub_planes_bytes = 0;
-        if ((e = hipMalloc(reinterpret_cast<void**>(&c->sub_planes), need)) != hipSuccess)
+        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->sub_planes), need)) != hipSuccess)
             return fail(c, PM_ERR_OOM, std::string("subtree leaf layout: ") + hipGetErrorString(e));
         c->sub_planes_bytes = need;
     }

@@ -76,11 +76,16 @@ class Pool {
         for (auto& t : workers_) t.join();
     }
     int size() const { return (int)workers_.size() + 1; }
+    // One generation at a time: run() publishes (job, tasks) only when no worker is inside
+    // work(), and returns only when every task is done and every worker has left work(), so a
+    // worker never mixes one generation's job with another's counter.  Workers take their
+    // (job, tasks) snapshot under the lock.
     template <class F>
     void run(int tasks, F&& fn) {
         std::function<void(int)> f(std::forward<F>(fn));
         {
-            std::lock_guard<std::mutex> lock(mu_);
+            std::unique_lock<std::mutex> lock(mu_);
+            done_.wait(lock, [this]() { return active_ == 0; });
             job_ = &f;
             tasks_ = tasks;
             next_.store(0);
@@ -88,16 +93,16 @@ class Pool {
             ++gen_;
         }
         cv_.notify_all();
-        work();
+        work(&f, tasks);
         std::unique_lock<std::mutex> lock(mu_);
-        done_.wait(lock, [this]() { return pending_ == 0; });
+        done_.wait(lock, [this]() { return pending_ == 0 && active_ == 0; });
         job_ = nullptr;
     }
 
   private:
-    void work() {
-        for (int i = next_++; i < tasks_; i = next_++) {
-            (*job_)(i);
+    void work(std::function<void(int)>* job, int tasks) {
+        for (int i = next_++; i < tasks; i = next_++) {
+            (*job)(i);
             std::lock_guard<std::mutex> lock(mu_);
             if (--pending_ == 0) done_.notify_all();
         }
@@ -105,20 +110,28 @@ class Pool {
     void loop() {
         uint64_t seen = 0;
         for (;;) {
+            std::function<void(int)>* job = nullptr;
+            int tasks = 0;
             {
                 std::unique_lock<std::mutex> lock(mu_);
                 cv_.wait(lock, [&]() { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
+                if (!job_) continue;   // that generation has finished already
+                job = job_;
+                tasks = tasks_;
+                ++active_;
             }
-            work();
+            work(job, tasks);
+            std::lock_guard<std::mutex> lock(mu_);
+            if (--active_ == 0) done_.notify_all();
         }
     }
     std::vector<std::thread> workers_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
     std::function<void(int)>* job_ = nullptr;
-    int tasks_ = 0, pending_ = 0;
+    int tasks_ = 0, pending_ = 0, active_ = 0;
     std::atomic<int> next_{0};
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -212,6 +225,29 @@ void free_hostio(pm_ctx* c) {
     if (c->rows_buf) (void)hipFree(c->rows_buf);
     c->rows_buf = nullptr;
     c->rows_cap = 0;
+}
+
+// The FASTA text and replay rows stay on the device between calls (grow-only, up to ~10 GB at
+// C5).  A large allocation that fails drops them and tries once more, so a context that
+// replayed before still runs a pass that needs the room (the rows only when no replay state
+// refers to them).
+void release_cached(pm_ctx* c) {
+    if (c->text_buf) (void)hipFree(c->text_buf);
+    c->text_buf = nullptr;
+    c->text_cap = 0;
+    if (!c->replay && c->rows_buf) {
+        (void)hipFree(c->rows_buf);
+        c->rows_buf = nullptr;
+        c->rows_cap = 0;
+    }
+}
+
+hipError_t malloc_or_release(pm_ctx* c, void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 1));
+    if (e == hipSuccess || (!c->text_buf && (c->replay || !c->rows_buf))) return e;
+    (void)hipGetLastError();
+    release_cached(c);
+    return hipMalloc(p, std::max<size_t>(bytes, 1));
 }
 
 hipError_t grow_device(void** buf, size_t* cap, size_t need) {

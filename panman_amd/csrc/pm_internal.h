@@ -335,6 +335,9 @@ struct PhaseClock {
     double lap(const char* name);   // seconds since construction / the last lap, logged as `name`
 };
 int host_threads();   // host worker threads (PM_HOST_THREADS, else min(16, cores))
+// hipMalloc that, on failure, releases the context's cached text / rows buffers and retries
+hipError_t malloc_or_release(pm_ctx* c, void** p, size_t bytes);
+void release_cached(pm_ctx* c);
 void host_parallel_for(int tasks, const std::function<void(int)>& fn);
 // malloc with transparent huge pages requested for large blocks (released with free / pm_free)
 void* host_alloc_large(size_t n);

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -146,23 +147,37 @@ bool xz_blocks(const std::vector<uint8_t>& in, std::vector<XzBlock>& blocks) {
     const uint8_t* p = idx + 1;
     uint64_t count = 0;
     if (!vli_read(p, foot - 4, count) || count < 2 || count > (1u << 20)) return false;
-    size_t off = 12, out = 0;
+    // The index's sizes are attacker-controlled (its CRC is computable): every block must fit
+    // between the stream header and the index, and the declared output must stay below a cap
+    // (a generous multiple of the input; a legitimate stream beyond it still decodes, serially,
+    // into a buffer grown from the data itself).  Nothing here can wrap: sizes are checked
+    // against what remains before they are added.
+    const uint64_t idx_pos = (uint64_t)(idx - in.data());
+    const uint64_t out_cap = std::min<uint64_t>((uint64_t)n * 4096 + ((uint64_t)1 << 20), (uint64_t)1 << 42);
+    uint64_t off = 12, out = 0;
     for (uint64_t k = 0; k < count; ++k) {
         XzBlock b{};
         if (!vli_read(p, foot - 4, b.unpadded) || !vli_read(p, foot - 4, b.size) || b.unpadded < 5) return false;
-        b.offset = off;
-        b.out = out;
-        off += (size_t)((b.unpadded + 3) & ~(uint64_t)3);
-        out += (size_t)b.size;
+        const uint64_t padded = (b.unpadded + 3) & ~(uint64_t)3;   // (a VLI is < 2^63)
+        if (padded > idx_pos - off || b.size > out_cap - out) return false;
+        b.offset = (size_t)off;
+        b.out = (size_t)out;
+        off += padded;
+        out += b.size;
         blocks.push_back(b);
     }
-    return off == (size_t)(idx - in.data());   // one stream: the blocks end where the index starts
+    return off == idx_pos;   // one stream: the blocks end where the index starts
 }
 
 bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
     std::vector<XzBlock> blocks;
     if (!xz_blocks(in, blocks)) return xz_decode_serial(in, out, err);
-    out.resize(blocks.back().out + (size_t)blocks.back().size);
+    try {
+        out.resize(blocks.back().out + (size_t)blocks.back().size);
+    } catch (const std::bad_alloc&) {
+        out.clear();
+        return xz_decode_serial(in, out, err);
+    }
     std::vector<int> ok(blocks.size(), 0);
     host_parallel_for((int)blocks.size(), [&](int k) {
         const XzBlock& b = blocks[(size_t)k];
@@ -206,6 +221,7 @@ bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::s
     });
     for (int v : ok)
         if (!v) return xz_decode_serial(in, out, err);   // (a block that does not decode alone)
+    phase_add("panman.xz_parallel_blocks", (double)blocks.size());   // (a count, not seconds)
     return true;
 }
 
@@ -236,17 +252,22 @@ bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out,
 // reach -- a dictionary larger than the input (or than one block) finds nothing more, but
 // the level-9 encoder initialises all 64 MiB of it, which dominated writing a small PanMAN.
 // Messages above 256 KiB go through liblzma's multi-threaded encoder in independent blocks
-// (at least 256 KiB, at most one per host thread): still one standard .xz stream that any xz
-// decoder (the reference's boost lzma filter included) reads back to the same bytes.  PM_XZ_THREADS=1 forces one
-// block; PM_XZ_BLOCK sets the block size.
+// of a FIXED size (kXzBlock; the bytes written do not depend on the machine's core count):
+// still one standard .xz stream that any xz decoder (the reference's boost lzma filter
+// included) reads back to the same bytes.  PM_XZ_THREADS=1 forces one block (what the
+// reference writes); PM_XZ_BLOCK sets the block size; the thread count only sets how many
+// blocks are encoded at once.
+constexpr uint64_t kXzBlock = (uint64_t)1 << 20;
+
 bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string& err) {
     pm_lzma_stream s{};
-    int threads = host_threads();
-    if (const char* e = std::getenv("PM_XZ_THREADS")) threads = std::max(1, std::atoi(e));
-    uint64_t block = std::max<uint64_t>((uint64_t)256 << 10, (n + threads - 1) / std::max(threads, 1));
+    bool one_block = false;
+    if (const char* e = std::getenv("PM_XZ_THREADS")) one_block |= std::atoi(e) <= 1;
+    uint64_t block = kXzBlock;
     if (const char* e = std::getenv("PM_XZ_BLOCK")) block = std::max<uint64_t>(4096, std::strtoull(e, nullptr, 10));
-    threads = (int)std::min<uint64_t>((uint64_t)threads, (n + block - 1) / block);
-    const uint64_t reach = threads > 1 ? block : std::max<uint64_t>(n, 1);
+    if ((n + block - 1) / block <= 1) one_block = true;
+    const int threads = one_block ? 1 : (int)std::max<uint64_t>(2, std::min<uint64_t>((uint64_t)host_threads(), (n + block - 1) / block));
+    const uint64_t reach = one_block ? std::max<uint64_t>(n, 1) : block;
     uint32_t dict = 4096;
     while (dict < reach && dict < ((uint32_t)64 << 20)) dict <<= 1;
     alignas(16) unsigned char opt[512] = {0};   // lzma_options_lzma (opaque past dict_size)
@@ -254,7 +275,7 @@ bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::stri
     uint32_t* dict_size = reinterpret_cast<uint32_t*>(opt);
     *dict_size = std::min(*dict_size, dict);
     const pm_lzma_filter filters[2] = {{0x21 /* LZMA2 */, opt}, {UINT64_MAX, nullptr}};
-    if (threads > 1) {
+    if (!one_block) {
         pm_lzma_mt mt{};
         mt.threads = (uint32_t)threads;
         mt.block_size = block;

@@ -212,12 +212,8 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
                         __builtin_prefetch(p->nuc_mut_gap_position[k + 16] != -1 ? &gap_col[pid][ppos] : &main_col[pid][ppos]);
                 }
                 const int32_t id = p->nuc_mut_primary[k];
-                // secondary blocks (blockGaps, src/fasta.cpp:1230-1233) are never written by
-                // TreeGroup::writeToFile; refused rather than applied to the primary block
-                if (p->nuc_mut_secondary && p->nuc_mut_secondary[k] != -1) {
-                    bad(PM_ERR_UNSUPPORTED, "mutation on a secondary block (blockGaps)");
-                    break;
-                }
+                // the secondary block id is read and never used (src/fasta.cpp:1838-1842): a
+                // mutation on a secondary block lands on its primary block, as there
                 const uint32_t info = p->nuc_mut_info[k], type = info & 7u;
                 int32_t n = (int32_t)(info >> 4);
                 if (type > 5) continue;           // no-op types
@@ -298,7 +294,7 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
 
     // ---- edits that overwrite an ancestor's edit of the same column get kEditOverrides in
     // their character byte: the replay kernel writes the others in any order and only these
-    // in path order (k_replay_tile).  A depth-first walk with a count of the ancestors' edits
+    // in path order (k_replay_piped).  A depth-first walk with a count of the ancestors' edits
     // per column; the columns are split into ranges of tiles walked by host threads (each
     // node's edits of a range are one slice of its column-sorted list, tile_edit).
     {
@@ -454,6 +450,9 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
     clock.lap("replay.upload");
+    // (counts, not seconds: the deepest root->leaf path and its 64-node edit chunks per tile)
+    phase_add("replay.max_depth", (double)h.max_depth);
+    phase_add("replay.path_chunks", (double)((h.max_depth + kWave - 1) / kWave));
     ReplayDev& d = r.dev;
     d.leaves = L;
     d.row_stride = h.stride;

@@ -7,11 +7,12 @@
 // are present at the leaf (blockSequence, :1766-1787, :1842).
 //
 //   k_replay_piped  one workgroup per (leaf, 8 column tiles of 16 KiB): consensus tile -> LDS,
-//                   the path nodes' edits inside the tile applied root first by all waves
-//                   (edits of one node are unique per column and sorted by column on the
-//                   host, so a per-(node, tile) offset table bounds each node's slice),
-//                   absent blocks restored, one coalesced write of the tile: 1 B per
-//                   leaf-column to HBM, the replay roofline of SURVEY.md §8d.
+//                   the path nodes' edits inside the tile applied root first by all four
+//                   waves, 64 path nodes (one chunk) at a time (edits of one node are unique
+//                   per column and sorted by column on the host, so a per-(node, tile) offset
+//                   table bounds each node's slice), absent blocks restored, one coalesced
+//                   write of the tile: 1 B per leaf-column to HBM, the replay roofline of
+//                   SURVEY.md §8d.  Any depth: a SARS-like tree's 280-node paths are 5 chunks.
 #include "pm_bits.h"
 #include "pm_internal.h"
 
@@ -49,22 +50,6 @@ struct EditRound {
 };
 constexpr uint32_t kNoEdit = ~0u;
 
-__device__ __forceinline__ EditChunk edit_chunk(const ReplayDev& d, int64_t q, int64_t p1, int32_t t, int lane) {
-    EditChunk c;
-    c.cnt = (int)min((int64_t)kWave, p1 - q);
-    c.lo = 0;
-    c.len = 0;
-    if (lane < c.cnt) {
-        const int64_t* te = d.tile_edit + (size_t)d.path[q + lane] * (d.tiles + 1) + t;
-        c.lo = te[0];
-        c.len = (int32_t)(te[1] - c.lo);
-    }
-    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)c.len);
-    c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    c.excl = incl - c.len;
-    return c;
-}
-
 __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& c, int32_t base, int64_t c0, int lane,
                                            EditRound& r) {
     int64_t e[kEditsPerLane];
@@ -100,42 +85,8 @@ __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& 
     }
 }
 
-__device__ __forceinline__ void edit_write(const EditRound& r, char* buf, int64_t c0) {
-    const int lane = (int)threadIdx.x & (kWave - 1);
-    uint64_t pend[kEditsPerLane];
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < kEditsPerLane; ++j) {
-        const bool ok = r.node8[j] != kNoEdit;
-        const bool ovr = ok && (r.chr[j] & kEditOverrides);
-        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
-        pend[j] = __ballot(ovr);
-        any |= pend[j] != 0;
-    }
-    // the overriding edits after them, node by node in path order: the first pending edit
-    // (edits are in path order) names the next node
-    while (any) {
-        uint32_t k = 0;
-        bool found = false;
-#pragma unroll
-        for (int j = 0; j < kEditsPerLane; ++j)
-            if (!found && pend[j]) {
-                k = (uint32_t)__builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
-                found = true;
-            }
-        any = false;
-#pragma unroll
-        for (int j = 0; j < kEditsPerLane; ++j) {
-            const bool mine = ((pend[j] >> lane) & 1ull) && (r.node8[j] >> 8) == k;
-            if (mine) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
-            pend[j] &= ~__ballot(mine);
-            any |= pend[j] != 0;
-        }
-    }
-}
-
-// edit_write in two halves for the all-wave editor below: the round's edits that overwrite
-// no ancestor's edit (returns whether the round holds any overriding one, wave-uniform) ...
+// A round's edits in two halves: the ones that overwrite no ancestor's edit (returns whether
+// the round holds any overriding one, wave-uniform) ...
 __device__ __forceinline__ bool edit_write_plain(const EditRound& r, char* buf, int64_t c0) {
     bool any = false;
 #pragma unroll
@@ -148,7 +99,8 @@ __device__ __forceinline__ bool edit_write_plain(const EditRound& r, char* buf, 
     return any;
 }
 
-// ... and its overriding ones, node by node in path order (as edit_write)
+// ... and its overriding ones, node by node in path order: the first pending edit (edits are
+// in path order) names the next node
 __device__ __forceinline__ void edit_write_overrides(const EditRound& r, char* buf, int64_t c0) {
     const int lane = (int)threadIdx.x & (kWave - 1);
     uint64_t pend[kEditsPerLane];
@@ -174,21 +126,6 @@ __device__ __forceinline__ void edit_write_overrides(const EditRound& r, char* b
             if (mine) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
             pend[j] &= ~__ballot(mine);
             any |= pend[j] != 0;
-        }
-    }
-}
-
-// Any path (deep ones too): the edits of tile t, chunk by chunk, each round loaded then
-// written (no prefetch).
-__device__ __forceinline__ void apply_path_edits(const ReplayDev& d, char* buf, int32_t leaf, int32_t t, int64_t c0) {
-    const int lane = (int)threadIdx.x;
-    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
-    for (int64_t q = p0; q < p1; q += kWave) {
-        const EditChunk ch = edit_chunk(d, q, p1, t, lane);
-        for (int32_t base = 0; base < ch.total; base += kEditsPerLane * kWave) {
-            EditRound r;
-            edit_round(d, ch, base, c0, lane, r);
-            edit_write(r, buf, c0);
         }
     }
 }
@@ -256,51 +193,11 @@ __device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf,
     }
 }
 
-// One workgroup = (leaf, group of kReplayGroup column tiles), tile after tile: the tile of
-// the leaf's row is assembled in LDS -- consensus copy (all waves), the path nodes' edits
-// (wave 0, apply order above), blocks absent at the leaf restored (waves 1-3) -- and leaves
-// as one coalesced write; each row byte is written to HBM once.  This is the general form
-// (paths deeper than 64 nodes); k_replay_piped below is the one for every other tree.
+// Column tiles per workgroup (a workgroup = (leaf, kReplayGroup tiles), tile after tile).
 #ifndef PM_REPLAY_GROUP
 #define PM_REPLAY_GROUP 8
 #endif
-constexpr int kReplayGroup = PM_REPLAY_GROUP;   // column tiles per workgroup
-
-#ifndef PM_REPLAY_WAVES
-#define PM_REPLAY_WAVES 7
-#endif
-__global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay_tile(ReplayDev d) {
-    __shared__ uint4 tile_buf[kReplayTile / 16];
-    __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
-    char* buf = reinterpret_cast<char*>(tile_buf);
-    const int32_t leaf = blockIdx.x;
-    const int32_t t_begin = (int32_t)blockIdx.y * kReplayGroup;
-    const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
-    const int tid = (int)threadIdx.x;
-    const bool editor = tid < kWave;
-    if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
-    for (int32_t t = t_begin; t < t_end; ++t) {
-        const int64_t c0 = (int64_t)t * kReplayTile;
-        const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
-        const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
-        const int wv = tid >> 6;
-        for (int64_t b = (int64_t)wv * kWave; b < n / 16; b += 4 * kWave) {
-            const int64_t k = b + (tid & (kWave - 1));
-            if (k < n / 16)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
-                                                 (__attribute__((address_space(3))) void*)(tile_buf + b), 16, 0, 0);
-        }
-        __syncthreads();
-        if (editor) apply_path_edits(d, buf, leaf, t, c0);
-        __syncthreads();
-        if (!editor) restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid - kWave, blockDim.x - kWave);
-        __syncthreads();
-        if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
-        uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
-        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = tile_buf[k];
-        __syncthreads();   // the tile buffer is refilled next
-    }
-}
+constexpr int kReplayGroup = PM_REPLAY_GROUP;
 
 #ifndef PM_REPLAY_PIPED_WAVES
 #define PM_REPLAY_PIPED_WAVES 6
@@ -327,15 +224,52 @@ __device__ __forceinline__ void tile_copy_in(const ReplayDev& d, int32_t t, uint
     }
 }
 
-// Every path at most 64 nodes (launch_replay checks max_depth): all four waves edit.  Every
-// wave holds the path's slice bounds (lane = path node) and takes every fourth round of the
-// tile's edits (a super-round = 4 x kEditsPerLane x 64 edits; a C5 tile has ~800).  Edits
-// that overwrite no ancestor's edit touch distinct columns along the path, so the waves write
-// them in any order; the overriding ones (kEditOverrides, rare) follow wave by wave -- the
-// rounds are in path order -- with a barrier between, and only in a super-round that has
-// any.  Each wave prefetches its first round of the next tile while the tile is restored and
-// written out, so a tile's edits cost LDS writes, not a chain of memory round trips in one
-// wave (the single-editor kernel above: ~10 us per 16 KiB tile at C5).
+// One chunk's edits of a tile, all four waves: every wave holds the chunk's slice bounds
+// (lane = path node) and takes every fourth round (a super-round = 4 x kEditsPerLane x 64
+// edits; a C5 tile has ~800).  Edits that overwrite no ancestor's edit touch distinct columns
+// along the path, so the waves write them in any order; the overriding ones (kEditOverrides,
+// rare) follow wave by wave -- the rounds are in path order -- with a barrier between, and
+// only in a super-round that has any.  Every super-round ends in a barrier, so the next
+// chunk's (deeper nodes') overriding edits land after this chunk's writes.  `r` holds the
+// wave's first round, already issued.
+__device__ __forceinline__ void chunk_edits(const ReplayDev& d, const EditChunk& ch, EditRound& r, char* buf,
+                                            int64_t c0, int wave, int lane) {
+    constexpr int32_t R = kEditsPerLane * kWave;
+    for (int32_t sr = 0; sr < ch.total; sr += 4 * R) {   // (uniform: every wave holds the same chunk)
+        const int32_t base = sr + wave * R;
+        if (sr > 0 && base < ch.total) edit_round(d, ch, base, c0, lane, r);   // (super-round 0: prefetched)
+        const bool ovr = base < ch.total && edit_write_plain(r, buf, c0);
+        if (__syncthreads_or(ovr)) {
+            for (int w = 0; w < 4; ++w) {
+                if (wave == w && base < ch.total) edit_write_overrides(r, buf, c0);
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// Slice bounds of chunk [q, q + 64) of the path at tile t (lane = path node); the path ids
+// and the bounds are two dependent loads, issued for chunk k + 1 before chunk k's rounds.
+struct ChunkBounds {
+    int cnt;
+    int64_t lo, hi;
+};
+
+__device__ __forceinline__ ChunkBounds chunk_bounds(const ReplayDev& d, int64_t q, int64_t p1, int32_t t, int lane) {
+    ChunkBounds b{(int)min((int64_t)kWave, p1 - q), 0, 0};
+    if (lane < b.cnt) {
+        const int64_t* te = d.tile_edit + (size_t)d.path[q + lane] * (d.tiles + 1) + t;
+        b.lo = te[0];
+        b.hi = te[1];
+    }
+    return b;
+}
+
+// Each wave prefetches its first round of the next tile's first chunk while the tile is
+// restored and written out, so a tile's edits cost LDS writes, not a chain of memory round
+// trips in one wave (round 3's single-editor kernel: ~10 us per 16 KiB tile at C5).  Paths
+// deeper than 64 nodes walk their further chunks after the first, each chunk's bounds loaded
+// while the previous chunk's rounds run.
 __global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(ReplayDev d) {
     __shared__ uint4 tile_buf[kReplayBufs][kReplayTile / 16];
     __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
@@ -369,15 +303,16 @@ __global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(Rep
         if (kReplayBufs == 1) tile_copy_in(d, t, cur, wave, lane);
         __syncthreads();   // tile t's copy-in landed; (two buffers) tile t - 1's write-out read its buffer
         if (kReplayBufs == 2 && t + 1 < t_end) tile_copy_in(d, t + 1, tile_buf[(t + 1 - t_begin) & 1], wave, lane);
-        for (int32_t sr = 0; sr < ch.total; sr += 4 * R) {   // (uniform: every wave holds the same chunk)
-            const int32_t base = sr + wave * R;
-            if (sr > 0 && base < ch.total) edit_round(d, ch, base, c0, lane, r);   // (super-round 0: prefetched)
-            const bool ovr = base < ch.total && edit_write_plain(r, buf, c0);
-            if (__syncthreads_or(ovr)) {
-                for (int w = 0; w < 4; ++w) {
-                    if (wave == w && base < ch.total) edit_write_overrides(r, buf, c0);
-                    __syncthreads();
-                }
+        if (p1 - p0 <= kWave) {
+            chunk_edits(d, ch, r, buf, c0, wave, lane);
+        } else {
+            ChunkBounds nb = chunk_bounds(d, p0 + kWave, p1, t, lane);
+            chunk_edits(d, ch, r, buf, c0, wave, lane);
+            for (int64_t q = p0 + kWave; q < p1; q += kWave) {
+                const EditChunk cq = edit_chunk_from(nb.cnt, nb.lo, nb.hi, lane);
+                if (wave * R < cq.total) edit_round(d, cq, wave * R, c0, lane, r);
+                if (q + kWave < p1) nb = chunk_bounds(d, q + kWave, p1, t, lane);
+                chunk_edits(d, cq, r, buf, c0, wave, lane);
             }
         }
         restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid, blockDim.x);
@@ -545,10 +480,7 @@ hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;
     timer_begin(c, 3);
     const unsigned groups = (unsigned)((d.tiles + kReplayGroup - 1) / kReplayGroup);
-    if (d.max_depth <= kWave)
-        hipLaunchKernelGGL(k_replay_piped, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
-    else
-        hipLaunchKernelGGL(k_replay_tile, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
+    hipLaunchKernelGGL(k_replay_piped, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
     timer_end(c, 3);
     return hipGetLastError();
 }

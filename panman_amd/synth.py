@@ -19,11 +19,16 @@ def _pack_words(codes: np.ndarray) -> np.ndarray:
 
 
 def c5_panmat(leaves: int = 1000, blocks: int = 500, mean_len: int = 10_000, mu: float = 1e-3,
-              block_rate: float = 1e-2, gaps_per_block: int = 20, seed: int = 3) -> PanMAT:
+              block_rate: float = 1e-2, gaps_per_block: int = 20, seed: int = 3, tree=None) -> PanMAT:
+    """`tree` = (child_offsets, child_index, root) replaces the random-join tree (e.g. a deep
+    sars_like_tree or a caterpillar); `leaves` is then ignored."""
     rng = np.random.default_rng(seed)
-    off, idx, root = random_join_tree(leaves, seed=1)
-    n = 2 * leaves - 1
-    names = [f"s{i}" if i < leaves else f"node_{i}" for i in range(n)]
+    if tree is None:
+        off, idx, root = random_join_tree(leaves, seed=1)
+    else:
+        off, idx, root = (np.asarray(tree[0], np.int32), np.asarray(tree[1], np.int32), int(tree[2]))
+    n = off.shape[0] - 1
+    names = [f"s{i}" if off[i] == off[i + 1] else f"node_{i}" for i in range(n)]
     pm = PanMAT(names, off, idx, root)
     lens = rng.integers(mean_len // 2, mean_len * 3 // 2 + 1, size=blocks)
     seq_off = np.zeros(blocks + 1, np.int64)

@@ -50,15 +50,19 @@ def test_random_panmat_vs_oracle(engine, oracle, seed):
         assert got == want
 
 
-def test_secondary_block_mutation_is_refused(engine):
-    # a nucleotide mutation on a secondary block (blockGaps, which TreeGroup::writeToFile never
-    # writes) fails loudly instead of being applied to its primary block
-    rng = np.random.default_rng(11)
+@pytest.mark.parametrize("seed", range(3))
+def test_secondary_block_mutation_lands_on_primary(engine, oracle, seed):
+    """printFASTAUltraFastHelper reads a NucMut's secondaryBlockId and never uses it
+    (src/fasta.cpp:1838-1842): the mutation is applied to the primary block.  Same here, vs
+    the oracle's restatement of that loop."""
+    rng = np.random.default_rng(11 + seed)
     off, idx, root = random_tree(12, rng, max_children=3)
-    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2)
-    pm.add_nuc_mut(pm.leaves()[0], 0, 1, -1, 0, [2], secondary=0)
-    with pytest.raises(panman_amd.PanmanError, match="secondary block"):
-        engine.fasta(pm, True)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2, options=False)
+    for leaf in pm.leaves()[:4]:
+        pm.add_nuc_mut(leaf, 0, 1, -1, 0, [2], secondary=int(rng.integers(0, 3)))
+        pm.add_nuc_mut(leaf, 1, 0, -1, 3, [8], secondary=0)
+    for aligned in (True, False):
+        assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))
 
 
 def test_long_blocks_wrap_vs_oracle(engine, oracle):

@@ -1,0 +1,128 @@
+"""GPU parity for FASTA replay and reroot on DEEP trees (root->leaf paths longer than 64 nodes):
+the replay kernel walks such a path in 64-node chunks (pm_replay.hip, chunk_edits), with an
+overriding edit's order kept across chunks.  The reference: printFASTAUltraFastHelper applies
+each node's mutations root first along the path (src/fasta.cpp:1753-1764, 1789-1979), so the
+deepest edit of a column wins.  Every case also asserts, through the phase log, that the
+tree really is deeper than one chunk."""
+import numpy as np
+import pytest
+
+import panman_amd
+from _panmat import random_panmat, tree_dump
+from _trees import names_for, parse_newick, to_newick
+from panman_amd._lib import phase_report, phase_reset
+from panman_amd.engine import sars_like_tree
+from panman_amd.synth import c5_panmat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = panman_amd.Engine(0)
+    yield e
+    e.close()
+
+
+def _records(text):
+    return sorted(">" + r for r in text.split(">")[1:])
+
+
+def caterpillar(leaves: int):
+    """((((s0,s1),s2),s3)...): leaf k hangs off spine node k; depth = leaves - 1."""
+    n = 2 * leaves - 1
+    kids = {}
+    cur = 0
+    nxt = leaves
+    for k in range(1, leaves):
+        kids[nxt] = [cur, k]
+        cur = nxt
+        nxt += 1
+    off = np.zeros(n + 1, np.int32)
+    idx = []
+    for v in range(n):
+        idx += kids.get(v, [])
+        off[v + 1] = len(idx)
+    return off, np.array(idx, np.int32), cur
+
+
+def _fasta_checked(engine, pm, aligned, min_chunks=2):
+    phase_reset()
+    text = engine.fasta(pm, aligned)
+    ph = dict(phase_report())
+    assert ph["replay.max_depth"] > 64 and ph["replay.path_chunks"] >= min_chunks, ph
+    return text
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_caterpillar_200_vs_oracle(engine, oracle, aligned):
+    rng = np.random.default_rng(4242)
+    off, idx, root = caterpillar(200)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=6, block_len=(40, 300), mut_rate=0.03)
+    text = _fasta_checked(engine, pm, aligned, min_chunks=4)
+    assert _records(text) == _records(oracle.fasta(pm, aligned))
+
+
+def test_caterpillar_override_chain_across_chunks(engine, oracle):
+    """Every spine node rewrites the SAME columns (each edit overrides its ancestor's, 199
+    deep, crossing three chunk boundaries); every leaf must end with its deepest ancestor's
+    characters.  Also a second column set edited only by every 63rd / 64th / 65th node."""
+    off, idx, root = caterpillar(200)
+    names = names_for(off)
+    pm = random_panmat(np.random.default_rng(7), off, idx, root, names, blocks=3, block_len=(30, 60),
+                       mut_rate=0.0, block_rate=0.0, options=False)
+    n = len(names)
+    spine = [v for v in range(n) if off[v] != off[v + 1]]
+    for k, v in enumerate(spine):
+        code = [1, 2, 4, 8][k % 4]
+        pm.add_nuc_mut(v, 0, 3, -1, 0, [code, [2, 4, 8, 1][k % 4]])   # MNP of 2 over columns 3-4
+        if k % 63 == 0 or k % 64 == 0 or k % 65 == 0:
+            pm.add_nuc_mut(v, 1, 5, -1, 3, [[8, 4, 2, 1][k % 4]])
+    for v in range(200):                                              # leaves: some override again
+        if v % 3 == 0:
+            pm.add_nuc_mut(v, 0, 4, -1, 3, [15])
+    for aligned in (True, False):
+        text = _fasta_checked(engine, pm, aligned, min_chunks=4)
+        assert _records(text) == _records(oracle.fasta(pm, aligned))
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_sars_like_2000_c5_style_vs_oracle(engine, oracle, aligned):
+    """A C5-style PanMAT (blocks with gap slots, block insertions / deletions / inversions,
+    SNPs, MNPs, gap-slot insertions, overriding edits) on the deep T2 tree family."""
+    tree = sars_like_tree(2000, seed=3)
+    pm = c5_panmat(blocks=12, mean_len=2500, mu=2e-3, block_rate=2e-2, seed=21, tree=tree)
+    text = _fasta_checked(engine, pm, aligned)
+    assert _records(text) == _records(oracle.fasta(pm, aligned))
+
+
+def test_deep_multi_tile_many_edits_vs_oracle(engine, oracle):
+    """Many column tiles (> one 8-tile workgroup group) and dense edits on a 150-deep path:
+    more than one super-round per chunk and per tile."""
+    off, idx, root = caterpillar(150)
+    pm = c5_panmat(blocks=30, mean_len=6000, mu=4e-3, block_rate=1e-2, seed=8, tree=(off, idx, root))
+    text = _fasta_checked(engine, pm, True, min_chunks=3)
+    assert _records(text) == _records(oracle.fasta(pm, True))
+
+
+@pytest.mark.parametrize("which", ["caterpillar", "sars_like"])
+def test_reroot_deep_tree_vs_oracle(engine, oracle, which):
+    """Reroot (M4) reads every leaf's replayed row (R4): on a deep tree that is the chunked
+    replay; the dump must equal the oracle's restatement."""
+    rng = np.random.default_rng(55)
+    if which == "caterpillar":
+        off, idx, root = caterpillar(120)
+    else:
+        off, idx, root = sars_like_tree(800, seed=5)
+    names, off, idx, root = parse_newick(to_newick(off, idx, root, names_for(off)))
+    pm = random_panmat(rng, off, idx, root, names, blocks=4, block_len=(20, 120), mut_rate=0.02)
+    pm.branch_length = rng.integers(1, 50, size=len(names)).astype(np.float32) / 8
+    leaves = pm.leaves()
+    for leaf in (names[leaves[0]], names[leaves[len(leaves) // 2]]):
+        phase_reset()
+        f = engine.reroot(pm, leaf)
+        try:
+            assert dict(phase_report())["replay.max_depth"] > 64
+            assert tree_dump(f) == oracle.reroot(pm, leaf)
+        finally:
+            f.close()

@@ -150,7 +150,99 @@ def test_multi_block_xz_round_trip(tmp_path, monkeypatch, oracle):
     multi, single = (open(paths[k], "rb").read() for k in ("4", "1"))
     assert multi != single                                   # several blocks vs one
     assert lzma.decompress(multi) == lzma.decompress(single)
-    back = [PanmanFile(paths[k]).to_panmat(0) for k in ("4", "1")]
+    from panman_amd._lib import phase_report, phase_reset
+    back = []
+    for k in ("4", "1"):
+        phase_reset()
+        back.append(PanmanFile(paths[k]).to_panmat(0))
+        blocks = [v for name, v in phase_report() if name == "panman.xz_parallel_blocks"]
+        if k == "4":   # the re-wrapped one-block streams decoded on their own, none fell back
+            assert blocks and blocks[0] == multi_blocks(multi)
+        else:
+            assert not blocks
     want = parse_records(oracle.fasta(pm, True))
     for b in back:
         assert parse_records(oracle.fasta(b, True)) == want
+
+
+def _vli(b, i):
+    v, k = 0, 0
+    while True:
+        x = b[i]
+        i += 1
+        v |= (x & 0x7F) << (7 * k)
+        k += 1
+        if not x & 0x80:
+            return v, i
+
+
+def _vli_bytes(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _xz_index(data):
+    """(index offset, [(unpadded, uncompressed)]) of a one-stream .xz file."""
+    import struct
+    backward = (struct.unpack("<I", data[-8:-4])[0] + 1) * 4
+    at = len(data) - 12 - backward
+    assert data[at] == 0
+    n, i = _vli(data, at + 1)
+    recs = []
+    for _ in range(n):
+        u, i = _vli(data, i)
+        c, i = _vli(data, i)
+        recs.append((u, c))
+    return at, recs
+
+
+def multi_blocks(data):
+    return len(_xz_index(data)[1])
+
+
+def _with_index(data, recs):
+    """The stream with its index records replaced (index + footer CRCs recomputed)."""
+    import struct
+    import zlib
+    at, _ = _xz_index(data)
+    idx = bytearray(b"\x00") + _vli_bytes(len(recs))
+    for u, c in recs:
+        idx += _vli_bytes(u) + _vli_bytes(c)
+    while len(idx) % 4:
+        idx.append(0)
+    idx += struct.pack("<I", zlib.crc32(idx))
+    tail = struct.pack("<I", len(idx) // 4 - 1) + data[6:8]
+    foot = struct.pack("<I", zlib.crc32(tail)) + tail + b"YZ"
+    return data[:at] + bytes(idx) + foot
+
+
+@pytest.mark.parametrize("attack", ["wrap", "huge", "overrun"])
+def test_crafted_xz_index_is_rejected(tmp_path, monkeypatch, attack):
+    """Index sizes are attacker-controlled (the CRC is computable): sizes whose sums wrap 2^64,
+    a declared output far beyond the input, or a block running past the index must not reach
+    the block-parallel decoder -- the load fails cleanly (PM_ERR_ARG) instead."""
+    from panman_amd.synth import c5_panmat
+    from panman_amd._lib import PanmanError
+    monkeypatch.setenv("PM_XZ_THREADS", "4")
+    monkeypatch.setenv("PM_XZ_BLOCK", "32768")
+    good = str(tmp_path / "good.panman")
+    write_panman(good, [c5_panmat(leaves=20, blocks=20, mean_len=4000, seed=2)])
+    data = open(good, "rb").read()
+    _, recs = _xz_index(data)
+    assert len(recs) >= 3
+    big = (1 << 63) - 1
+    if attack == "wrap":       # out offsets wrap to a tiny total
+        recs = [(recs[0][0], big), (recs[1][0], big)] + [(u, 2) for u, _ in recs[2:]]
+    elif attack == "huge":
+        recs = [(recs[0][0], 1 << 50)] + recs[1:]
+    else:                      # first block claims the whole file
+        recs = [(len(data), recs[0][1])] + recs[1:]
+    bad = str(tmp_path / "bad.panman")
+    open(bad, "wb").write(_with_index(data, recs))
+    with pytest.raises(PanmanError) as e:
+        PanmanFile(bad)
+    assert "xz" in str(e.value)
