@@ -67,7 +67,7 @@ def parse():
                         "the tail (0); -1: library default")
     p.add_argument("--plain-up", type=int, default=-1,
                    help="Fitch: PM_OPT_PLAIN_UP, the grouped post-order's plain nodes in the lean kernel (1) or "
-                        "not (0); -1: library default")
+                        "not (0); >= 2: on for launches of at least that many waves; -1: library default")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -138,8 +138,8 @@ def main():
         eng.set_up_group(False)
     if args.sub_down >= 0:
         eng.set_sub_down(bool(args.sub_down))
-    if args.plain_up >= 0:
-        eng.set_plain_up(bool(args.plain_up))
+    if args.plain_up >= 0:   # 0 off, 1 on (library threshold), >= 2: on from that many waves
+        eng.set_plain_up(bool(args.plain_up), args.plain_up if args.plain_up >= 2 else 0)
     if args.group >= 0 or args.group_levels != 4:
         eng.set_group(args.group if args.group >= 0 else 32768, args.group_levels)
 

@@ -370,9 +370,12 @@ struct ReplayDev {
     const int64_t* blk_lo = nullptr;
     const int64_t* blk_hi = nullptr;
     const int32_t* tile_blk = nullptr;   // [tiles + 1]
-    // column tiles of kReplayTile bytes: per node, the first edit of each tile
+    // column tiles of kReplayTile bytes.  A node's edits are [plain | overriding] (an
+    // overriding edit rewrites a column an ancestor edits), each part column-sorted; per
+    // (node, tile) the first edit of each part in that tile
     int32_t tiles = 0;
-    const int64_t* tile_edit = nullptr;   // [N][tiles + 1]
+    const int2* tile2 = nullptr;   // [N][tiles + 1] {plain, overriding}
+    int32_t ring = 0;              // path nodes per leaf whose tile bounds a workgroup keeps in LDS
     const int64_t* path_off = nullptr;    // [leaves + 1] root-to-leaf node lists
     const int32_t* path = nullptr;
 };
@@ -381,6 +384,7 @@ struct ReplayDev {
 #endif
 constexpr int64_t kReplayTile = PM_REPLAY_TILE;   // leaf-row bytes assembled in LDS per workgroup
 constexpr uint8_t kEditOverrides = 0x80;   // edit_chr flag: an ancestor edits the same column
+constexpr int32_t kReplayRingMax = 512;     // ReplayDev::ring cap (deeper path nodes: bounds from HBM)
 
 // FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
 // segment per (leaf, print position) -- a block read forward or reverse-complemented from

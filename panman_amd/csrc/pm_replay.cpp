@@ -327,6 +327,46 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
             }
         });
     }
+    // ---- each node's slice as [plain edits | overriding edits], both column-sorted, and per
+    // (node, tile) the first edit of each part (int2 {plain, overriding}): the kernel writes a
+    // tile's plain edits in any order and resolves the overriding ones afterwards
+    // (k_replay: deepest on the path wins)
+    if (r.edits >= ((int64_t)1 << 31)) return fail_(PM_ERR_UNSUPPORTED, "more than 2^31 column edits");
+    std::vector<int2>& tile2 = h.tile2;
+    tile2.resize((size_t)N * (tiles + 1));
+    host_parallel_for((N + 15) / 16, [&](int task) {
+        std::vector<uint32_t> oc;
+        std::vector<uint8_t> oh;
+        for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
+            const int64_t b = eoff[v], e = eoff[v + 1];
+            oc.clear();
+            oh.clear();
+            int64_t w = b;
+            for (int64_t k = b; k < e; ++k) {
+                if (echr[k] & kEditOverrides) {
+                    oc.push_back(ecol[k]);
+                    oh.push_back(echr[k]);
+                } else {
+                    ecol[w] = ecol[k];
+                    echr[w] = echr[k];
+                    ++w;
+                }
+            }
+            const int64_t mid = w;
+            for (size_t k = 0; k < oc.size(); ++k, ++w) {
+                ecol[w] = oc[k];
+                echr[w] = oh[k];
+            }
+            int64_t ep = b, eo = mid;
+            for (int32_t t = 0; t <= tiles; ++t) {
+                const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
+                while (ep < mid && (int64_t)ecol[ep] < c0) ++ep;
+                while (eo < e && (int64_t)ecol[eo] < c0) ++eo;
+                tile2[(size_t)v * (tiles + 1) + t] = make_int2((int)ep, (int)eo);
+            }
+        }
+    });
+    std::vector<int64_t>().swap(tile_edit);
     clock.lap("replay.flat_overrides");
     // ---- per-leaf block state (getBlockSequence + the block-mutation pass of the helper)
     const int32_t L = (int32_t)r.leaves.size();
@@ -445,7 +485,7 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         (e = dput(&r.d_eoff, h.eoff, c->stream)) != hipSuccess || (e = dput(&r.d_ecol, h.ecol, c->stream)) != hipSuccess ||
         (e = dput(&r.d_echr, h.echr, c->stream)) != hipSuccess || (e = dput(&r.d_blk_lo, h.blk_lo, c->stream)) != hipSuccess ||
         (e = dput(&r.d_blk_hi, h.blk_hi, c->stream)) != hipSuccess || (e = dput(&r.d_tile_blk, h.tile_blk, c->stream)) != hipSuccess ||
-        (e = dput(&r.d_tile_edit, h.tile_edit, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_tile2, h.tile2, c->stream)) != hipSuccess ||
         (e = dput(&r.d_path_off, h.path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, h.path_all, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
@@ -472,7 +512,8 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     d.blk_hi = r.d_blk_hi;
     d.tile_blk = r.d_tile_blk;
     d.tiles = h.tiles;
-    d.tile_edit = r.d_tile_edit;
+    d.tile2 = r.d_tile2;
+    d.ring = std::min(std::max(kWave, (h.max_depth + kWave - 1) / kWave * kWave), kReplayRingMax);
     d.path_off = r.d_path_off;
     d.path = r.d_path;
     return PM_OK;
@@ -492,7 +533,7 @@ void free_replay(pm_ctx* c) {
     dfree(r->d_blk_lo);
     dfree(r->d_blk_hi);
     dfree(r->d_tile_blk);
-    dfree(r->d_tile_edit);
+    dfree(r->d_tile2);
     dfree(r->d_path_off);
     dfree(r->d_path);
     delete r;

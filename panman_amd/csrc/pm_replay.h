@@ -45,7 +45,7 @@ struct ReplayState {
     int64_t* d_blk_lo = nullptr;
     int64_t* d_blk_hi = nullptr;
     int32_t* d_tile_blk = nullptr;
-    int64_t* d_tile_edit = nullptr;
+    int2* d_tile2 = nullptr;
     int64_t* d_path_off = nullptr;
     int32_t* d_path = nullptr;
     bool ran = false;
@@ -62,7 +62,8 @@ struct ReplayHost {
     std::vector<int64_t> eoff;
     std::vector<uint32_t> ecol;
     std::vector<uint8_t> echr;
-    std::vector<int64_t> blk_lo, blk_hi, tile_edit, path_off;
+    std::vector<int64_t> blk_lo, blk_hi, tile_edit, path_off;   // (tile_edit: flattening scratch)
+    std::vector<int2> tile2;   // [N][tiles + 1] {first plain edit, first overriding edit}
     std::vector<int32_t> tile_blk, path_all;
     int32_t max_depth = 0, words = 0, tiles = 0;
     int64_t stride = 0;

@@ -6,59 +6,73 @@
 // nucleotide mutations of each node on its root->leaf path in order, only for blocks that
 // are present at the leaf (blockSequence, :1766-1787, :1842).
 //
-//   k_replay_piped  one workgroup per (leaf, 8 column tiles of 16 KiB): consensus tile -> LDS,
-//                   the path nodes' edits inside the tile applied root first by all four
-//                   waves, 64 path nodes (one chunk) at a time (edits of one node are unique
-//                   per column and sorted by column on the host, so a per-(node, tile) offset
-//                   table bounds each node's slice), absent blocks restored, one coalesced
-//                   write of the tile: 1 B per leaf-column to HBM, the replay roofline of
-//                   SURVEY.md §8d.  Any depth: a SARS-like tree's 280-node paths are 5 chunks.
+//   k_replay  one workgroup per (leaf, 8 column tiles of 16 KiB), tile after tile: the
+//             consensus tile -> LDS (LDS-DMA), the path nodes' edits inside the tile written
+//             by all four waves, absent blocks restored, one coalesced write of the tile:
+//             1 B per leaf-column to HBM, the replay roofline of SURVEY.md §8d.  Any depth.
+//
+// Edit order.  printFASTAUltraFastHelper applies each path node's mutations root first, so
+// of several edits of one column along a path the deepest wins.  The host marks an edit that
+// rewrites a column some ancestor edits (kEditOverrides; the flag holds for every leaf below
+// the node) and stores each node's edits as [plain | overriding], both column-sorted, with a
+// per-(node, tile) table of where each part starts (ReplayDev::tile2).  Along one path the
+// plain edits touch distinct columns (the shallowest edit of each column), so a tile's plain
+// edits are written by all waves in any order; the overriding ones (rare: collisions of two
+// edits on one path) are then gathered into an LDS list in path order and each is written
+// unless a later list entry -- a deeper node -- has the same column.  Tiles with more than
+// kOvrCap overriding edits apply them in path order instead, wave by wave.
 #include "pm_bits.h"
 #include "pm_internal.h"
 
 namespace pm {
 namespace {
 
-// The path's edits that fall in column tile t, applied to the LDS tile by ONE wave.  Only
-// an edit that overwrites an ancestor's edit of the same column (kEditOverrides, marked on
-// the host) needs ordering: the others touch distinct columns along any one path and are
-// written in any order, the overriding ones after them node by node, root first -- the
-// LDS writes of a wave take effect in issue order, so a descendant's edit wins without a
-// barrier.  A chunk is up to 64 path nodes: their slice bounds (one load per lane) and a
-// wave prefix sum of the slice lengths; a round gathers up to kEditsPerLane x 64 of the
-// chunk's edits at once (one memory round trip).
+// A chunk is up to 64 path nodes (lane = path node): their slice lengths in this tile and a
+// wave prefix sum over them; a round gathers kEditsPerLane x 64 of the chunk's edits at once
+// (one memory round trip).  2 per lane: 1.72 -> 1.67 ms at C5, 4.27 -> 3.45 ms on the
+// SARS-like tree against 4 (r05, interleaved); 1: 1.74 / 3.41.
 #ifndef PM_REPLAY_EPL
-#define PM_REPLAY_EPL 4
+#define PM_REPLAY_EPL 2
 #endif
 constexpr int kEditsPerLane = PM_REPLAY_EPL;
+constexpr int32_t kRound = kEditsPerLane * kWave;   // edits per wave-round
 
 struct EditChunk {
     int cnt;
-    int64_t lo;       // this lane's node: first edit of its slice
+    int32_t lo;       // this lane's node: first edit of its slice
     int32_t len;      // this lane's node: slice length
     int32_t excl;     // exclusive prefix of the lengths
     int32_t total;    // edits in the chunk
 };
 
-// A round in flight: col / chr straight from their loads (not combined with anything
-// until edit_write, so a prefetched round does not wait for its loads), node8 = path
-// position << 8, kNoEdit: none.
+__device__ __forceinline__ EditChunk edit_chunk_from(int cnt, int32_t lo, int32_t hi, int lane) {
+    EditChunk c;
+    c.cnt = cnt;
+    c.lo = lo;
+    c.len = lane < cnt ? hi - lo : 0;
+    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)c.len);
+    c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    c.excl = incl - c.len;
+    return c;
+}
+
+// A round in flight: col / chr straight from their loads (not combined with anything until
+// they are written, so a prefetched round does not wait for its loads); g = the edit's index
+// in the chunk, kNoEdit: none.
 struct EditRound {
     uint32_t col[kEditsPerLane];
     uint32_t chr[kEditsPerLane];
-    uint32_t node8[kEditsPerLane];
+    int32_t g[kEditsPerLane];
 };
-constexpr uint32_t kNoEdit = ~0u;
+constexpr int32_t kNoEdit = -1;
 
 __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& c, int32_t base, int64_t c0, int lane,
                                            EditRound& r) {
-    int64_t e[kEditsPerLane];
-    int32_t node[kEditsPerLane];
-    const uint32_t lo_lo = (uint32_t)c.lo, lo_hi = (uint32_t)(c.lo >> 32);
+    int32_t e[kEditsPerLane];
 #pragma unroll
     for (int j = 0; j < kEditsPerLane; ++j) {
-        // edit g of the chunk belongs to the last path node whose slice starts at or
-        // before g: a binary search over the lanes' prefix sums (64 nodes: 6 steps)
+        // edit g of the chunk belongs to the last path node whose slice starts at or before
+        // g: a binary search over the lanes' prefix sums (64 nodes: 6 steps)
         const int32_t g = base + lane + j * kWave;
         int k_lo = 0, k_hi = c.cnt - 1;
 #pragma unroll
@@ -67,79 +81,56 @@ __device__ __forceinline__ void edit_round(const ReplayDev& d, const EditChunk& 
             if (__shfl(c.excl, mid) <= g) k_lo = mid;
             else k_hi = mid - 1;
         }
-        const int32_t ek = __shfl(c.excl, k_lo);
-        const int64_t lok = (int64_t)(((uint64_t)(uint32_t)__shfl((int)lo_hi, k_lo) << 32) |
-                                      (uint32_t)__shfl((int)lo_lo, k_lo));
-        node[j] = g < c.total ? k_lo : -1;
-        e[j] = lok + (g - ek);
+        r.g[j] = g < c.total ? g : kNoEdit;
+        e[j] = __shfl(c.lo, k_lo) + (g - __shfl(c.excl, k_lo));
     }
 #pragma unroll
     for (int j = 0; j < kEditsPerLane; ++j) {
         r.col[j] = (uint32_t)c0;
         r.chr[j] = 0;
-        if (node[j] >= 0) {
+        if (r.g[j] != kNoEdit) {
             r.col[j] = d.edit_col[e[j]];
             r.chr[j] = d.edit_chr[e[j]];
         }
-        r.node8[j] = node[j] >= 0 ? (uint32_t)node[j] << 8 : kNoEdit;
     }
 }
 
-// A round's edits in two halves: the ones that overwrite no ancestor's edit (returns whether
-// the round holds any overriding one, wave-uniform) ...
-__device__ __forceinline__ bool edit_write_plain(const EditRound& r, char* buf, int64_t c0) {
-    bool any = false;
+__device__ __forceinline__ void edit_write_all(const EditRound& r, char* buf, int64_t c0) {
 #pragma unroll
-    for (int j = 0; j < kEditsPerLane; ++j) {
-        const bool ok = r.node8[j] != kNoEdit;
-        const bool ovr = ok && (r.chr[j] & kEditOverrides);
-        if (ok && !ovr) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
-        any |= __ballot(ovr) != 0;
-    }
-    return any;
+    for (int j = 0; j < kEditsPerLane; ++j)
+        if (r.g[j] != kNoEdit) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
 }
 
-// ... and its overriding ones, node by node in path order: the first pending edit (edits are
-// in path order) names the next node
-__device__ __forceinline__ void edit_write_overrides(const EditRound& r, char* buf, int64_t c0) {
+// Fallback for a tile with more than kOvrCap overriding edits: a round's edits node by node
+// in path order (the first pending edit -- edits are in path order -- names the next node;
+// g orders the nodes as it orders the edits).  node_of: the path position of each edit.
+__device__ __forceinline__ void edit_write_ordered(const EditRound& r, const int32_t* node_of, char* buf, int64_t c0) {
     const int lane = (int)threadIdx.x & (kWave - 1);
     uint64_t pend[kEditsPerLane];
     bool any = false;
 #pragma unroll
     for (int j = 0; j < kEditsPerLane; ++j) {
-        pend[j] = __ballot(r.node8[j] != kNoEdit && (r.chr[j] & kEditOverrides));
+        pend[j] = __ballot(r.g[j] != kNoEdit);
         any |= pend[j] != 0;
     }
     while (any) {
-        uint32_t k = 0;
+        int32_t k = 0;
         bool found = false;
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j)
             if (!found && pend[j]) {
-                k = (uint32_t)__builtin_amdgcn_readlane(r.node8[j], (int)__builtin_ctzll(pend[j])) >> 8;
+                k = __builtin_amdgcn_readlane(node_of[j], (int)__builtin_ctzll(pend[j]));
                 found = true;
             }
         any = false;
 #pragma unroll
         for (int j = 0; j < kEditsPerLane; ++j) {
-            const bool mine = ((pend[j] >> lane) & 1ull) && (r.node8[j] >> 8) == k;
+            const bool mine = ((pend[j] >> lane) & 1ull) && node_of[j] == k;
             if (mine) buf[r.col[j] - c0] = (char)(r.chr[j] & 0x7fu);
             pend[j] &= ~__ballot(mine);
             any |= pend[j] != 0;
         }
     }
-}
-
-// A chunk from slice bounds already in registers (the short-path pipeline below).
-__device__ __forceinline__ EditChunk edit_chunk_from(int cnt, int64_t lo, int64_t hi, int lane) {
-    EditChunk c;
-    c.cnt = cnt;
-    c.lo = lo;
-    c.len = lane < cnt ? (int32_t)(hi - lo) : 0;
-    const int32_t incl = (int32_t)wave_inclusive_scan((uint32_t)c.len);
-    c.total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    c.excl = incl - c.len;
-    return c;
 }
 
 // Blocks absent at the leaf that overlap tile t, as tile-relative column ranges in LDS
@@ -199,17 +190,16 @@ __device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf,
 #endif
 constexpr int kReplayGroup = PM_REPLAY_GROUP;
 
-#ifndef PM_REPLAY_PIPED_WAVES
-#define PM_REPLAY_PIPED_WAVES 6
-#endif
-// PM_REPLAY_DB: two LDS tile buffers -- tile t + 1's consensus copy-in is issued as tile t's
-// edits start, so it lands behind them instead of heading tile t + 1's critical path.  Off:
-// the second 16 KiB buffer takes the kernel from 6 to 4 workgroups per CU (LDS), and C5 went
-// 1.75 -> 2.04 ms (r04i, interleaved).
-#ifndef PM_REPLAY_DB
-#define PM_REPLAY_DB 0
-#endif
-constexpr int kReplayBufs = PM_REPLAY_DB ? 2 : 1;
+// A workgroup barrier that orders LDS only: each wave's LDS accesses are complete (lgkmcnt)
+// and visible to the others, while its global stores and loads stay in flight.  __syncthreads()
+// is a workgroup release / acquire over global memory too, which on gfx950 waits for every
+// outstanding vector memory operation (vmcnt(0)): behind the write-out that is a full HBM
+// write round trip per tile, and before it the next tile's prefetched edit loads.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // LDS-DMA copy-in of the consensus tile t (1 KiB per wave-instruction, all in flight).
 __device__ __forceinline__ void tile_copy_in(const ReplayDev& d, int32_t t, uint4* dst, int wave, int lane) {
@@ -224,110 +214,201 @@ __device__ __forceinline__ void tile_copy_in(const ReplayDev& d, int32_t t, uint
     }
 }
 
-// One chunk's edits of a tile, all four waves: every wave holds the chunk's slice bounds
-// (lane = path node) and takes every fourth round (a super-round = 4 x kEditsPerLane x 64
-// edits; a C5 tile has ~800).  Edits that overwrite no ancestor's edit touch distinct columns
-// along the path, so the waves write them in any order; the overriding ones (kEditOverrides,
-// rare) follow wave by wave -- the rounds are in path order -- with a barrier between, and
-// only in a super-round that has any.  Every super-round ends in a barrier, so the next
-// chunk's (deeper nodes') overriding edits land after this chunk's writes.  `r` holds the
-// wave's first round, already issued.
-__device__ __forceinline__ void chunk_edits(const ReplayDev& d, const EditChunk& ch, EditRound& r, char* buf,
-                                            int64_t c0, int wave, int lane) {
-    constexpr int32_t R = kEditsPerLane * kWave;
-    for (int32_t sr = 0; sr < ch.total; sr += 4 * R) {   // (uniform: every wave holds the same chunk)
-        const int32_t base = sr + wave * R;
-        if (sr > 0 && base < ch.total) edit_round(d, ch, base, c0, lane, r);   // (super-round 0: prefetched)
-        const bool ovr = base < ch.total && edit_write_plain(r, buf, c0);
-        if (__syncthreads_or(ovr)) {
-            for (int w = 0; w < 4; ++w) {
-                if (wave == w && base < ch.total) edit_write_overrides(r, buf, c0);
-                __syncthreads();
-            }
+// Overriding edits of a tile resolved in parallel (list in LDS, 4 B each); more: in path order.
+constexpr int kOvrCap = 1024;
+
+#ifndef PM_REPLAY_WAVES
+#define PM_REPLAY_WAVES 6
+#endif
+
+// The path's tile bounds in LDS.  A chunk's slice bounds for tile t are {plain, overriding}
+// starts at t and t + 1 for each of its path nodes; the first ReplayDev::ring path nodes keep
+// three tiles of them in a ring (dynamic LDS, `ring` = [3][d.ring]), written two tiles ahead by
+// the thread that owns the node (nodes tid, tid + 256), so a tile's chunks wait on no bounds
+// load; deeper path nodes (beyond the ring) load theirs from HBM.
+struct PathCtx {
+    int64_t p0;
+    int depth;
+    const int2* ring;
+    int32_t ring_n;
+};
+
+__device__ __forceinline__ void chunk_bounds(const ReplayDev& d, const PathCtx& pc, int q, int s0, int s1, int32_t t,
+                                             int lane, int& cnt, int2& lo, int2& hi) {
+    cnt = min(kWave, pc.depth - q);
+    lo = hi = make_int2(0, 0);
+    if (lane < cnt) {
+        const int k = q + lane;
+        if (k < pc.ring_n) {
+            lo = pc.ring[s0 * pc.ring_n + k];
+            hi = pc.ring[s1 * pc.ring_n + k];
+        } else {
+            const int2* te = d.tile2 + (size_t)d.path[pc.p0 + k] * (d.tiles + 1) + t;
+            lo = te[0];
+            hi = te[1];
         }
     }
 }
 
-// Slice bounds of chunk [q, q + 64) of the path at tile t (lane = path node); the path ids
-// and the bounds are two dependent loads, issued for chunk k + 1 before chunk k's rounds.
-struct ChunkBounds {
-    int cnt;
-    int64_t lo, hi;
-};
-
-__device__ __forceinline__ ChunkBounds chunk_bounds(const ReplayDev& d, int64_t q, int64_t p1, int32_t t, int lane) {
-    ChunkBounds b{(int)min((int64_t)kWave, p1 - q), 0, 0};
-    if (lane < b.cnt) {
-        const int64_t* te = d.tile_edit + (size_t)d.path[q + lane] * (d.tiles + 1) + t;
-        b.lo = te[0];
-        b.hi = te[1];
-    }
-    return b;
-}
-
-// Each wave prefetches its first round of the next tile's first chunk while the tile is
-// restored and written out, so a tile's edits cost LDS writes, not a chain of memory round
-// trips in one wave (round 3's single-editor kernel: ~10 us per 16 KiB tile at C5).  Paths
-// deeper than 64 nodes walk their further chunks after the first, each chunk's bounds loaded
-// while the previous chunk's rounds run.
-__global__ __launch_bounds__(256, PM_REPLAY_PIPED_WAVES) void k_replay_piped(ReplayDev d) {
-    __shared__ uint4 tile_buf[kReplayBufs][kReplayTile / 16];
+// One workgroup = (leaf, group of kReplayGroup column tiles).  Per tile: copy-in; the plain
+// edits, chunk after chunk, rounds dealt to the four waves (the first round of the first
+// chunk prefetched during the previous tile's write-out); the overriding edits staged in path
+// order and resolved; absent blocks restored; write-out.
+__global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay(ReplayDev d) {
+    __shared__ uint4 tile_buf[kReplayTile / 16];
+    __shared__ uint32_t olist[kOvrCap];   // (column in tile) | chr << 16, path order
     __shared__ int32_t rng[2][2 + 2 * kRestoreRanges];
+    extern __shared__ int2 ring[];        // [3][d.ring]
+    char* buf = reinterpret_cast<char*>(tile_buf);
     const int32_t leaf = blockIdx.x;
     const int32_t t_begin = (int32_t)blockIdx.y * kReplayGroup;
     const int32_t t_end = min(d.tiles, t_begin + kReplayGroup);
     const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & (kWave - 1);
-    constexpr int32_t R = kEditsPerLane * kWave;   // edits per wave-round
-    const int64_t p0 = d.path_off[leaf], p1 = d.path_off[leaf + 1];
-    const int cnt = (int)min((int64_t)kWave, p1 - p0);
-    const int64_t* te = nullptr;
-    int64_t te_next = 0, te_next2 = 0;   // this lane's node: slice starts of tiles t+1, t+2
-    EditChunk ch{};
-    EditRound r{};
-    if (cnt > 0) {
-        const int32_t node = lane < cnt ? d.path[p0 + lane] : d.path[p0];
-        te = d.tile_edit + (size_t)node * (d.tiles + 1);
-        const int64_t te_cur = te[t_begin];
-        te_next = te[t_begin + 1];
-        if (t_begin + 2 <= d.tiles) te_next2 = te[t_begin + 2];
-        ch = edit_chunk_from(cnt, te_cur, te_next, lane);
-        if (wave * R < ch.total) edit_round(d, ch, wave * R, (int64_t)t_begin * kReplayTile, lane, r);
+    PathCtx pc;
+    pc.p0 = d.path_off[leaf];
+    pc.depth = (int)(d.path_off[leaf + 1] - pc.p0);
+    pc.ring = ring;
+    pc.ring_n = d.ring;
+    const int ring_use = min(pc.depth, d.ring);
+    // the ring: tiles t_begin, t_begin + 1 now, t_begin + 2 in flight (pre)
+    int2 pre[2] = {make_int2(0, 0), make_int2(0, 0)};
+    int32_t pnode[2] = {-1, -1};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int k = tid + 256 * h;
+        if (k < ring_use) {
+            pnode[h] = d.path[pc.p0 + k];
+            const int2* te = d.tile2 + (size_t)pnode[h] * (d.tiles + 1);
+            ring[k] = te[t_begin];
+            ring[d.ring + k] = te[t_begin + 1];
+            if (t_begin + 2 <= t_end) pre[h] = te[t_begin + 2];
+        }
     }
     if (tid == kWave) absent_ranges(d, leaf, t_begin, rng[0]);
-    if (kReplayBufs == 2) tile_copy_in(d, t_begin, tile_buf[0], wave, lane);
+    EditChunk ch{}, co{};
+    EditRound r{}, ro{};
+    bool have_pf = false;   // (ch, r), (co, ro): tile t's first chunk and its first rounds
     for (int32_t t = t_begin; t < t_end; ++t) {
         const int64_t c0 = (int64_t)t * kReplayTile;
         const int64_t n = min(kReplayTile, d.row_stride - c0);   // multiple of 16
-        uint4* cur = tile_buf[kReplayBufs == 2 ? (t - t_begin) & 1 : 0];
-        char* buf = reinterpret_cast<char*>(cur);
-        if (kReplayBufs == 1) tile_copy_in(d, t, cur, wave, lane);
-        __syncthreads();   // tile t's copy-in landed; (two buffers) tile t - 1's write-out read its buffer
-        if (kReplayBufs == 2 && t + 1 < t_end) tile_copy_in(d, t + 1, tile_buf[(t + 1 - t_begin) & 1], wave, lane);
-        if (p1 - p0 <= kWave) {
-            chunk_edits(d, ch, r, buf, c0, wave, lane);
-        } else {
-            ChunkBounds nb = chunk_bounds(d, p0 + kWave, p1, t, lane);
-            chunk_edits(d, ch, r, buf, c0, wave, lane);
-            for (int64_t q = p0 + kWave; q < p1; q += kWave) {
-                const EditChunk cq = edit_chunk_from(nb.cnt, nb.lo, nb.hi, lane);
-                if (wave * R < cq.total) edit_round(d, cq, wave * R, c0, lane, r);
-                if (q + kWave < p1) nb = chunk_bounds(d, q + kWave, p1, t, lane);
-                chunk_edits(d, cq, r, buf, c0, wave, lane);
+        const int s0 = (t - t_begin) % 3, s1 = (t - t_begin + 1) % 3;
+        tile_copy_in(d, t, tile_buf, wave, lane);
+        __syncthreads();   // the copy-in landed; the ring's slots for t, t + 1 written
+        // Chunk by chunk: the plain edits written (any order), the overriding ones staged in
+        // path order (chunk base + index in the chunk); both parts' first rounds are issued
+        // together (for the first chunk during the previous tile's write-out)
+        int32_t no = 0;   // (uniform) overriding edits staged so far
+        for (int q = 0; q < pc.depth; q += kWave) {
+            if (q > 0 || !have_pf) {
+                int cnt;
+                int2 lo, hi;
+                chunk_bounds(d, pc, q, s0, s1, t, lane, cnt, lo, hi);
+                ch = edit_chunk_from(cnt, lo.x, hi.x, lane);
+                co = edit_chunk_from(cnt, lo.y, hi.y, lane);
+                if (wave * kRound < ch.total) edit_round(d, ch, wave * kRound, c0, lane, r);
+                if (wave * kRound < co.total) edit_round(d, co, wave * kRound, c0, lane, ro);
+            }
+            for (int32_t sr = 0; sr < ch.total; sr += 4 * kRound) {   // (uniform)
+                const int32_t base = sr + wave * kRound;
+                if (base >= ch.total) break;
+                if (sr > 0) edit_round(d, ch, base, c0, lane, r);
+                edit_write_all(r, buf, c0);
+            }
+            for (int32_t sr = 0; sr < co.total; sr += 4 * kRound) {
+                const int32_t base = sr + wave * kRound;
+                if (base >= co.total) break;
+                if (sr > 0) edit_round(d, co, base, c0, lane, ro);
+#pragma unroll
+                for (int j = 0; j < kEditsPerLane; ++j)
+                    if (ro.g[j] != kNoEdit && no + ro.g[j] < kOvrCap)
+                        olist[no + ro.g[j]] = (uint32_t)(ro.col[j] - c0) | (ro.chr[j] & 0x7fu) << 16;
+            }
+            no += co.total;
+        }
+        have_pf = false;
+        if (no > 0) {   // (uniform)
+            lds_barrier();   // the plain edits and the list are in LDS
+            if (no <= kOvrCap) {
+                // an entry is written unless a later one (a deeper path node) has its column
+                for (int32_t i = tid; i < no; i += 256) {
+                    const uint32_t e = olist[i], col = e & 0xffffu;
+                    bool later = false;
+                    for (int32_t k = i + 1; k < no && !later; ++k) later = (olist[k] & 0xffffu) == col;
+                    if (!later) buf[col] = (char)(e >> 16);
+                }
+            } else {
+                // in path order: the overriding rounds again, wave by wave, each round's edits
+                // node by node
+                for (int q = 0; q < pc.depth; q += kWave) {
+                    int cnt;
+                    int2 lo, hi;
+                    chunk_bounds(d, pc, q, s0, s1, t, lane, cnt, lo, hi);
+                    const EditChunk cf = edit_chunk_from(cnt, lo.y, hi.y, lane);
+                    for (int32_t sr = 0; sr < cf.total; sr += 4 * kRound) {
+                        const int32_t base = sr + wave * kRound;
+                        EditRound rf{};
+                        int32_t node_of[kEditsPerLane];
+#pragma unroll
+                        for (int j = 0; j < kEditsPerLane; ++j) node_of[j] = 0;
+                        if (base < cf.total) {
+                            edit_round(d, cf, base, c0, lane, rf);
+#pragma unroll
+                            for (int j = 0; j < kEditsPerLane; ++j) {   // path position of each edit
+                                int k_lo = 0, k_hi = cf.cnt - 1;
+#pragma unroll
+                                for (int st = 0; st < 6; ++st) {
+                                    const int mid = (k_lo + k_hi + 1) >> 1;
+                                    if (__shfl(cf.excl, mid) <= base + lane + j * kWave) k_lo = mid;
+                                    else k_hi = mid - 1;
+                                }
+                                node_of[j] = q + k_lo;
+                            }
+                        }
+                        for (int w = 0; w < 4; ++w) {
+                            if (wave == w && base < cf.total) edit_write_ordered(rf, node_of, buf, c0);
+                            lds_barrier();
+                        }
+                    }
+                }
             }
         }
+        lds_barrier();   // every edit in LDS before the restore overwrites absent blocks
         restore_absent(d, leaf, t, rng[(t - t_begin) & 1], buf, tid, blockDim.x);
-        if (cnt > 0 && t + 1 < t_end) {
-            // the next tile's first rounds, in flight through the restore / write / copy
-            ch = edit_chunk_from(cnt, te_next, te_next2, lane);
-            te_next = te_next2;
-            if (t + 3 <= d.tiles) te_next2 = te[t + 3];
-            if (wave * R < ch.total) edit_round(d, ch, wave * R, c0 + kReplayTile, lane, r);
+        // the ring slot of tile t - 1 (read by nobody any more) takes tile t + 2
+        if (t + 2 <= t_end) {
+            const int s2 = (t - t_begin + 2) % 3;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = tid + 256 * h;
+                if (k < ring_use) {
+                    ring[s2 * d.ring + k] = pre[h];
+                    if (t + 3 <= t_end) pre[h] = d.tile2[(size_t)pnode[h] * (d.tiles + 1) + t + 3];
+                }
+            }
         }
         if (tid == kWave && t + 1 < t_end) absent_ranges(d, leaf, t + 1, rng[(t + 1 - t_begin) & 1]);
-        __syncthreads();
+        lds_barrier();
+        if (t + 1 < t_end) {
+            // the next tile's first plain round, in flight through the write-out and copy-in
+            int cnt;
+            int2 lo, hi;
+            chunk_bounds(d, pc, 0, s1, (t - t_begin + 2) % 3, t + 1, lane, cnt, lo, hi);
+            ch = edit_chunk_from(cnt, lo.x, hi.x, lane);
+            co = edit_chunk_from(cnt, lo.y, hi.y, lane);
+            if (wave * kRound < ch.total) edit_round(d, ch, wave * kRound, c0 + kReplayTile, lane, r);
+            if (wave * kRound < co.total) edit_round(d, co, wave * kRound, c0 + kReplayTile, lane, ro);
+            have_pf = true;
+        }
         uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)leaf * d.row_stride + c0);
-        for (int64_t k = tid; k < n / 16; k += blockDim.x) dst[k] = cur[k];
-        if (kReplayBufs == 1) __syncthreads();   // the tile buffer is refilled next
+        // a fixed count of stores (the compiler then waits for an earlier load with
+        // vmcnt(#stores) instead of draining them)
+        static_assert(kReplayTile / 16 % 256 == 0, "write-out: whole rounds of 256 threads");
+#pragma unroll
+        for (int j = 0; j < kReplayTile / 16 / 256; ++j) {
+            const int k = tid + 256 * j;
+            if (k < n / 16) dst[k] = tile_buf[k];
+        }
+        lds_barrier();   // the tile buffer is refilled next
     }
 }
 
@@ -480,7 +561,8 @@ hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;
     timer_begin(c, 3);
     const unsigned groups = (unsigned)((d.tiles + kReplayGroup - 1) / kReplayGroup);
-    hipLaunchKernelGGL(k_replay_piped, dim3((unsigned)d.leaves, groups), dim3(256), 0, c->stream, d);
+    const size_t ring_bytes = (size_t)3 * d.ring * sizeof(int2);
+    hipLaunchKernelGGL(k_replay, dim3((unsigned)d.leaves, groups), dim3(256), ring_bytes, c->stream, d);
     timer_end(c, 3);
     return hipGetLastError();
 }

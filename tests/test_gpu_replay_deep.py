@@ -54,20 +54,23 @@ def _fasta_checked(engine, pm, aligned, min_chunks=2):
     return text
 
 
+# 200: k_replay_deep (slice bounds in LDS, <= 512 path nodes); 600: k_replay_piped<true>
+@pytest.mark.parametrize("leaves", [200, 600])
 @pytest.mark.parametrize("aligned", [True, False])
-def test_caterpillar_200_vs_oracle(engine, oracle, aligned):
+def test_caterpillar_vs_oracle(engine, oracle, aligned, leaves):
     rng = np.random.default_rng(4242)
-    off, idx, root = caterpillar(200)
+    off, idx, root = caterpillar(leaves)
     pm = random_panmat(rng, off, idx, root, names_for(off), blocks=6, block_len=(40, 300), mut_rate=0.03)
-    text = _fasta_checked(engine, pm, aligned, min_chunks=4)
+    text = _fasta_checked(engine, pm, aligned, min_chunks=(leaves - 1 + 63) // 64)
     assert _records(text) == _records(oracle.fasta(pm, aligned))
 
 
-def test_caterpillar_override_chain_across_chunks(engine, oracle):
-    """Every spine node rewrites the SAME columns (each edit overrides its ancestor's, 199
-    deep, crossing three chunk boundaries); every leaf must end with its deepest ancestor's
+@pytest.mark.parametrize("leaves", [200, 600])
+def test_caterpillar_override_chain_across_chunks(engine, oracle, leaves):
+    """Every spine node rewrites the SAME columns (each edit overrides its ancestor's, up to
+    599 deep, crossing every chunk boundary); every leaf must end with its deepest ancestor's
     characters.  Also a second column set edited only by every 63rd / 64th / 65th node."""
-    off, idx, root = caterpillar(200)
+    off, idx, root = caterpillar(leaves)
     names = names_for(off)
     pm = random_panmat(np.random.default_rng(7), off, idx, root, names, blocks=3, block_len=(30, 60),
                        mut_rate=0.0, block_rate=0.0, options=False)
@@ -78,11 +81,11 @@ def test_caterpillar_override_chain_across_chunks(engine, oracle):
         pm.add_nuc_mut(v, 0, 3, -1, 0, [code, [2, 4, 8, 1][k % 4]])   # MNP of 2 over columns 3-4
         if k % 63 == 0 or k % 64 == 0 or k % 65 == 0:
             pm.add_nuc_mut(v, 1, 5, -1, 3, [[8, 4, 2, 1][k % 4]])
-    for v in range(200):                                              # leaves: some override again
+    for v in range(leaves):                                           # leaves: some override again
         if v % 3 == 0:
             pm.add_nuc_mut(v, 0, 4, -1, 3, [15])
     for aligned in (True, False):
-        text = _fasta_checked(engine, pm, aligned, min_chunks=4)
+        text = _fasta_checked(engine, pm, aligned, min_chunks=(leaves - 1 + 63) // 64)
         assert _records(text) == _records(oracle.fasta(pm, aligned))
 
 
@@ -126,3 +129,20 @@ def test_reroot_deep_tree_vs_oracle(engine, oracle, which):
             assert tree_dump(f) == oracle.reroot(pm, leaf)
         finally:
             f.close()
+
+
+@pytest.mark.parametrize("leaves", [60, 200])
+def test_override_fallback_more_than_cap(engine, oracle, leaves):
+    """More overriding edits in one tile than the kernel's parallel resolver holds (kOvrCap =
+    1024): every spine node rewrites the same 24 columns, so the tile's overriding edits are
+    applied in path order by the fallback; 60 leaves = one chunk, 200 = four."""
+    off, idx, root = caterpillar(leaves)
+    names = names_for(off)
+    pm = random_panmat(np.random.default_rng(17), off, idx, root, names, blocks=2, block_len=(80, 90),
+                       mut_rate=0.0, block_rate=0.0, options=False)
+    spine = [v for v in range(len(names)) if off[v] != off[v + 1]]
+    for k, v in enumerate(spine):
+        for start in (0, 6, 20, 40):
+            pm.add_nuc_mut(v, 0, start, -1, 0, [[1, 2, 4, 8][(k + i) % 4] for i in range(6)])
+    for aligned in (True, False):
+        assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))

@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         uint64_t x = 1469598103934665603ull;
         x = mix(x, h.cons_row); x = mix(x, h.presence); x = mix(x, h.eoff); x = mix(x, h.ecol); x = mix(x, h.echr);
-        x = mix(x, h.tile_edit); x = mix(x, h.tile_blk); x = mix(x, h.path_off); x = mix(x, h.path_all);
+        x = mix(x, h.tile2); x = mix(x, h.tile_blk); x = mix(x, h.path_off); x = mix(x, h.path_all);
         std::printf("rc %d %s  %.3f s  edits %lld columns %lld  hash %016llx\n", rc, msg.c_str(), s, (long long)st.edits,
                     (long long)st.columns, (unsigned long long)x);
     }
