@@ -183,6 +183,7 @@ struct HostTree {
     int32_t num_tail_k = 0;
     int32_t num_tail_s = 0;               // subtree form: the first num_tail_s tail items are the S2 / S3 nodes
     int32_t sbase = -1;                   // ... dense indices sbase + item
+    int32_t vbase = -1;                   // virtual leaf-parents: dense indices [vbase, num_internal)
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form,
     // (up only) its Fitch groups, its Sankoff groups
     int64_t lvl_up[5] = {0, 0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
@@ -254,7 +255,12 @@ struct pm_ctx {
     // reads a subtree's leaves at scattered lanes draws one 64-B sector per lane, not four
     uint4* sub_planes = nullptr;
     size_t sub_planes_bytes = 0;
-    bool sub_planes_ok = false;
+    bool sub_planes_ok = false;   // (with pair_planes)
+    // every leaf present: each virtual leaf-parent's (one or) two leaf words side by side
+    // ([num_virtual][wpad][2] uint4, dense index vbase + pair), so the pre-order's reads of a
+    // leaf-parent child at its scattered dirty lanes draw one sector per lane instead of two
+    uint4* pair_planes = nullptr;
+    size_t pair_planes_bytes = 0;
     int32_t* score = nullptr;         // [S]
     uint8_t* root_code = nullptr;     // [S]
     bool ran = false;
@@ -321,6 +327,7 @@ hipError_t launch_pack_sites(pm_ctx* c, const uint8_t* d_codes4, uint4* dst);
 hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
 hipError_t launch_sub_planes(pm_ctx* c);
+hipError_t launch_pair_planes(pm_ctx* c);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
 void free_replay(pm_ctx* c);
 void comm_release(pm_ctx* c);   // pm_rccl.hip
@@ -376,6 +383,19 @@ struct ReplayDev {
     int32_t tiles = 0;
     const int2* tile2 = nullptr;   // [N][tiles + 1] {plain, overriding}
     int32_t ring = 0;              // path nodes per leaf whose tile bounds a workgroup keeps in LDS
+    int32_t tile_bytes = 0;        // column tile size of tile2 / tile_blk: kReplayTile or kDfsTile
+    // k_replay_dfs: leaves in depth-first order (dfs_row = their rows), cut into groups
+    // [g_leaf_off[g], g_leaf_off[g + 1]); a group's path nodes g_union[g_union_off[g] ..] in
+    // order of first appearance; per leaf its path length and the prefix shared with the
+    // previous leaf of its group (0 for a group's first)
+    bool dfs = false;
+    int32_t groups = 0;
+    const int32_t* dfs_row = nullptr;
+    const uint16_t* dfs_len = nullptr;
+    const uint16_t* dfs_lpfx = nullptr;
+    const int32_t* g_leaf_off = nullptr;
+    const int32_t* g_union_off = nullptr;
+    const int32_t* g_union = nullptr;
     const int64_t* path_off = nullptr;    // [leaves + 1] root-to-leaf node lists
     const int32_t* path = nullptr;
 };
@@ -385,6 +405,16 @@ struct ReplayDev {
 constexpr int64_t kReplayTile = PM_REPLAY_TILE;   // leaf-row bytes assembled in LDS per workgroup
 constexpr uint8_t kEditOverrides = 0x80;   // edit_chr flag: an ancestor edits the same column
 constexpr int32_t kReplayRingMax = 512;     // ReplayDev::ring cap (deeper path nodes: bounds from HBM)
+// k_replay_dfs: column tile per wave, leaves and path nodes per leaf group
+#ifndef PM_DFS_TILE
+#define PM_DFS_TILE 4096
+#endif
+constexpr int64_t kDfsTile = PM_DFS_TILE;
+#ifndef PM_DFS_LEAVES
+#define PM_DFS_LEAVES 16
+#endif
+constexpr int32_t kDfsLeaves = PM_DFS_LEAVES;
+constexpr int32_t kDfsUnionCap = 128;
 
 // FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
 // segment per (leaf, print position) -- a block read forward or reverse-complemented from

@@ -276,16 +276,87 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
 
     clock.lap("replay.flat_edits");
 
+    // ---- root-to-leaf paths (root first) of this shard's leaves
+    const int32_t L = (int32_t)r.leaves.size();
+    std::vector<int64_t>& path_off = h.path_off;
+    std::vector<int32_t>& path_all = h.path_all;
+    path_off.assign(L + 1, 0);
+    for (int32_t li = 0; li < L; ++li) {
+        int32_t depth = 0;
+        for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) ++depth;
+        path_off[li + 1] = path_off[li] + depth;
+        h.max_depth = std::max(h.max_depth, depth);
+    }
+    path_all.resize((size_t)path_off[L]);
+    host_parallel_for((L + 255) / 256, [&](int task) {
+        for (int32_t li = task * 256; li < std::min(L, task * 256 + 256); ++li) {
+            int32_t at = (int32_t)(path_off[li + 1] - path_off[li]);
+            for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path_all[(size_t)path_off[li] + --at] = n;
+        }
+    });
+    // ---- leaf groups for k_replay_dfs: the leaves in depth-first order, cut into runs of at
+    // most kDfsLeaves whose paths together hold at most kDfsUnionCap nodes; per leaf its path
+    // length and the prefix it shares with the previous leaf of its group.  Only when every
+    // path fits (else k_replay, tiles of kReplayTile).
+    h.dfs = h.max_depth <= kDfsUnionCap && L > 0;
+    if (h.dfs) {
+        std::vector<int32_t> row_of(N, -1);
+        for (int32_t li = 0; li < L; ++li) row_of[r.leaves[li]] = li;
+        std::vector<int32_t> order;
+        order.reserve(L);
+        std::vector<int32_t> st{p->root};
+        while (!st.empty()) {   // pre-order, children in list order
+            const int32_t v = st.back();
+            st.pop_back();
+            if (row_of[v] >= 0) order.push_back(row_of[v]);
+            for (int32_t e = p->child_offsets[v + 1] - 1; e >= p->child_offsets[v]; --e) st.push_back(p->child_index[e]);
+        }
+        h.dfs_row = order;
+        h.dfs_len.resize(L);
+        h.dfs_lpfx.resize(L);
+        h.g_leaf_off.assign(1, 0);
+        h.g_union_off.assign(1, 0);
+        h.g_union.clear();
+        int32_t cnt = 0, uni = 0;
+        for (int32_t i = 0; i < L; ++i) {
+            const int32_t* pa = path_all.data() + path_off[order[i]];
+            const int32_t la = (int32_t)(path_off[order[i] + 1] - path_off[order[i]]);
+            int32_t lp = 0;
+            if (i > 0) {
+                const int32_t* pb = path_all.data() + path_off[order[i - 1]];
+                const int32_t lb = (int32_t)(path_off[order[i - 1] + 1] - path_off[order[i - 1]]);
+                while (lp < la && lp < lb && pa[lp] == pb[lp]) ++lp;
+            }
+            if (i == 0 || cnt == kDfsLeaves || uni + (la - lp) > kDfsUnionCap) {   // a new group
+                if (i > 0) {
+                    h.g_leaf_off.push_back(i);
+                    h.g_union_off.push_back((int32_t)h.g_union.size());
+                }
+                cnt = 0;
+                uni = 0;
+                lp = 0;
+            }
+            for (int32_t k = lp; k < la; ++k) h.g_union.push_back(pa[k]);
+            uni += la - lp;
+            ++cnt;
+            h.dfs_len[i] = (uint16_t)la;
+            h.dfs_lpfx[i] = (uint16_t)lp;
+        }
+        h.g_leaf_off.push_back(L);
+        h.g_union_off.push_back((int32_t)h.g_union.size());
+    }
+    const int64_t tb = h.dfs ? kDfsTile : kReplayTile;   // bytes per column tile
+
     // ---- column tiles: per node, the first (column-sorted) edit of every tile
     const int64_t stride = (r.columns + 15) / 16 * 16;
-    const int32_t tiles = (int32_t)((stride + kReplayTile - 1) / kReplayTile);
+    const int32_t tiles = (int32_t)((stride + tb - 1) / tb);
     std::vector<int64_t>& tile_edit = h.tile_edit;
     tile_edit.resize((size_t)N * (tiles + 1));
     host_parallel_for((N + 15) / 16, [&](int task) {
         for (int32_t v = task * 16; v < std::min(N, task * 16 + 16); ++v) {
             int64_t e = eoff[v];
             for (int32_t t = 0; t <= tiles; ++t) {
-                const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
+                const int64_t c0 = std::min<int64_t>((int64_t)t * tb, stride);
                 while (e < eoff[v + 1] && (int64_t)ecol[e] < c0) ++e;
                 tile_edit[(size_t)v * (tiles + 1) + t] = e;
             }
@@ -314,8 +385,8 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
         host_parallel_for(T, [&](int task) {
             const int32_t t0 = (int32_t)((int64_t)tiles * task / T), t1 = (int32_t)((int64_t)tiles * (task + 1) / T);
             if (t1 <= t0) return;
-            const int64_t c0 = (int64_t)t0 * kReplayTile;
-            std::vector<int32_t> active((size_t)(t1 - t0) * kReplayTile, 0);
+            const int64_t c0 = (int64_t)t0 * tb;
+            std::vector<int32_t> active((size_t)(t1 - t0) * tb, 0);
             for (const auto& [v, leaving] : walk) {
                 const int64_t e0 = tile_edit[(size_t)v * (tiles + 1) + t0], e1 = tile_edit[(size_t)v * (tiles + 1) + t1];
                 if (leaving) {
@@ -359,7 +430,7 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
             }
             int64_t ep = b, eo = mid;
             for (int32_t t = 0; t <= tiles; ++t) {
-                const int64_t c0 = std::min<int64_t>((int64_t)t * kReplayTile, stride);
+                const int64_t c0 = std::min<int64_t>((int64_t)t * tb, stride);
                 while (ep < mid && (int64_t)ecol[ep] < c0) ++ep;
                 while (eo < e && (int64_t)ecol[eo] < c0) ++eo;
                 tile2[(size_t)v * (tiles + 1) + t] = make_int2((int)ep, (int)eo);
@@ -369,31 +440,18 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
     std::vector<int64_t>().swap(tile_edit);
     clock.lap("replay.flat_overrides");
     // ---- per-leaf block state (getBlockSequence + the block-mutation pass of the helper)
-    const int32_t L = (int32_t)r.leaves.size();
     const int32_t words = (M + 31) / 32;
     std::vector<uint32_t>& presence = h.presence;
     presence.assign((size_t)L * words, 0);
     r.present.assign(L, {});
     r.exists.assign(L, {});
     r.strand.assign(L, {});
-    std::vector<int64_t>& path_off = h.path_off;
-    std::vector<int32_t>& path_all = h.path_all;
-    path_off.assign(L + 1, 0);
-    for (int32_t li = 0; li < L; ++li) {
-        int32_t depth = 0;
-        for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) ++depth;
-        path_off[li + 1] = path_off[li] + depth;
-        h.max_depth = std::max(h.max_depth, depth);
-    }
-    path_all.resize((size_t)path_off[L]);
     const int64_t nb_slots = (int64_t)B + 1;   // blockSequence has blocks.size()+1 entries
     std::vector<int> leaf_err(L, PM_OK);
     host_parallel_for((L + 15) / 16, [&](int task) {
         for (int32_t li = task * 16; li < std::min(L, task * 16 + 16); ++li) {
-            int32_t* path = path_all.data() + path_off[li];   // root first
+            const int32_t* path = path_all.data() + path_off[li];   // root first
             const int32_t depth = (int32_t)(path_off[li + 1] - path_off[li]);
-            int32_t at = depth;
-            for (int32_t n = r.leaves[li]; n >= 0; n = r.parent[n]) path[--at] = n;
             std::vector<uint8_t> pres(std::max<int64_t>(M, nb_slots), 0), ex(M, 0), st(M, 1);
             for (int32_t i = 0; i < depth; ++i) {
                 const int32_t n = path[i];
@@ -447,7 +505,7 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
     }
     h.tile_blk.resize(tiles + 1);
     for (int32_t t = 0, id = 0; t <= tiles; ++t) {
-        const int64_t c0 = (int64_t)t * kReplayTile;
+        const int64_t c0 = (int64_t)t * tb;
         while (id < M && h.blk_hi[id] <= c0) ++id;
         h.tile_blk[t] = id;
     }
@@ -456,6 +514,7 @@ int replay_flatten(const pm_panmat* p, ReplayState& r, ReplayHost& h, int64_t le
     h.words = words;
     h.stride = stride;
     h.tiles = tiles;
+    h.tile_bytes = (int32_t)tb;
     r.cons = std::move(cons);
     r.main_col = std::move(main_col);
     r.gap_col = std::move(gap_col);
@@ -487,12 +546,18 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         (e = dput(&r.d_blk_hi, h.blk_hi, c->stream)) != hipSuccess || (e = dput(&r.d_tile_blk, h.tile_blk, c->stream)) != hipSuccess ||
         (e = dput(&r.d_tile2, h.tile2, c->stream)) != hipSuccess ||
         (e = dput(&r.d_path_off, h.path_off, c->stream)) != hipSuccess || (e = dput(&r.d_path, h.path_all, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_dfs_row, h.dfs_row, c->stream)) != hipSuccess || (e = dput(&r.d_dfs_len, h.dfs_len, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_dfs_lpfx, h.dfs_lpfx, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_g_leaf_off, h.g_leaf_off, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_g_union_off, h.g_union_off, c->stream)) != hipSuccess ||
+        (e = dput(&r.d_g_union, h.g_union, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
     clock.lap("replay.upload");
     // (counts, not seconds: the deepest root->leaf path and its 64-node edit chunks per tile)
     phase_add("replay.max_depth", (double)h.max_depth);
     phase_add("replay.path_chunks", (double)((h.max_depth + kWave - 1) / kWave));
+    phase_add("replay.dfs_groups", h.dfs ? (double)(h.g_leaf_off.size() - 1) : 0.0);   // 0: k_replay
     ReplayDev& d = r.dev;
     d.leaves = L;
     d.row_stride = h.stride;
@@ -516,6 +581,15 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     d.ring = std::min(std::max(kWave, (h.max_depth + kWave - 1) / kWave * kWave), kReplayRingMax);
     d.path_off = r.d_path_off;
     d.path = r.d_path;
+    d.tile_bytes = h.tile_bytes;
+    d.dfs = h.dfs;
+    d.groups = h.dfs ? (int32_t)h.g_leaf_off.size() - 1 : 0;
+    d.dfs_row = r.d_dfs_row;
+    d.dfs_len = r.d_dfs_len;
+    d.dfs_lpfx = r.d_dfs_lpfx;
+    d.g_leaf_off = r.d_g_leaf_off;
+    d.g_union_off = r.d_g_union_off;
+    d.g_union = r.d_g_union;
     return PM_OK;
 }
 
@@ -536,6 +610,12 @@ void free_replay(pm_ctx* c) {
     dfree(r->d_tile2);
     dfree(r->d_path_off);
     dfree(r->d_path);
+    dfree(r->d_dfs_row);
+    dfree(r->d_dfs_len);
+    dfree(r->d_dfs_lpfx);
+    dfree(r->d_g_leaf_off);
+    dfree(r->d_g_union_off);
+    dfree(r->d_g_union);
     delete r;
     c->replay = nullptr;
 }

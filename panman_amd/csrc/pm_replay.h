@@ -46,6 +46,8 @@ struct ReplayState {
     int64_t* d_blk_hi = nullptr;
     int32_t* d_tile_blk = nullptr;
     int2* d_tile2 = nullptr;
+    int32_t *d_dfs_row = nullptr, *d_g_leaf_off = nullptr, *d_g_union_off = nullptr, *d_g_union = nullptr;
+    uint16_t *d_dfs_len = nullptr, *d_dfs_lpfx = nullptr;
     int64_t* d_path_off = nullptr;
     int32_t* d_path = nullptr;
     bool ran = false;
@@ -65,7 +67,11 @@ struct ReplayHost {
     std::vector<int64_t> blk_lo, blk_hi, tile_edit, path_off;   // (tile_edit: flattening scratch)
     std::vector<int2> tile2;   // [N][tiles + 1] {first plain edit, first overriding edit}
     std::vector<int32_t> tile_blk, path_all;
-    int32_t max_depth = 0, words = 0, tiles = 0;
+    int32_t max_depth = 0, words = 0, tiles = 0, tile_bytes = 0;
+    // leaf groups for k_replay_dfs (dfs: every path fits kDfsUnionCap)
+    bool dfs = false;
+    std::vector<int32_t> dfs_row, g_leaf_off, g_union_off, g_union;
+    std::vector<uint16_t> dfs_len, dfs_lpfx;
     int64_t stride = 0;
 };
 // Its host half (no device call): fills r and the arrays replay_prepare uploads.

@@ -137,8 +137,9 @@ __device__ __forceinline__ void edit_write_ordered(const EditRound& r, const int
 // (rng[0] = count, -1 = more than kRestoreRanges: the restore walks the blocks itself).
 constexpr int kRestoreRanges = 6;
 
+template <int64_t TB = kReplayTile>
 __device__ __forceinline__ void absent_ranges(const ReplayDev& d, int32_t leaf, int32_t t, int32_t* rng) {
-    const int64_t c0 = (int64_t)t * kReplayTile, c1 = min(c0 + kReplayTile, d.row_stride);
+    const int64_t c0 = (int64_t)t * TB, c1 = min(c0 + TB, d.row_stride);
     const uint32_t* pres = d.presence + (size_t)leaf * d.presence_words;
     int nr = 0;
     for (int32_t id = d.tile_blk[t]; id < d.blocks; ++id) {
@@ -412,6 +413,352 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay(ReplayDev d) {
     }
 }
 
+// ---- k_replay_dfs: one wave = (leaf group, column tile), the leaves of the group in
+// depth-first order against ONE copy of the tile in the wave's own LDS.
+//
+// Consecutive leaves in depth-first order share their path down to their lowest common
+// ancestor, so leaf i's row is leaf i - 1's with the edits of the nodes below the LCA on
+// i - 1's path undone and those on i's path applied: every edge of the group's subtree is
+// applied and undone once per tile, instead of every path node once per leaf (C5: 3.6x
+// fewer edit writes; a SARS-like tree ~7x), and the consensus tile is copied in once per
+// group instead of once per leaf.  Undo: every applied edit pushes the byte it overwrote
+// (plain edits onto one stack, overriding ones onto another, frames per path position); the
+// exit pops the overriding frames deepest first, node by node, then every plain entry at
+// once (plain edits of one path touch distinct columns).  A wave's LDS operations take effect
+// in issue order, so the phases need no barrier.  Blocks absent at a leaf are substituted
+// with the consensus at write-out.  A leaf whose edits would overflow a stack rebuilds its
+// row (consensus copy-in, whole path, nothing pushed), as do the group's later leaves.
+static_assert(kDfsLeaves <= kWave && kDfsUnionCap <= 256, "k_replay_dfs: a lane per leaf, u8 group node indices");
+constexpr int kDfsPCap = 384;   // plain edits on the current path in one tile
+constexpr int kDfsOCap = 64;    // overriding edits on the current path in one tile
+
+struct DfsLds {
+    uint4 tile[kDfsTile / 16];
+    int4 bnd[kDfsUnionCap];          // per group node: {plain lo, plain hi, overriding lo, hi} of this tile
+    uint32_t pst[kDfsPCap];          // plain undo stack: (column in tile) | old byte << 16
+    uint32_t ost[kDfsOCap];          // overriding undo stack
+    uint16_t psp_at[kDfsUnionCap];   // stack pointers before each path position's pushes
+    uint16_t osp_at[kDfsUnionCap];
+    uint8_t cur_u[kDfsUnionCap];     // group node index at each position of the current path
+    // the tile's blocks (tile-relative [ba, bb), nb of them; -1: more than the table holds) and,
+    // per leaf of the group, its row, path length, shared prefix and absent-block mask
+    int16_t ba[kWave], bb[kWave];
+    int32_t nb;
+    uint64_t absent[kDfsLeaves];
+    int32_t lrow[kDfsLeaves];
+    uint16_t llen[kDfsLeaves], llp[kDfsLeaves];
+};
+
+// edit_round plus each edit's node (position in the chunk) for the ordered apply
+__device__ __forceinline__ void edit_nodes(const EditChunk& c, int32_t base, int lane, int32_t* node_of) {
+#pragma unroll
+    for (int j = 0; j < kEditsPerLane; ++j) {
+        const int32_t g = base + lane + j * kWave;
+        int k_lo = 0, k_hi = c.cnt - 1;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            const int mid = (k_lo + k_hi + 1) >> 1;
+            if (__shfl(c.excl, mid) <= g) k_lo = mid;
+            else k_hi = mid - 1;
+        }
+        node_of[j] = k_lo;
+    }
+}
+
+
+// Item start: the tile's blocks, and for each leaf of the group its metadata and which of
+// those blocks are absent at it (one pass of loads, in flight with the consensus copy-in).
+__device__ __forceinline__ void dfs_leaf_tables(const ReplayDev& d, DfsLds& S, int32_t i0, int32_t cnt, int32_t t,
+                                                int64_t c0, int64_t n, int lane) {
+    const int32_t id = d.tile_blk[t] + lane;
+    bool ok = false;
+    if (id < d.blocks) {
+        const int64_t lo = d.blk_lo[id];
+        ok = lo < c0 + n;
+        if (ok) {
+            S.ba[lane] = (int16_t)(max(lo, c0) - c0);
+            S.bb[lane] = (int16_t)(min(d.blk_hi[id], c0 + n) - c0);
+        }
+    }
+    const int nb = __popcll(__ballot(ok));   // (blocks are in column order: a prefix of the lanes)
+    if (lane < cnt) {
+        S.lrow[lane] = d.dfs_row[i0 + lane];
+        S.llen[lane] = d.dfs_len[i0 + lane];
+        S.llp[lane] = d.dfs_lpfx[i0 + lane];
+        S.absent[lane] = 0;
+    }
+    S.nb = nb == kWave ? -1 : nb;
+    if (nb == kWave) return;   // (the write-out walks the blocks itself)
+    const int32_t id0 = d.tile_blk[t];
+    for (int32_t e = lane; e < cnt * nb; e += kWave) {
+        const int32_t k = e / nb, j = e - k * nb, bid = id0 + j;
+        const uint32_t w = d.presence[(size_t)S.lrow[k] * d.presence_words + (bid >> 5)];
+        if (!((w >> (bid & 31)) & 1u)) atomicOr(reinterpret_cast<unsigned long long*>(&S.absent[k]), 1ull << j);
+    }
+}
+
+// The leaf's row for this tile from the LDS tile, blocks absent at the leaf from the consensus.
+__device__ __forceinline__ uint32_t byte_span_mask(int32_t w0, int32_t a, int32_t b) {   // bytes of dword [w0, w0 + 4) in [a, b)
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m |= (w0 + k >= a && w0 + k < b) ? 0xffu << (8 * k) : 0u;
+    return m;
+}
+
+__device__ __forceinline__ void dfs_write_out(const ReplayDev& d, DfsLds& S, int32_t li, int32_t t, int64_t c0, int64_t n,
+                                              int lane) {
+    const int32_t row = S.lrow[li];
+    const int nb = S.nb;
+    const uint64_t am = nb >= 0 ? S.absent[li] : ~0ull;
+    uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)row * d.row_stride + c0);
+    const uint4* cons16 = reinterpret_cast<const uint4*>(d.cons_row + c0);
+    static_assert(kDfsTile / 16 % kWave == 0, "write-out: whole rounds of 64 lanes");
+    for (int j = 0; j < kDfsTile / 16 / kWave; ++j) {
+        const int k = lane + kWave * j;
+        if (k >= n / 16) break;
+        uint4 v = S.tile[k];
+        if (am != 0) {   // (uniform)
+            uint32_t m[4] = {0, 0, 0, 0};
+            if (nb >= 0) {
+                for (uint64_t x = am; x; x &= x - 1) {
+                    const int bj = __builtin_ctzll(x);
+                    const int32_t a = S.ba[bj], b = S.bb[bj];
+                    if (a < 16 * k + 16 && b > 16 * k)
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) m[w] |= byte_span_mask(16 * k + 4 * w, a, b);
+                }
+            } else {   // more blocks than the table holds: walk them
+                const uint32_t* pres = d.presence + (size_t)row * d.presence_words;
+                for (int32_t id = d.tile_blk[t]; id < d.blocks; ++id) {
+                    const int64_t b_lo = d.blk_lo[id];
+                    if (b_lo >= c0 + 16 * k + 16) break;
+                    if ((pres[id >> 5] >> (id & 31)) & 1u) continue;
+                    const int32_t a = (int32_t)(max(b_lo, c0) - c0), b = (int32_t)(min(d.blk_hi[id], c0 + n) - c0);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) m[w] |= byte_span_mask(16 * k + 4 * w, a, b);
+                }
+            }
+            if (m[0] | m[1] | m[2] | m[3]) {
+                const uint4 cv = cons16[k];
+                v.x = (v.x & ~m[0]) | (cv.x & m[0]);
+                v.y = (v.y & ~m[1]) | (cv.y & m[1]);
+                v.z = (v.z & ~m[2]) | (cv.z & m[2]);
+                v.w = (v.w & ~m[3]) | (cv.w & m[3]);
+            }
+        }
+        dst[k] = v;
+    }
+}
+
+// A leaf's first chunk of entering positions (lane = position, group nodes u_lo + lane) and
+// the first round of its plain and of its overriding edits, issued ahead (during the previous
+// leaf's write-out).
+struct DfsPrefetch {
+    EditChunk ch, co;
+    EditRound r, ro;
+};
+
+__device__ __forceinline__ void dfs_prefetch(const ReplayDev& d, const DfsLds& S, int32_t u_lo, int32_t cnt, int64_t c0,
+                                             int lane, DfsPrefetch& f) {
+    int4 b = make_int4(0, 0, 0, 0);
+    if (lane < cnt) b = S.bnd[u_lo + lane];
+    f.ch = edit_chunk_from(cnt, b.x, b.y, lane);
+    f.co = edit_chunk_from(cnt, b.z, b.w, lane);
+    if (f.ch.total > 0) edit_round(d, f.ch, 0, c0, lane, f.r);
+    if (f.co.total > 0) edit_round(d, f.co, 0, c0, lane, f.ro);
+}
+
+// Apply the edits of path positions [p_lo, p_hi) of the current path (group nodes cur_u[p]):
+// plain ones first (all positions at once, any order), then the overriding ones position by
+// position in path order.  PUSH: save every overwritten byte and record the frames.  `pf`:
+// the first chunk and its first rounds are in `f` (dfs_prefetch).
+template <bool PUSH>
+__device__ __forceinline__ void dfs_apply(const ReplayDev& d, DfsLds& S, int32_t p_lo, int32_t p_hi, int64_t c0, int lane,
+                                          int32_t& psp, int32_t& osp, bool pf, DfsPrefetch& f) {
+    char* buf = reinterpret_cast<char*>(S.tile);
+    for (int32_t q = p_lo; q < p_hi; q += kWave) {   // plain
+        const int cnt = min(kWave, p_hi - q);
+        const bool first = pf && q == p_lo;
+        if (!first) {
+            int4 b = make_int4(0, 0, 0, 0);
+            if (lane < cnt) b = S.bnd[S.cur_u[q + lane]];
+            f.ch = edit_chunk_from(cnt, b.x, b.y, lane);
+        }
+        const EditChunk& ch = f.ch;
+        if (PUSH && lane < cnt) S.psp_at[q + lane] = (uint16_t)(psp + ch.excl);
+        for (int32_t base = 0; base < ch.total; base += kRound) {
+            if (!first || base > 0) edit_round(d, ch, base, c0, lane, f.r);
+            const EditRound& r = f.r;
+#pragma unroll
+            for (int j = 0; j < kEditsPerLane; ++j)
+                if (r.g[j] != kNoEdit) {
+                    const uint32_t col = r.col[j] - (uint32_t)c0;
+                    if (PUSH) S.pst[psp + r.g[j]] = col | (uint32_t)(uint8_t)buf[col] << 16;
+                    buf[col] = (char)(r.chr[j] & 0x7fu);
+                }
+        }
+        if (PUSH) psp += ch.total;
+    }
+    for (int32_t q = p_lo; q < p_hi; q += kWave) {   // overriding, in path order
+        const int cnt = min(kWave, p_hi - q);
+        const bool first = pf && q == p_lo;
+        if (!first) {
+            int4 b = make_int4(0, 0, 0, 0);
+            if (lane < cnt) b = S.bnd[S.cur_u[q + lane]];
+            f.co = edit_chunk_from(cnt, b.z, b.w, lane);
+        }
+        const EditChunk& co = f.co;
+        if (PUSH && lane < cnt) S.osp_at[q + lane] = (uint16_t)(osp + co.excl);
+        for (int32_t base = 0; base < co.total; base += kRound) {
+            if (!first || base > 0) edit_round(d, co, base, c0, lane, f.ro);
+            const EditRound& r = f.ro;
+            int32_t node_of[kEditsPerLane];
+            edit_nodes(co, base, lane, node_of);
+            uint64_t pend[kEditsPerLane];
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < kEditsPerLane; ++j) {
+                pend[j] = __ballot(r.g[j] != kNoEdit);
+                any |= pend[j] != 0;
+            }
+            while (any) {   // node by node: the first pending edit names the next node
+                int32_t k = 0;
+                bool found = false;
+#pragma unroll
+                for (int j = 0; j < kEditsPerLane; ++j)
+                    if (!found && pend[j]) {
+                        k = __builtin_amdgcn_readlane(node_of[j], (int)__builtin_ctzll(pend[j]));
+                        found = true;
+                    }
+                any = false;
+#pragma unroll
+                for (int j = 0; j < kEditsPerLane; ++j) {
+                    const bool mine = ((pend[j] >> lane) & 1ull) && node_of[j] == k;
+                    if (mine) {
+                        const uint32_t col = r.col[j] - (uint32_t)c0;
+                        if (PUSH) S.ost[osp + r.g[j]] = col | (uint32_t)(uint8_t)buf[col] << 16;
+                        buf[col] = (char)(r.chr[j] & 0x7fu);
+                    }
+                    pend[j] &= ~__ballot(mine);
+                    any |= pend[j] != 0;
+                }
+            }
+        }
+        if (PUSH) osp += co.total;
+    }
+}
+
+// Edits of positions [p_lo, p_hi): plain and overriding counts (uniform).
+__device__ __forceinline__ void dfs_counts(DfsLds& S, int32_t p_lo, int32_t p_hi, int lane, int32_t& np, int32_t& no) {
+    np = no = 0;
+    for (int32_t q = p_lo; q < p_hi; q += kWave) {
+        int4 b = make_int4(0, 0, 0, 0);
+        if (q + lane < p_hi) b = S.bnd[S.cur_u[q + lane]];
+        np += (int32_t)wave_inclusive_scan((uint32_t)(b.y - b.x)) ;
+        no += (int32_t)wave_inclusive_scan((uint32_t)(b.w - b.z));
+        np = __builtin_amdgcn_readlane(np, kWave - 1);
+        no = __builtin_amdgcn_readlane(no, kWave - 1);
+    }
+}
+
+__device__ __forceinline__ void dfs_copy_in(const ReplayDev& d, DfsLds& S, int64_t c0, int64_t n, int lane) {
+    const uint4* src = reinterpret_cast<const uint4*>(d.cons_row + c0);
+    for (int64_t b = 0; b < n / 16; b += kWave) {
+        const int64_t k = b + lane;
+        if (k < n / 16)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                             (__attribute__((address_space(3))) void*)(S.tile + b), 16, 0, 0);
+    }
+}
+
+// waves per SIMD (the second __launch_bounds__ argument is amdgpu_waves_per_eu): 4 = 128 VGPRs
+#ifndef PM_DFS_WAVES
+#define PM_DFS_WAVES 4
+#endif
+__global__ __launch_bounds__(kWave, PM_DFS_WAVES) void k_replay_dfs(ReplayDev d) {
+    __shared__ DfsLds S;
+    const int lane = (int)threadIdx.x;
+#ifdef PM_DFS_TILE_MAJOR   // (A/B) concurrent waves = many groups' rows at one tile
+    const int32_t t = (int32_t)(blockIdx.x / (uint32_t)d.groups), g = (int32_t)(blockIdx.x % (uint32_t)d.groups);
+#else
+    // concurrent waves = consecutive tiles of few groups: their writes are adjacent pieces of
+    // the same few rows (DRAM pages, translations) instead of one piece of thousands of rows
+    const int32_t g = (int32_t)(blockIdx.x / (uint32_t)d.tiles), t = (int32_t)(blockIdx.x % (uint32_t)d.tiles);
+#endif
+    const int64_t c0 = (int64_t)t * kDfsTile;
+    const int64_t n = min(kDfsTile, d.row_stride - c0);   // multiple of 16
+    const int32_t i0 = d.g_leaf_off[g], i1 = d.g_leaf_off[g + 1];
+    const int32_t u0 = d.g_union_off[g], nu = d.g_union_off[g + 1] - u0;
+    // the group's node bounds for this tile, and the consensus tile
+    for (int32_t u = lane; u < nu; u += kWave) {
+        const int2* te = d.tile2 + (size_t)d.g_union[u0 + u] * (d.tiles + 1) + t;
+        const int2 a = te[0], b = te[1];
+        S.bnd[u] = make_int4(a.x, b.x, a.y, b.y);
+    }
+    dfs_copy_in(d, S, c0, n, lane);
+    dfs_leaf_tables(d, S, i0, i1 - i0, t, c0, n, lane);
+    __syncthreads();   // (one wave: the copy-in and the tables landed)
+    int32_t psp = 0, osp = 0, prev_len = 0, next_u = 0;
+    bool rebuild = false;
+    DfsPrefetch f;
+    int32_t len = S.llen[0], lp = 0;
+    dfs_prefetch(d, S, 0, min(kWave, len), c0, lane, f);
+    for (int32_t i = i0; i < i1; ++i) {
+        // the path positions [lp, len) are new group nodes next_u ..
+        for (int32_t p = lp + lane; p < len; p += kWave) S.cur_u[p] = (uint8_t)(next_u + (p - lp));
+        next_u += len - lp;
+        int32_t np = 0, no = 0;
+#ifdef PM_DFS_NOEDITS   // timing experiments only: the rows are the consensus
+        if (true) {
+            prev_len = len;
+            dfs_write_out(d, S, i - i0, t, c0, n, lane);
+            if (i + 1 < i1) { len = S.llen[i + 1 - i0]; lp = S.llp[i + 1 - i0]; }
+            continue;
+        }
+#endif
+        if (!rebuild) {
+            dfs_counts(S, lp, len, lane, np, no);
+            const int32_t psp_x = lp < prev_len ? (int32_t)S.psp_at[lp] : psp;
+            const int32_t osp_x = lp < prev_len ? (int32_t)S.osp_at[lp] : osp;
+            rebuild = psp_x + np > kDfsPCap || osp_x + no > kDfsOCap;
+        }
+        char* buf = reinterpret_cast<char*>(S.tile);
+        if (!rebuild) {
+            // exit: overriding frames deepest first, then the plain entries above lp
+            if (lp < prev_len) {
+                for (int32_t p = prev_len - 1; p >= lp && osp > (int32_t)S.osp_at[lp]; --p) {
+                    const int32_t a = S.osp_at[p];
+                    for (int32_t k = a + lane; k < osp; k += kWave) {
+                        const uint32_t e = S.ost[k];
+                        buf[e & 0xffffu] = (char)(e >> 16);
+                    }
+                    osp = a;
+                }
+                osp = S.osp_at[lp];
+                const int32_t a = S.psp_at[lp];
+                for (int32_t k = a + lane; k < psp; k += kWave) {
+                    const uint32_t e = S.pst[k];
+                    buf[e & 0xffffu] = (char)(e >> 16);
+                }
+                psp = a;
+            }
+            dfs_apply<true>(d, S, lp, len, c0, lane, psp, osp, true, f);
+        } else {
+            // rebuild: the consensus again, the whole path, nothing pushed
+            dfs_copy_in(d, S, c0, n, lane);
+            __syncthreads();
+            dfs_apply<false>(d, S, 0, len, c0, lane, psp, osp, false, f);
+        }
+        prev_len = len;
+        if (i + 1 < i1) {   // the next leaf's first entering chunk, in flight through the write-out
+            len = S.llen[i + 1 - i0];
+            lp = S.llp[i + 1 - i0];
+            dfs_prefetch(d, S, next_u, min(kWave, len - lp), c0, lane, f);
+        }
+        dfs_write_out(d, S, i - i0, t, c0, n, lane);
+    }
+}
+
 // getCodeFromNucleotide (src/panman.cpp:78-113) for the replayed characters; the reroot
 // driver turns '-' and the 'x' sentinel into state 1 = code 0 (src/reroot.cpp:176-181).
 __device__ __forceinline__ uint32_t code_of_char(char ch) {
@@ -561,8 +908,12 @@ hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     if (d.leaves == 0) return hipSuccess;
     timer_begin(c, 3);
     const unsigned groups = (unsigned)((d.tiles + kReplayGroup - 1) / kReplayGroup);
-    const size_t ring_bytes = (size_t)3 * d.ring * sizeof(int2);
-    hipLaunchKernelGGL(k_replay, dim3((unsigned)d.leaves, groups), dim3(256), ring_bytes, c->stream, d);
+    if (d.dfs) {
+        hipLaunchKernelGGL(k_replay_dfs, dim3((unsigned)((int64_t)d.groups * d.tiles)), dim3(kWave), 0, c->stream, d);
+    } else {
+        const size_t ring_bytes = (size_t)3 * d.ring * sizeof(int2);
+        hipLaunchKernelGGL(k_replay, dim3((unsigned)d.leaves, groups), dim3(256), ring_bytes, c->stream, d);
+    }
     timer_end(c, 3);
     return hipGetLastError();
 }

@@ -1,2 +1,2 @@
 set -o pipefail
-tools/replay_variants.sh base epl1 epl2 base epl1 epl2 && TREE=sars-like tools/replay_variants.sh base epl1 epl2
+tools/replay_variants.sh base dfstm dfsne dfst8 base && TREE=sars-like tools/replay_variants.sh base dfst8
