@@ -616,9 +616,6 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     dn.vinner = dt.vinner;
-    // leaf-parent children's leaves side by side (every leaf present: build_sub_planes)
-    dn.pair_planes = c->leaves_all_present && c->sub_planes_ok ? c->pair_planes : nullptr;
-    dn.vbase = c->ht.vbase;
     if (sub_down) {   // the S children's leaf words and node ids (their tail descriptors)
         dn.tail = dt.tail_desc_k;
         dn.num_s = ht.num_tail_s;

@@ -108,8 +108,6 @@ void free_columns(pm_ctx* c) {
     dev_free(c->sub_planes);
     c->sub_planes_bytes = 0;
     c->sub_planes_ok = false;
-    dev_free(c->pair_planes);
-    c->pair_planes_bytes = 0;
     c->has_leaves = c->has_sites = c->has_forced = false;
     c->ran = false;
 }
@@ -232,7 +230,7 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
                               (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
                               (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
                               (uint64_t)(uintptr_t)c->root_code, (uint64_t)(uintptr_t)c->shard_cnt,
-                              (uint64_t)(uintptr_t)c->sub_planes, (uint64_t)(uintptr_t)c->pair_planes,
+                              (uint64_t)(uintptr_t)c->sub_planes,
                               (uint64_t)(uintptr_t)c->dt.child_off, (uint64_t)(uintptr_t)c->stream};
     uint64_t h = 1469598103934665603ull;
     for (uint64_t v : parts) h = (h ^ v) * 1099511628211ull;
@@ -342,24 +340,6 @@ int build_sub_planes(pm_ctx* c) {
     // (only the subtree form reads it, and that form needs every leaf present)
     if (c->sub_planes_ok || !c->has_tree || !c->has_leaves || !c->leaves_all_present) return PM_OK;
     hipError_t e = hipSuccess;
-#ifndef PM_NO_PAIRS
-    // leaf-parent pairs (pm_ctx::pair_planes)
-    const int64_t nv = (int64_t)c->dt.num_internal - c->ht.vbase;
-    const size_t need_p = c->ht.vbase >= 0 && nv > 0 ? (size_t)nv * (size_t)wpad_of(c) * 2 * sizeof(uint4) : 0;
-    if (need_p > c->pair_planes_bytes) {
-        dev_free(c->pair_planes);
-        c->pair_planes_bytes = 0;
-        if ((e = malloc_or_release(c, reinterpret_cast<void**>(&c->pair_planes), need_p)) != hipSuccess)
-            return fail(c, PM_ERR_OOM, std::string("leaf-parent layout: ") + hipGetErrorString(e));
-        c->pair_planes_bytes = need_p;
-    }
-    if (need_p > 0) {
-        PhaseClock clock;
-        if ((e = launch_pair_planes(c)) != hipSuccess) return hip_fail(c, e, "leaf-parent layout");
-        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "leaf-parent layout");
-        clock.lap("upload.pair_planes");
-    }
-#endif
     if (c->ht.num_tail_s == 0) {
         c->sub_planes_ok = true;
         return PM_OK;
@@ -771,10 +751,6 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             virt[d] = all_leaves;
             ht.num_virtual += all_leaves;
         }
-        // (the dense numbering puts them last: one range, the leaf-parent pairs' index)
-        ht.vbase = I - (int32_t)ht.num_virtual;
-        for (int32_t d = std::max(ht.vbase, 0); d < I && ht.vbase >= 0; ++d)
-            if (!virt[d]) ht.vbase = -1;
         for (auto& x : child_enc_v)
             if (x >= 0 && virt[x]) x |= kVirtualBit;
         for (int32_t d = 0; d < I; ++d)

@@ -300,7 +300,7 @@ int pm_memory_footprint(pm_ctx* c, int64_t* out, int n) {
     int64_t v[12] = {0};
     if (c->leaf_planes) v[1] += L * wpad * (int64_t)sizeof(uint4) + L;   // code planes + flags
     if (c->leaf_present) v[1] += L * wpad * (int64_t)sizeof(uint32_t);
-    v[2] = (int64_t)c->sub_planes_bytes + (int64_t)c->pair_planes_bytes;
+    v[2] = (int64_t)c->sub_planes_bytes;
     v[3] = (int64_t)c->sets_bytes;
     v[4] = (int64_t)(c->cmask_bytes + c->upm_bytes);   // (mask records + up slots)
     v[5] = (int64_t)c->sk_parts_bytes;

@@ -183,7 +183,6 @@ struct HostTree {
     int32_t num_tail_k = 0;
     int32_t num_tail_s = 0;               // subtree form: the first num_tail_s tail items are the S2 / S3 nodes
     int32_t sbase = -1;                   // ... dense indices sbase + item
-    int32_t vbase = -1;                   // virtual leaf-parents: dense indices [vbase, num_internal)
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form,
     // (up only) its Fitch groups, its Sankoff groups
     int64_t lvl_up[5] = {0, 0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
@@ -255,12 +254,7 @@ struct pm_ctx {
     // reads a subtree's leaves at scattered lanes draws one 64-B sector per lane, not four
     uint4* sub_planes = nullptr;
     size_t sub_planes_bytes = 0;
-    bool sub_planes_ok = false;   // (with pair_planes)
-    // every leaf present: each virtual leaf-parent's (one or) two leaf words side by side
-    // ([num_virtual][wpad][2] uint4, dense index vbase + pair), so the pre-order's reads of a
-    // leaf-parent child at its scattered dirty lanes draw one sector per lane instead of two
-    uint4* pair_planes = nullptr;
-    size_t pair_planes_bytes = 0;
+    bool sub_planes_ok = false;
     int32_t* score = nullptr;         // [S]
     uint8_t* root_code = nullptr;     // [S]
     bool ran = false;
@@ -327,7 +321,6 @@ hipError_t launch_pack_sites(pm_ctx* c, const uint8_t* d_codes4, uint4* dst);
 hipError_t launch_synth(pm_ctx* c, int64_t site_begin, uint64_t seed);
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out);
 hipError_t launch_sub_planes(pm_ctx* c);
-hipError_t launch_pair_planes(pm_ctx* c);
 hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t ns, uint8_t* d_out);
 void free_replay(pm_ctx* c);
 void comm_release(pm_ctx* c);   // pm_rccl.hip
@@ -414,7 +407,10 @@ constexpr int64_t kDfsTile = PM_DFS_TILE;
 #define PM_DFS_LEAVES 16
 #endif
 constexpr int32_t kDfsLeaves = PM_DFS_LEAVES;
-constexpr int32_t kDfsUnionCap = 128;
+#ifndef PM_DFS_UNION
+#define PM_DFS_UNION 128
+#endif
+constexpr int32_t kDfsUnionCap = PM_DFS_UNION;
 
 // FASTA formatting on the device (printSequenceLinesNew, src/fasta.cpp:155-254): one
 // segment per (leaf, print position) -- a block read forward or reverse-complemented from

@@ -834,8 +834,6 @@ struct DownArgs {
     int32_t num_s;         // k_tail (subtree form): items [0, num_s) are the S2 / S3 nodes ...
     int32_t sbase;         // ... of dense index sbase + item
     const uint4* sub_planes;   // ... whose leaves sit side by side there (sub_word)
-    const uint4* pair_planes;  // (nullable) virtual leaf-parents' leaf words side by side, ...
-    int32_t vbase;             // ... pair = dense index - vbase
 };
 
 template <class Args>
@@ -1093,19 +1091,7 @@ __device__ __forceinline__ void kid_fetch(const DownArgs& a, int32_t enc, int4 v
     }
     k.L0 = k.L1 = make_uint4(0, 0, 0, 0);
     k.m0 = k.m1 = 0;
-    if (AP && M != Mode::kBlockFitch && a.pair_planes != nullptr && enc >= 0 && (enc & kVirtualBit) &&
-        !(SUB && kid_shape(enc))) {
-        // a leaf-parent: both leaves' words from one 32-B slot (one sector per dirty lane)
-        const uint4* q = a.pair_planes + ((size_t)((enc & kDenseMask) - a.vbase) * a.wpad + word) * 2;
-        if (dirty) {
-            k.L0 = q[0];
-            k.m0 = ~0u;
-        }
-        if (l1 >= 0 && dirty) {
-            k.L1 = q[1];
-            k.m1 = ~0u;
-        }
-    } else if (AP) {
+    if (AP) {
         if (l0 >= 0 && dirty) {
             k.L0 = a.leaf_planes[(size_t)l0 * a.wpad + word];
             k.m0 = ~0u;

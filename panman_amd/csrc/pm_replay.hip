@@ -429,7 +429,10 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay(ReplayDev d) {
 // with the consensus at write-out.  A leaf whose edits would overflow a stack rebuilds its
 // row (consensus copy-in, whole path, nothing pushed), as do the group's later leaves.
 static_assert(kDfsLeaves <= kWave && kDfsUnionCap <= 256, "k_replay_dfs: a lane per leaf, u8 group node indices");
-constexpr int kDfsPCap = 384;   // plain edits on the current path in one tile
+#ifndef PM_DFS_PCAP
+#define PM_DFS_PCAP 384
+#endif
+constexpr int kDfsPCap = PM_DFS_PCAP;   // plain edits on the current path in one tile
 constexpr int kDfsOCap = 64;    // overriding edits on the current path in one tile
 
 struct DfsLds {
@@ -671,6 +674,148 @@ __device__ __forceinline__ void dfs_copy_in(const ReplayDev& d, DfsLds& S, int64
     }
 }
 
+// Small transitions (the common case: at most kFastNodes entering nodes, each with at most
+// kFastEdits plain and overriding edits in the tile): lane = (node k, edit j) with k = lane /
+// kFastEdits, so the edits come with one load per lane and no prefix scan or binary search
+// (the general path, dfs_apply, costs ~100 VALU instructions per round; the kernel is issue-
+// bound: r05 SQ counters, 27 % of wave cycles issuing at ~4 waves per SIMD).
+constexpr int kFastEdits = 16, kFastNodes = kWave / kFastEdits;
+
+struct DfsFast {
+    bool on;                  // (uniform) this transition is small
+    int4 b;                   // this lane's node's bounds
+    uint32_t cp, hp, co, ho;  // this lane's plain / overriding edit (column, char); kNoCol: none
+};
+constexpr uint32_t kNoCol = ~0u;
+
+__device__ __forceinline__ void dfs_fast_prefetch(const ReplayDev& d, const DfsLds& S, int32_t u_lo, int32_t cnt, int lane,
+                                                  DfsFast& x) {
+    const int k = lane / kFastEdits, j = lane % kFastEdits;
+    x.b = make_int4(0, 0, 0, 0);
+    if (k < cnt) x.b = S.bnd[u_lo + k];
+    x.on = cnt <= kFastNodes && !__ballot(k < cnt && (x.b.y - x.b.x > kFastEdits || x.b.w - x.b.z > kFastEdits));
+    x.cp = x.co = kNoCol;
+    x.hp = x.ho = 0;
+    if (!x.on) return;
+    if (j < x.b.y - x.b.x) {
+        x.cp = d.edit_col[x.b.x + j];
+        x.hp = d.edit_chr[x.b.x + j];
+    }
+    if (j < x.b.w - x.b.z) {
+        x.co = d.edit_col[x.b.z + j];
+        x.ho = d.edit_chr[x.b.z + j];
+    }
+}
+
+// Per-node counts of a small transition (lane k * kFastEdits holds node k's): the exclusive
+// prefix for this lane's node and the totals.
+__device__ __forceinline__ void fast_prefix(int32_t len, int lane, int32_t& pre, int32_t& total) {
+    const int32_t l0 = __builtin_amdgcn_readlane(len, 0), l1 = __builtin_amdgcn_readlane(len, kFastEdits),
+                  l2 = __builtin_amdgcn_readlane(len, 2 * kFastEdits), l3 = __builtin_amdgcn_readlane(len, 3 * kFastEdits);
+    const int k = lane / kFastEdits;
+    pre = k == 0 ? 0 : k == 1 ? l0 : k == 2 ? l0 + l1 : l0 + l1 + l2;
+    total = l0 + l1 + l2 + l3;
+}
+
+// Apply a small transition's entering positions [lp, lp + cnt): plain edits (pushed), then the
+// overriding ones node by node in path order (pushed).
+__device__ __forceinline__ void dfs_fast_apply(DfsLds& S, const DfsFast& x, int32_t lp, int32_t cnt, int64_t c0, int lane,
+                                               int32_t& psp, int32_t& osp) {
+    char* buf = reinterpret_cast<char*>(S.tile);
+    const int k = lane / kFastEdits, j = lane % kFastEdits;
+    int32_t pre, tot, opre, otot;
+    fast_prefix(k < cnt ? x.b.y - x.b.x : 0, lane, pre, tot);
+    fast_prefix(k < cnt ? x.b.w - x.b.z : 0, lane, opre, otot);
+    if (j == 0 && k < cnt) {
+        S.psp_at[lp + k] = (uint16_t)(psp + pre);
+        S.osp_at[lp + k] = (uint16_t)(osp + opre);
+    }
+    if (x.cp != kNoCol) {
+        const uint32_t col = x.cp - (uint32_t)c0;
+        S.pst[psp + pre + j] = col | (uint32_t)(uint8_t)buf[col] << 16;
+        buf[col] = (char)(x.hp & 0x7fu);
+    }
+    psp += tot;
+    if (otot > 0) {   // (uniform) in path order: node k after node k - 1
+        for (int kk = 0; kk < cnt; ++kk) {
+            if (k == kk && x.co != kNoCol) {
+                const uint32_t col = x.co - (uint32_t)c0;
+                S.ost[osp + opre + j] = col | (uint32_t)(uint8_t)buf[col] << 16;
+                buf[col] = (char)(x.ho & 0x7fu);
+            }
+        }
+        osp += otot;
+    }
+}
+
+struct DfsState {
+    int32_t psp, osp, prev_len, next_u, len, lp;   // stacks, previous path length, next group node, this leaf's path
+    bool rebuild;
+};
+
+// Leaf i of the group: its transition (cur: the fast one, prefetched two leaves ahead; or f:
+// the general one, prefetched one leaf ahead), its write-out; meanwhile leaf i + 1's general
+// prefetch (when nxt, its fast one, does not apply) and leaf i + 2's fast one (into cur).
+__device__ __forceinline__ void dfs_leaf(const ReplayDev& d, DfsLds& S, DfsState& st, int32_t i, int32_t i0, int32_t i1,
+                                         int32_t t, int64_t c0, int64_t n, int lane, DfsPrefetch& f, DfsFast& cur,
+                                         const DfsFast& nxt) {
+    const int32_t len = st.len, lp = st.lp;
+    // the path positions [lp, len) are new group nodes next_u ..
+    for (int32_t p = lp + lane; p < len; p += kWave) S.cur_u[p] = (uint8_t)(st.next_u + (p - lp));
+    st.next_u += len - lp;
+    char* buf = reinterpret_cast<char*>(S.tile);
+#ifndef PM_DFS_NOEDITS
+    int32_t np = 0, no = 0;
+    if (!st.rebuild) {
+        if (cur.on) {   // (the counts from the prefetched bounds)
+            int32_t pre;
+            fast_prefix(lane / kFastEdits < len - lp ? cur.b.y - cur.b.x : 0, lane, pre, np);
+            fast_prefix(lane / kFastEdits < len - lp ? cur.b.w - cur.b.z : 0, lane, pre, no);
+        } else {
+            dfs_counts(S, lp, len, lane, np, no);
+        }
+        const int32_t psp_x = lp < st.prev_len ? (int32_t)S.psp_at[lp] : st.psp;
+        const int32_t osp_x = lp < st.prev_len ? (int32_t)S.osp_at[lp] : st.osp;
+        st.rebuild = psp_x + np > kDfsPCap || osp_x + no > kDfsOCap;
+    }
+    if (!st.rebuild) {
+        // exit: overriding frames deepest first, then the plain entries above lp
+        if (lp < st.prev_len) {
+            for (int32_t p = st.prev_len - 1; p >= lp && st.osp > (int32_t)S.osp_at[lp]; --p) {
+                const int32_t a = S.osp_at[p];
+                for (int32_t k = a + lane; k < st.osp; k += kWave) {
+                    const uint32_t e = S.ost[k];
+                    buf[e & 0xffffu] = (char)(e >> 16);
+                }
+                st.osp = a;
+            }
+            st.osp = S.osp_at[lp];
+            const int32_t a = S.psp_at[lp];
+            for (int32_t k = a + lane; k < st.psp; k += kWave) {
+                const uint32_t e = S.pst[k];
+                buf[e & 0xffffu] = (char)(e >> 16);
+            }
+            st.psp = a;
+        }
+        if (cur.on) dfs_fast_apply(S, cur, lp, len - lp, c0, lane, st.psp, st.osp);
+        else dfs_apply<true>(d, S, lp, len, c0, lane, st.psp, st.osp, true, f);
+    } else {
+        // rebuild: the consensus again, the whole path, nothing pushed
+        dfs_copy_in(d, S, c0, n, lane);
+        __syncthreads();
+        dfs_apply<false>(d, S, 0, len, c0, lane, st.psp, st.osp, false, f);
+    }
+#endif
+    st.prev_len = len;
+    if (i + 1 < i1) {
+        st.len = S.llen[i + 1 - i0];
+        st.lp = S.llp[i + 1 - i0];
+        if (!nxt.on) dfs_prefetch(d, S, st.next_u, min(kWave, st.len - st.lp), c0, lane, f);
+        if (i + 2 < i1) dfs_fast_prefetch(d, S, st.next_u + (st.len - st.lp), S.llen[i + 2 - i0] - S.llp[i + 2 - i0], lane, cur);
+    }
+    dfs_write_out(d, S, i - i0, t, c0, n, lane);
+}
+
 // waves per SIMD (the second __launch_bounds__ argument is amdgpu_waves_per_eu): 4 = 128 VGPRs
 #ifndef PM_DFS_WAVES
 #define PM_DFS_WAVES 4
@@ -698,64 +843,18 @@ __global__ __launch_bounds__(kWave, PM_DFS_WAVES) void k_replay_dfs(ReplayDev d)
     dfs_copy_in(d, S, c0, n, lane);
     dfs_leaf_tables(d, S, i0, i1 - i0, t, c0, n, lane);
     __syncthreads();   // (one wave: the copy-in and the tables landed)
-    int32_t psp = 0, osp = 0, prev_len = 0, next_u = 0;
-    bool rebuild = false;
+    DfsState st{0, 0, 0, 0, S.llen[0], 0, false};
     DfsPrefetch f;
-    int32_t len = S.llen[0], lp = 0;
-    dfs_prefetch(d, S, 0, min(kWave, len), c0, lane, f);
-    for (int32_t i = i0; i < i1; ++i) {
-        // the path positions [lp, len) are new group nodes next_u ..
-        for (int32_t p = lp + lane; p < len; p += kWave) S.cur_u[p] = (uint8_t)(next_u + (p - lp));
-        next_u += len - lp;
-        int32_t np = 0, no = 0;
-#ifdef PM_DFS_NOEDITS   // timing experiments only: the rows are the consensus
-        if (true) {
-            prev_len = len;
-            dfs_write_out(d, S, i - i0, t, c0, n, lane);
-            if (i + 1 < i1) { len = S.llen[i + 1 - i0]; lp = S.llp[i + 1 - i0]; }
-            continue;
-        }
-#endif
-        if (!rebuild) {
-            dfs_counts(S, lp, len, lane, np, no);
-            const int32_t psp_x = lp < prev_len ? (int32_t)S.psp_at[lp] : psp;
-            const int32_t osp_x = lp < prev_len ? (int32_t)S.osp_at[lp] : osp;
-            rebuild = psp_x + np > kDfsPCap || osp_x + no > kDfsOCap;
-        }
-        char* buf = reinterpret_cast<char*>(S.tile);
-        if (!rebuild) {
-            // exit: overriding frames deepest first, then the plain entries above lp
-            if (lp < prev_len) {
-                for (int32_t p = prev_len - 1; p >= lp && osp > (int32_t)S.osp_at[lp]; --p) {
-                    const int32_t a = S.osp_at[p];
-                    for (int32_t k = a + lane; k < osp; k += kWave) {
-                        const uint32_t e = S.ost[k];
-                        buf[e & 0xffffu] = (char)(e >> 16);
-                    }
-                    osp = a;
-                }
-                osp = S.osp_at[lp];
-                const int32_t a = S.psp_at[lp];
-                for (int32_t k = a + lane; k < psp; k += kWave) {
-                    const uint32_t e = S.pst[k];
-                    buf[e & 0xffffu] = (char)(e >> 16);
-                }
-                psp = a;
-            }
-            dfs_apply<true>(d, S, lp, len, c0, lane, psp, osp, true, f);
-        } else {
-            // rebuild: the consensus again, the whole path, nothing pushed
-            dfs_copy_in(d, S, c0, n, lane);
-            __syncthreads();
-            dfs_apply<false>(d, S, 0, len, c0, lane, psp, osp, false, f);
-        }
-        prev_len = len;
-        if (i + 1 < i1) {   // the next leaf's first entering chunk, in flight through the write-out
-            len = S.llen[i + 1 - i0];
-            lp = S.llp[i + 1 - i0];
-            dfs_prefetch(d, S, next_u, min(kWave, len - lp), c0, lane, f);
-        }
-        dfs_write_out(d, S, i - i0, t, c0, n, lane);
+    DfsFast xa, xb;
+    xa.on = false;   // (the first leaf: its whole path, the general path)
+    dfs_prefetch(d, S, 0, min(kWave, st.len), c0, lane, f);
+    xb.on = false;
+    if (i0 + 1 < i1) dfs_fast_prefetch(d, S, st.len, S.llen[1] - S.llp[1], lane, xb);
+    // two leaves per trip, the roles of the two transition buffers swapped by the code rather
+    // than by register moves (a move of a load's destination would wait for the load)
+    for (int32_t i = i0; i < i1; i += 2) {
+        dfs_leaf(d, S, st, i, i0, i1, t, c0, n, lane, f, xa, xb);
+        if (i + 1 < i1) dfs_leaf(d, S, st, i + 1, i0, i1, t, c0, n, lane, f, xb, xa);
     }
 }
 

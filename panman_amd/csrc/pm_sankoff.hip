@@ -641,9 +641,6 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.absent_code0 = block;
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
-    // leaf-parent children's leaves side by side (every leaf present: build_sub_planes)
-    dn.pair_planes = c->leaves_all_present && c->sub_planes_ok ? c->pair_planes : nullptr;
-    dn.vbase = c->ht.vbase;
     dn.vinner = dt.vinner;
     const int D = (int)down_off.size() - 1;
     // a pre-order level = one range of dense indices: [down_off[d], down_off[d+1]) in the

@@ -258,29 +258,6 @@ hipError_t launch_sub_planes(pm_ctx* c) {
     return hipGetLastError();
 }
 
-// Leaf-parent pairs (pm_ctx::pair_planes): thread = (pair, word), the virtual node's one or two
-// leaf words side by side.
-__global__ __launch_bounds__(256) void k_pair_planes(const int4* vleaf, int32_t vbase, int64_t pairs,
-                                                     const uint4* leaf_planes, int64_t wpad, uint4* out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= pairs * wpad) return;
-    const int64_t pair = i / wpad, word = i - pair * wpad;
-    const int4 vl = vleaf[vbase + pair];
-    uint4* o = out + (size_t)i * 2;
-    o[0] = vl.x >= 0 ? leaf_planes[(size_t)vl.x * wpad + word] : make_uint4(0, 0, 0, 0);
-    o[1] = vl.y >= 0 ? leaf_planes[(size_t)vl.y * wpad + word] : make_uint4(0, 0, 0, 0);
-}
-
-hipError_t launch_pair_planes(pm_ctx* c) {
-    const int64_t wpad = (int64_t)((c->words + kWave - 1) / kWave) * kWave;
-    const int64_t pairs = (int64_t)c->dt.num_internal - c->ht.vbase;
-    if (c->ht.vbase < 0 || pairs <= 0) return hipSuccess;
-    const int64_t n = pairs * wpad;
-    hipLaunchKernelGGL(k_pair_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
-                       reinterpret_cast<const int4*>(c->dt.vleaf), c->ht.vbase, pairs, c->leaf_planes, wpad, c->pair_planes);
-    return hipGetLastError();
-}
-
 hipError_t launch_unpack_leaf_codes(pm_ctx* c, int64_t s0, int64_t ns, uint8_t* d_out) {
     const int64_t wpad = (int64_t)((c->words + kWave - 1) / kWave) * kWave;
     const int64_t n = (int64_t)c->dt.num_leaves * ns;
