@@ -746,8 +746,13 @@ def replay_block(args, world, rank, local):
     lo, hi = shard_range(rank, world, len(leaf_nodes))
     eng = panman_amd.Engine(local)
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    panman_amd.phase_reset()
     eng.replay_prepare(pm, (lo, hi) if world > 1 else None)
     leaves, cols, edits = eng.replay_shape()
+    prep = dict(panman_amd.phase_report())
+    # the kernel launch_replay picks: depth-first leaf groups when every path fits, else k_replay
+    kernel = "k_replay_dfs" if prep.get("replay.dfs_groups", 0) > 0 else "k_replay"
+    dfs_groups = int(prep.get("replay.dfs_groups", 0))
     log(rank, f"[bench] replay PanMAT {leaves} of {total_leaves} leaves x {cols} columns, {edits} edits "
               f"({time.time() - t0:.1f}s)")
     for _ in range(max(1, args.warmup)):
@@ -790,9 +795,11 @@ def replay_block(args, world, rank, local):
             acc[v] += acc[parent[v]]
     path_recs = float(acc[leaf_nodes[lo:hi]].sum())
     # bytes the replay must move: every row byte written once, the consensus row read once
-    # (it stays cache-resident across leaves), 5 B (column u32 + char) per edit on each
-    # leaf's root-to-leaf path
-    alg_bytes = units + float(cols) + 5.0 * path_recs
+    # (it stays cache-resident across leaves), 5 B (column u32 + char) per distinct edit (the
+    # depth-first kernel reads an edit once per leaf group, not once per leaf below it; round 4
+    # counted 5 B per edit on each leaf's path, `path_model_bytes` below)
+    alg_bytes = units + float(cols) + 5.0 * float(edits)
+    path_model_bytes = units + float(cols) + 5.0 * path_recs
     kms = ms[3] / args.steps
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     # host formatting (aligned FASTA of every leaf)
@@ -826,11 +833,11 @@ def replay_block(args, world, rank, local):
                "sample": f"first {k} leaves by name, aligned FASTA, oracle printFASTAUltraFast restatement "
                          f"({secs:.1f}s on {threads} threads, leaves in parallel as the reference's "
                          f"tbb::parallel_for_each over leaves, src/fasta.cpp:1993)"}
-    # PMC-measured HBM bytes per k_replay_piped launch (tools/pmc_traffic.py, key replay:LxC)
+    # PMC-measured HBM bytes per replay launch (tools/pmc_traffic.py, key replay:LxC)
     traffic, traffic_note = None, "no PMC traffic for this workload"
     if os.path.exists(args.traffic):
         try:
-            entry = json.load(open(args.traffic)).get("k_replay_piped", {})
+            entry = json.load(open(args.traffic)).get(kernel, {})
             key = f"replay:{leaves}x{cols}"
             if key in entry and entry.get(key + ":build") == panman_amd.build_id():
                 traffic = entry[key]
@@ -851,10 +858,12 @@ def replay_block(args, world, rank, local):
                    "leaves": total_leaves, "leaves_per_gpu": leaves, "columns": cols,
                    "path_mutation_records_rank0": path_recs,
                    "parallelism": f"leaf shards x{world}, tree + mutations replicated, no collective"},
-        "roofline": {"bound": "hbm", "kernel": "k_replay_piped", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_note": traffic_note, "design_bytes_per_launch": alg_bytes,
-                     "bytes_model": "row bytes written once + consensus row once + 5 B per path edit",
+                     "bytes_model": "row bytes written once + consensus row once + 5 B per distinct edit",
+                     "path_model_frac": round(path_model_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "leaf_groups": dfs_groups,
                      "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,
                      "avg_launch_ms": round(kms, 4), "launches_per_step": launches[3] / args.steps},
         "host_format_s": round(fmt_s, 3),

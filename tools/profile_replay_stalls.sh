@@ -11,7 +11,7 @@ pass() {  # NAME COUNTERS...
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- python3 bench.py --no-cpu --mode replay --steps 2 --warmup 1 \
     > "$out/$name.json" 2> "$out/$name.log" || { echo "pass $name failed"; tail -5 "$out/$name.log"; return 1; }
-  python3 tools/pmc_summary.py "$out/$name" | grep -A12 "^k_replay_piped" > "$out/$name.txt" || true
+  python3 tools/pmc_summary.py "$out/$name" | grep -A12 "^k_replay" > "$out/$name.txt" || true
   echo "== $name"; cat "$out/$name.txt"
 }
 pass tcc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_avr || exit 2
