@@ -79,6 +79,10 @@ typedef struct pm_mut {
 /* Context / device (replaces the device setup of gpu/fitchSankoff.cu:370-440). */
 int pm_create(int device, pm_ctx** out);
 void pm_destroy(pm_ctx* ctx);
+/* Initialise the HIP runtime on `device` and load the library's code objects (what the
+ * first pm_create and first launches would otherwise pay), from any thread: a caller with
+ * host work to do first (reading and decoding input) can overlap it.  Optional. */
+int pm_warmup(int device);
 const char* pm_last_error(const pm_ctx* ctx);
 /* Queue all work on `hip_stream` (a hipStream_t; NULL = the ctx's own stream). */
 int pm_set_stream(pm_ctx* ctx, void* hip_stream);

@@ -735,5 +735,11 @@ hipError_t launch_score(pm_ctx* c) {
     return hipGetLastError();
 }
 
+// This file's code object, loaded ahead of its first launch (pm_warmup).
+hipError_t warm_fitch() {
+    hipFuncAttributes at;
+    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_site_score));
+}
+
 }  // namespace pm
 

@@ -418,6 +418,26 @@ int pm_create(int device, pm_ctx** out) {
     return PM_OK;
 }
 
+int pm_warmup(int device) {
+    PhaseClock clock;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return PM_ERR_HIP;
+    if (device < 0 || device >= n) return PM_ERR_ARG;
+    if ((e = hipSetDevice(device)) != hipSuccess) return PM_ERR_HIP;
+    for (auto warm : {warm_fitch, warm_sankoff, warm_replay, warm_synth, warm_sort})
+        if ((e = warm()) != hipSuccess) return PM_ERR_HIP;
+    // the runtime's first allocation and staged copies
+    void* d = nullptr;
+    uint8_t h[4096] = {0};
+    if ((e = hipMalloc(&d, sizeof h)) != hipSuccess) return PM_ERR_HIP;
+    e = hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    clock.lap("hip.warmup");
+    return e == hipSuccess ? PM_OK : PM_ERR_HIP;
+}
+
 void pm_destroy(pm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);

@@ -309,6 +309,12 @@ void timer_end(pm_ctx* c, int cls);
 hipError_t launch_fitch(pm_ctx* c, bool block);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
 // Records of the last run, sorted by (node, site) on the device, copied to host `out`.
+// pm_warmup: one kernel of each code object looked up, so the object is loaded
+hipError_t warm_fitch();
+hipError_t warm_sankoff();
+hipError_t warm_replay();
+hipError_t warm_synth();
+hipError_t warm_sort();
 hipError_t sort_records_to_host(pm_ctx* c, const std::vector<uint32_t>& counts, int64_t n, pm_mut* out);
 // (Re)build the S2 / S3 leaf layout after the leaf columns or the tree changed (no-op when
 // it is current or the tree has no S2 / S3 node).

@@ -251,19 +251,29 @@ bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out,
 // (match finder, nice length, lc / lp / pb) with the dictionary cut to the data it can
 // reach -- a dictionary larger than the input (or than one block) finds nothing more, but
 // the level-9 encoder initialises all 64 MiB of it, which dominated writing a small PanMAN.
-// Messages above 256 KiB go through liblzma's multi-threaded encoder in independent blocks
-// of a FIXED size (kXzBlock; the bytes written do not depend on the machine's core count):
-// still one standard .xz stream that any xz decoder (the reference's boost lzma filter
-// included) reads back to the same bytes.  PM_XZ_THREADS=1 forces one block (what the
-// reference writes); PM_XZ_BLOCK sets the block size; the thread count only sets how many
-// blocks are encoded at once.
+// Messages above one block go through liblzma's multi-threaded encoder in independent
+// blocks whose size depends on the message size only (xz_block_size; the bytes written do
+// not depend on the machine's core count): still one standard .xz stream that any xz decoder
+// (the reference's boost lzma filter included) reads back to the same bytes.  Level 9 encodes
+// PanMAN messages at ~2 MB/s a thread, so a message of a few hundred KiB (a 2 000-leaf PanMAN)
+// is cut into >= 16 blocks of >= 64 KiB (+3-6 % of file size against one block), a large one
+// into 1 MiB blocks.  PM_XZ_THREADS=1 forces one block (what the reference writes);
+// PM_XZ_BLOCK sets the block size; the thread count only sets how many blocks are encoded at
+// once.
 constexpr uint64_t kXzBlock = (uint64_t)1 << 20;
+constexpr uint64_t kXzMinBlock = (uint64_t)1 << 16;
+
+uint64_t xz_block_size(size_t n) {
+    uint64_t b = kXzMinBlock;
+    while (b < kXzBlock && b * 16 < n) b <<= 1;
+    return b;
+}
 
 bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string& err) {
     pm_lzma_stream s{};
     bool one_block = false;
     if (const char* e = std::getenv("PM_XZ_THREADS")) one_block |= std::atoi(e) <= 1;
-    uint64_t block = kXzBlock;
+    uint64_t block = xz_block_size(n);
     if (const char* e = std::getenv("PM_XZ_BLOCK")) block = std::max<uint64_t>(4096, std::strtoull(e, nullptr, 10));
     if ((n + block - 1) / block <= 1) one_block = true;
     const int threads = one_block ? 1 : (int)std::max<uint64_t>(2, std::min<uint64_t>((uint64_t)host_threads(), (n + block - 1) / block));

@@ -1017,4 +1017,10 @@ hipError_t launch_replay(pm_ctx* c, const ReplayDev& d) {
     return hipGetLastError();
 }
 
+// This file's code object, loaded ahead of its first launch (pm_warmup).
+hipError_t warm_replay() {
+    hipFuncAttributes at;
+    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fmt_count));
+}
+
 }  // namespace pm

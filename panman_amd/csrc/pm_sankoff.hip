@@ -724,4 +724,10 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     return hipGetLastError();
 }
 
+// This file's code object, loaded ahead of its first launch (pm_warmup).
+hipError_t warm_sankoff() {
+    hipFuncAttributes at;
+    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_sankoff_up_wide<4>));
+}
+
 }  // namespace pm

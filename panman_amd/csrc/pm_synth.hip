@@ -273,4 +273,10 @@ hipError_t launch_unpack_sites(pm_ctx* c, const uint4* src, int64_t s0, int64_t 
     return hipGetLastError();
 }
 
+// This file's code object, loaded ahead of its first launch (pm_warmup).
+hipError_t warm_synth() {
+    hipFuncAttributes at;
+    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_pack_sites));
+}
+
 }  // namespace pm

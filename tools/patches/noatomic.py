@@ -3,7 +3,7 @@
 import sys
 p = sys.argv[1] + "/pm_kernels.h"
 s = open(p).read()
-old = "    if (lane == 0) base = atomicAdd(&a.shard_cnt[em.shard], total);\n"
+old = "    if (lane == 0) got = atomicAdd(&a.shard_cnt[em.shard], total);\n"
 assert old in s
-s = s.replace(old, "    base = (em.shard * 977u) % (uint32_t)(a.shard_cap > 4096 ? a.shard_cap - 4096 : 1);\n")
+s = s.replace(old, "    got = (em.shard * 977u) % (uint32_t)(a.shard_cap > 4096 ? a.shard_cap - 4096 : 1);\n")
 open(p, "w").write(s)
