@@ -250,6 +250,9 @@ const char* pm_build_id(void);
 /* Achievable HBM rate on `device`: a 16-B-per-lane streaming copy of `bytes` bytes, `reps`
  * times; *gbs = (read + write bytes) / s / 1e9. */
 int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs);
+/* The same for writes only (the replay rows' access pattern): 16 B per lane, 4 non-temporal
+ * stores in flight; *gbs = written bytes / s / 1e9. */
+int pm_stream_write_rate(int device, int64_t bytes, int reps, double* gbs);
 
 /* Phase log: the drivers (pm_fasta, pm_msa_build / pm_msa_to_panman*, pm_panman_load /
  * pm_panman_write, pm_create) append the wall time of each host / device phase of every

@@ -259,7 +259,7 @@ __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t re
     mx = __ballot(complex_word);
     ms = __ballot(!complex_word && !same);
     md = __ballot(complex_word || dirty_extra);
-    if (!complex_word && !same) p[lanes_below(ms)] = make_uint4(code[0], code[1], code[2], code[3]);
+    if (!complex_word && !same) store_stream(p + lanes_below(ms), make_uint4(code[0], code[1], code[2], code[3]));
     if (lane == 0) {
         cm[kMaskWords * rec] = mx;
         cm[kMaskWords * rec + 1] = ms;
@@ -362,7 +362,7 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+        for (int q = 0; q < 4; ++q) store_stream(p + kWave + q * kWave + k, make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]));
     }
 }
 
@@ -421,10 +421,10 @@ __device__ __forceinline__ void store_sankoff(uint4* sets, uint64_t* cmask, cons
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) p[kWave + q * kWave + k] = make_uint4(z0[4 * q], z0[4 * q + 1], z0[4 * q + 2], z0[4 * q + 3]);
+        for (int q = 0; q < 4; ++q) store_stream(p + kWave + q * kWave + k, make_uint4(z0[4 * q], z0[4 * q + 1], z0[4 * q + 2], z0[4 * q + 3]));
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            p[5 * kWave + q * kWave + k] = make_uint4(z1[4 * q], z1[4 * q + 1], z1[4 * q + 2], z1[4 * q + 3]);
+            store_stream(p + 5 * kWave + q * kWave + k, make_uint4(z1[4 * q], z1[4 * q + 1], z1[4 * q + 2], z1[4 * q + 3]));
     }
 }
 

@@ -36,6 +36,17 @@ __global__ __launch_bounds__(kBlock) void k_stream_copy(const uint4* __restrict_
     }
 }
 
+// Write-only streaming: 16 B per lane, kCopyUnroll non-temporal stores per thread (the
+// replay's row stores).
+__global__ __launch_bounds__(kBlock) void k_stream_write(uint4* __restrict__ dst, int64_t n, uint32_t tag) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * kCopyUnroll + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n) store_stream(dst + i, make_uint4((uint32_t)i, tag, (uint32_t)(i >> 32), ~tag));
+    }
+}
+
 // FETCH_SIZE calibration for scattered 16-B-per-lane reads (the pre-order's parent finals and
 // dirty-lane leaf words): thread i reads 16 B at i * stride, (i + n) * stride, ... (kGather
 // reads, each lane its own 16 B of a stride-spaced slot) and writes one coalesced 16-B XOR.
@@ -95,6 +106,38 @@ int pm_stream_copy_rate(int device, int64_t bytes, int reps, double* gbs) {
     if (s) (void)hipStreamDestroy(s);
     if (a) (void)hipFree(a);
     if (b) (void)hipFree(b);
+    return rc;
+}
+
+int pm_stream_write_rate(int device, int64_t bytes, int reps, double* gbs) {
+    if (!gbs || bytes < (1 << 20) || reps < 1) return PM_ERR_ARG;
+    *gbs = 0.0;
+    if (hipSetDevice(device) != hipSuccess) return PM_ERR_HIP;
+    const int64_t n = bytes / (int64_t)sizeof(uint4);
+    uint4* a = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = PM_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&a), n * sizeof(uint4)) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess) {
+        rc = PM_ERR_OOM;
+    } else {
+        const dim3 grid((unsigned)((n + (int64_t)kBlock * kCopyUnroll - 1) / ((int64_t)kBlock * kCopyUnroll)));
+        hipLaunchKernelGGL(k_stream_write, grid, dim3(kBlock), 0, s, a, n, 0u);   // warm-up (first touch)
+        (void)hipEventRecord(e0, s);
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_stream_write, grid, dim3(kBlock), 0, s, a, n, (uint32_t)r + 1);
+        (void)hipEventRecord(e1, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.f)
+            rc = PM_ERR_HIP;
+        else
+            *gbs = (double)n * sizeof(uint4) * reps / (ms * 1e-3) / 1e9;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    if (a) (void)hipFree(a);
     return rc;
 }
 

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay(ReplayDev d) {
 #pragma unroll
         for (int j = 0; j < kReplayTile / 16 / 256; ++j) {
             const int k = tid + 256 * j;
-            if (k < n / 16) dst[k] = tile_buf[k];
+            if (k < n / 16) store_stream(dst + k, tile_buf[k]);
         }
         lds_barrier();   // the tile buffer is refilled next
     }
@@ -549,7 +549,7 @@ __device__ __forceinline__ void dfs_write_out(const ReplayDev& d, DfsLds& S, int
                 v.w = (v.w & ~m[3]) | (cv.w & m[3]);
             }
         }
-        dst[k] = v;
+        store_stream(dst + k, v);
     }
 }
 
