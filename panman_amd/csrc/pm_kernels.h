@@ -1330,7 +1330,7 @@ __device__ __forceinline__ uint4 node_final(const DownArgs& a, int32_t node, int
 __device__ __forceinline__ void store_final(const DownArgs& a, bool is_root, uint4* p, const RecMask& m, int lane,
                                             int64_t word, const uint32_t* F) {
     if (is_root) a.root_final[word] = make_uint4(F[0], F[1], F[2], F[3]);
-    else if ((m.x >> lane) & 1ull) p[final_slot(m)] = make_uint4(F[0], F[1], F[2], F[3]);
+    else if ((m.x >> lane) & 1ull) store_stream(p + final_slot(m), make_uint4(F[0], F[1], F[2], F[3]));
 }
 
 // The node's final codes F (code planes) and the sites where it is resolved (pres), from
