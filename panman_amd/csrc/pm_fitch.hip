@@ -725,8 +725,8 @@ hipError_t launch_score(pm_ctx* c) {
     hipError_t e = hipMemsetAsync(c->score, 0, sizeof(int32_t) * c->num_sites, c->stream);
     if (e != hipSuccess) return e;
     const bool use_lds = c->num_sites * 4 <= 150 * 1024;
-    const int spb = 4;
-    const int blocks = kShards / spb;
+    const int spb = kShards >= 1024 ? kShards / 256 : 4;   // 256 workgroups
+    const int blocks = (kShards + spb - 1) / spb;
     const size_t lds = use_lds ? (size_t)c->num_sites * 4 : 0;
     timer_begin(c, 2);
     hipLaunchKernelGGL(k_site_score, dim3(blocks), dim3(kScoreBlock), lds, c->stream, c->recs, c->shard_cnt,

@@ -30,7 +30,10 @@ namespace pm {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kShards = 1024;
+#ifndef PM_SHARDS
+#define PM_SHARDS 1024
+#endif
+constexpr int kShards = PM_SHARDS;
 constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
 constexpr int kDegreeClasses = 4;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
