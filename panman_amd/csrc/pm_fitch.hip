@@ -194,7 +194,7 @@ __device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, in
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 w = p[kWave + q * kWave + k];
+                const uint4 w = load_stream(p + kWave + q * kWave + k);
                 f.w[4 * q] = w.x; f.w[4 * q + 1] = w.y; f.w[4 * q + 2] = w.z; f.w[4 * q + 3] = w.w;
             }
         } else {

@@ -173,6 +173,12 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+__device__ __forceinline__ uint4 load_stream(const uint4* p) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 struct RecMask {
     uint64_t x, s, d;   // complex lanes, simple (non-consensus) lanes, dirty lanes (below)
     uint64_t px, ps;    // the parent's x and s, pushed by the parent's post-order wave
@@ -243,7 +249,7 @@ __device__ __forceinline__ void store_kid_masks(uint64_t* cm, size_t rec, int la
 
 // Code planes of a non-complex lane: stored (simple) or the consensus word.
 __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
-    if ((m.s >> lane) & 1ull) return p[lanes_below(m.s)];
+    if ((m.s >> lane) & 1ull) return load_stream(p + lanes_below(m.s));
     return cons[word];
 }
 
@@ -273,7 +279,7 @@ __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t re
 __device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, int lane, const uint4* cons,
                                               int64_t word) {
     const uint4* src = ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
-    return *src;
+    return load_stream(src);
 }
 
 // Where a wave's complex-slot loads point: the record's complex area, or -- when the record
@@ -299,7 +305,7 @@ __device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m
     const uint4* base = cx_base(p, m, cons);
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
+    for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
 }
 
 __device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s) {
@@ -323,7 +329,7 @@ __device__ __forceinline__ void load_fitch_set(const uint4* p, const RecMask& m,
     if (cx) {
         const uint32_t k = lanes_below(m.x);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = p[kWave + q * kWave + k];
+        for (int q = 0; q < 4; ++q) v[q] = load_stream(p + kWave + q * kWave + k);
     }
     onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
     if (cx) {
@@ -374,13 +380,13 @@ __device__ __forceinline__ void load_sankoff(const uint4* p, const RecMask& m, c
         const uint32_t k = lanes_below(m.x);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint4 v = p[kWave + q * kWave + k];
+            const uint4 v = load_stream(p + kWave + q * kWave + k);
             z0[4 * q + 0] = v.x; z0[4 * q + 1] = v.y; z0[4 * q + 2] = v.z; z0[4 * q + 3] = v.w;
         }
         if (want_z1) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 v = p[5 * kWave + q * kWave + k];
+                const uint4 v = load_stream(p + 5 * kWave + q * kWave + k);
                 z1[4 * q + 0] = v.x; z1[4 * q + 1] = v.y; z1[4 * q + 2] = v.z; z1[4 * q + 3] = v.w;
             }
         }
@@ -505,7 +511,7 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 w = p[kWave + q * kWave + k];
+                const uint4 w = load_stream(p + kWave + q * kWave + k);
                 const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -567,7 +573,7 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
         const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
+        for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
     }
 }
 
@@ -589,7 +595,7 @@ __device__ __forceinline__ void fetch_child_ap_m(const UpArgs& a, int32_t c, int
     const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f.v[q] = base[q * kWave + k];
+    for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
 }
 
 // (the builtin returns int: each half goes through uint32_t, or the low half's bit 31 would
