@@ -108,6 +108,7 @@ _SIGS = {
     "pm_phase_report": (C.c_int64, [C.c_char_p, C.c_int64]),
     "pm_stream_copy_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
     "pm_stream_write_rate": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double)]),
+    "pm_warmup": (C.c_int, [C.c_int]),
     "pm_replay_shape": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 

@@ -89,3 +89,28 @@ def test_graph_follows_tree_change(engine):
                 assert g.shape == w.shape and (g == w).all()
     finally:
         engine.set_graph(False)
+
+
+def test_warmup_then_run_and_write_probe(engine):
+    """pm_warmup (HIP initialisation + code objects, callable from any thread: the CLI's -I
+    overlap) leaves the context working, and the write-only roof probe measures something
+    plausible on the device."""
+    import threading
+    from panman_amd._lib import load
+    rc = []
+    t = threading.Thread(target=lambda: rc.append(load().pm_warmup(0)))
+    t.start()
+    t.join()
+    assert rc == [0]
+    assert load().pm_warmup(1 << 20) != 0   # no such device: an error, not a crash
+    rng = np.random.default_rng(3)
+    off, idx, root = random_tree(200, rng, max_children=4)
+    leaves = int((off[1:] == off[:-1]).sum())
+    engine.tree_upload(off, idx, root)
+    codes, present = _columns(rng, leaves, 1500, False)
+    _load(engine, off, idx, root, codes, present, False, rng)
+    engine.set_graph(False)
+    recs, score, rootc = _results(engine, panman_amd.MODE_FITCH)
+    assert recs.shape[0] > 0 and score.shape[0] == 1500
+    gbs = panman_amd.stream_write_rate(0, gib=1, reps=2)
+    assert 100.0 < gbs < 20000.0

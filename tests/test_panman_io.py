@@ -246,3 +246,26 @@ def test_crafted_xz_index_is_rejected(tmp_path, monkeypatch, attack):
     with pytest.raises(PanmanError) as e:
         PanmanFile(bad)
     assert "xz" in str(e.value)
+
+
+def test_xz_blocks_depend_on_message_size_only(tmp_path, monkeypatch):
+    """The writer cuts a message into >= 16 blocks of >= 64 KiB (1 MiB from 16 MiB up), whatever
+    the host's thread count: the bytes written are the same with 1 and 8 encoder threads, and
+    the stream holds the block count the size rule gives."""
+    import lzma
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=40, blocks=30, mean_len=3000, seed=9)
+    monkeypatch.delenv("PM_XZ_BLOCK", raising=False)
+    monkeypatch.delenv("PM_XZ_THREADS", raising=False)
+    out = {}
+    for threads in ("1", "8"):
+        monkeypatch.setenv("PM_HOST_THREADS", threads)
+        path = str(tmp_path / f"t{threads}.panman")
+        write_panman(path, [pm])
+        out[threads] = open(path, "rb").read()
+    assert out["1"] == out["8"]
+    n = len(lzma.decompress(out["1"]))
+    block = 1 << 16
+    while block < (1 << 20) and block * 16 < n:
+        block <<= 1
+    assert multi_blocks(out["1"]) == max(1, -(-n // block))
