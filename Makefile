@@ -22,6 +22,10 @@ build/flags.stamp: FORCE
 	@mkdir -p build
 	@echo '$(FLAGS_LINE)' | cmp -s - $@ || echo '$(FLAGS_LINE)' > $@
 
+# the _nt copies compile their base file with PM_NT_LOADS
+build/pm_fitch_nt.hip.o: panman_amd/csrc/pm_fitch.hip
+build/pm_sankoff_nt.hip.o: panman_amd/csrc/pm_sankoff.hip
+
 build/%.o: panman_amd/csrc/% $(HDR) build/flags.stamp
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@

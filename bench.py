@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--sub-down", type=int, default=-1,
                    help="Fitch: PM_OPT_SUB_DOWN, S2 / S3 records from the parent's pre-order wave (1) or "
                         "the tail (0); -1: library default")
+    p.add_argument("--nt-loads", type=int, default=-1, choices=(-1, 0, 1),
+                   help="set records read non-temporal (1), ordinary (0), or by level size (-1, default)")
     p.add_argument("--plain-up", type=int, default=-1,
                    help="Fitch: PM_OPT_PLAIN_UP, the grouped post-order's plain nodes in the lean kernel (1) or "
                         "not (0); >= 2: on for launches of at least that many waves; -1: library default")
@@ -138,6 +140,8 @@ def main():
         eng.set_up_group(False)
     if args.sub_down >= 0:
         eng.set_sub_down(bool(args.sub_down))
+    if args.nt_loads != -1:   # set-record load policy (default: the library's, by level size)
+        eng.set_nt_loads(args.nt_loads)
     if args.plain_up >= 0:   # 0 off, 1 on (library threshold), >= 2: on from that many waves
         eng.set_plain_up(bool(args.plain_up), args.plain_up if args.plain_up >= 2 else 0)
     if args.group >= 0 or args.group_levels != 4:

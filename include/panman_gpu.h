@@ -119,6 +119,10 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  first guess (about 1.5 % of node*site pairs); a run that overflows it is
  *                  re-run with a larger buffer when its results are read (pm_mutation_count,
  *                  pm_site_results*, pm_run_gather), so results never depend on it.
+ *   PM_OPT_NT_LOADS (default -1): set records read with non-temporal loads (1), ordinary
+ *                  loads (0), or by the tree's widest level (-1: non-temporal from 64k
+ *                  (node, tile) waves up, where the records have left the caches by the time
+ *                  they are read).
  * (Option ids 1, 4, 5 and 11 -- subtree-region, heavy-path-chain and level-band schedules,
  * tail records overlapped with the pre-order levels -- were measured slower than, or no
  * faster than, the level kernels on MI355X and removed.) */
@@ -132,6 +136,7 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
 #define PM_OPT_RECORD_CAP 12
 #define PM_OPT_SUB_DOWN 13
 #define PM_OPT_PLAIN_UP 14
+#define PM_OPT_NT_LOADS 16
 int pm_set_option(pm_ctx* ctx, int option, int64_t value);
 /* Accumulate per-kernel-class device time with HIP events (see pm_kernel_times). */
 int pm_set_profiling(pm_ctx* ctx, int enable);

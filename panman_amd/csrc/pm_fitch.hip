@@ -14,6 +14,11 @@
 // Integer bit-set work only: no MFMA (SURVEY.md §8d roofline is HBM bandwidth).
 #include "pm_kernels.h"
 
+#if PM_NT_LOADS   // (pm_fitch_nt.hip: the same passes, non-temporal set-record loads)
+#define launch_fitch launch_fitch_nt
+#define warm_fitch warm_fitch_nt
+#endif
+
 namespace pm {
 namespace {
 
@@ -194,7 +199,7 @@ __device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, in
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 w = load_stream(p + kWave + q * kWave + k);
+                const uint4 w = load_rec(p + kWave + q * kWave + k);
                 f.w[4 * q] = w.x; f.w[4 * q + 1] = w.y; f.w[4 * q + 2] = w.z; f.w[4 * q + 3] = w.w;
             }
         } else {
@@ -397,6 +402,7 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
     }
 }
 
+#if !PM_NT_LOADS   // (the score kernel: once, in pm_fitch.hip)
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
 // LDS (sites fit) or straight into global counters.  1024-thread workgroups: the LDS
 // histogram (4 B per site) admits one workgroup per CU, so the workgroup brings the waves.
@@ -438,6 +444,8 @@ __global__ __launch_bounds__(kScoreBlock) void k_site_score(const pm_mut* recs, 
             if (hist[s]) atomicAdd(&score[s], (int32_t)hist[s]);
     }
 }
+
+#endif
 
 }  // namespace
 
@@ -721,6 +729,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     return hipGetLastError();
 }
 
+#if !PM_NT_LOADS
 hipError_t launch_score(pm_ctx* c) {
     hipError_t e = hipMemsetAsync(c->score, 0, sizeof(int32_t) * c->num_sites, c->stream);
     if (e != hipSuccess) return e;
@@ -735,10 +744,12 @@ hipError_t launch_score(pm_ctx* c) {
     return hipGetLastError();
 }
 
+#endif
+
 // This file's code object, loaded ahead of its first launch (pm_warmup).
 hipError_t warm_fitch() {
     hipFuncAttributes at;
-    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_site_score));
+    return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fitch_up_wide<true>));
 }
 
 }  // namespace pm

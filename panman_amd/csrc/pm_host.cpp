@@ -208,10 +208,24 @@ int alloc_work(pm_ctx* c, int mode) {
     return PM_OK;
 }
 
+// Non-temporal set-record loads (pm_fitch_nt.hip / pm_sankoff_nt.hip) when the tree has a
+// level of at least 64k (node, tile) waves: there the records a wave reads have left the
+// caches anyway (N* Fitch 14.7 -> 14.06 ms); a tree of small levels (C3: <= ~900 nodes x 15
+// tiles) reads them back from cache and keeps ordinary loads (C3 Fitch 4.42 -> 4.30 ms).
+bool nt_policy(const pm_ctx* c) {
+    if (c->nt_loads >= 0) return c->nt_loads != 0;
+    const std::vector<int32_t>& off = c->ht.down_level_off;
+    int64_t widest = 0;
+    for (size_t l = 0; l + 1 < off.size(); ++l) widest = std::max<int64_t>(widest, off[l + 1] - off[l]);
+    return widest * (wpad_of(c) / kWave) >= 65536;
+}
+
 hipError_t launch_all(pm_ctx* c, int mode) {
     const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
     const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
-    hipError_t e = sankoff ? launch_sankoff(c, block) : launch_fitch(c, block);
+    const bool nt = nt_policy(c);
+    hipError_t e = sankoff ? (nt ? launch_sankoff_nt(c, block) : launch_sankoff(c, block))
+                           : (nt ? launch_fitch_nt(c, block) : launch_fitch(c, block));
     if (e == hipSuccess) e = launch_score(c);
     return e;
 }
@@ -230,7 +244,7 @@ uint64_t graph_key_of(const pm_ctx* c, int mode) {
                               (uint64_t)(uintptr_t)c->leaf_flag, (uint64_t)(uintptr_t)c->cons,
                               (uint64_t)(uintptr_t)c->forced, (uint64_t)(uintptr_t)c->score,
                               (uint64_t)(uintptr_t)c->root_code, (uint64_t)(uintptr_t)c->shard_cnt,
-                              (uint64_t)(uintptr_t)c->sub_planes,
+                              (uint64_t)(uintptr_t)c->sub_planes, (uint64_t)nt_policy(c),
                               (uint64_t)(uintptr_t)c->dt.child_off, (uint64_t)(uintptr_t)c->stream};
     uint64_t h = 1469598103934665603ull;
     for (uint64_t v : parts) h = (h ^ v) * 1099511628211ull;
@@ -425,7 +439,7 @@ int pm_warmup(int device) {
     if (e != hipSuccess || n == 0) return PM_ERR_HIP;
     if (device < 0 || device >= n) return PM_ERR_ARG;
     if ((e = hipSetDevice(device)) != hipSuccess) return PM_ERR_HIP;
-    for (auto warm : {warm_fitch, warm_sankoff, warm_replay, warm_synth, warm_sort})
+    for (auto warm : {warm_fitch, warm_sankoff, warm_fitch_nt, warm_sankoff_nt, warm_replay, warm_synth, warm_sort})
         if ((e = warm()) != hipSuccess) return PM_ERR_HIP;
     // the runtime's first allocation and staged copies
     void* d = nullptr;
@@ -516,6 +530,11 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->shard_cap = 0;   // the next run allocates record_cap per shard
         c->record_cap = value;
         c->ran = false;
+        return PM_OK;
+    }
+    if (option == PM_OPT_NT_LOADS) {
+        if (value < -1 || value > 1) return fail(c, PM_ERR_ARG, "PM_OPT_NT_LOADS: -1 (by level size), 0 or 1");
+        c->nt_loads = (int32_t)value;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {

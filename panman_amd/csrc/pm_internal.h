@@ -271,6 +271,7 @@ struct pm_ctx {
     // hipGraph of one pm_run (PM_OPT_GRAPH): captured on first use, replayed while the
     // launch sequence and every buffer it touches stay the same (graph_key)
     bool use_graph = false;
+    int32_t nt_loads = -1;            // PM_OPT_NT_LOADS: -1 by level size (nt_policy), 0 off, 1 on
     hipGraphExec_t graph_exec = nullptr;
     uint64_t graph_key = 0;
 
@@ -311,10 +312,14 @@ void timer_end(pm_ctx* c, int cls);
 // kernel launchers (pm_fitch.hip / pm_sankoff.hip / pm_synth.hip)
 hipError_t launch_fitch(pm_ctx* c, bool block);
 hipError_t launch_sankoff(pm_ctx* c, bool block);
+hipError_t launch_fitch_nt(pm_ctx* c, bool block);     // non-temporal set-record loads
+hipError_t launch_sankoff_nt(pm_ctx* c, bool block);
 // Records of the last run, sorted by (node, site) on the device, copied to host `out`.
 // pm_warmup: one kernel of each code object looked up, so the object is loaded
 hipError_t warm_fitch();
 hipError_t warm_sankoff();
+hipError_t warm_fitch_nt();
+hipError_t warm_sankoff_nt();
 hipError_t warm_replay();
 hipError_t warm_synth();
 hipError_t warm_sort();

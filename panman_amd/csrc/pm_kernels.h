@@ -8,7 +8,20 @@
 #include "pm_bits.h"
 #include "pm_internal.h"
 
+// Set-record load policy of this translation unit: pm_fitch.hip / pm_sankoff.hip build the
+// kernels with ordinary loads, pm_fitch_nt.hip / pm_sankoff_nt.hip with non-temporal ones
+// (PM_NT_LOADS), each copy in a namespace of its own; launch_all picks one per run (nt_policy).
+#ifndef PM_NT_LOADS
+#define PM_NT_LOADS 0
+#endif
+#if PM_NT_LOADS
+#define PM_KNS kern_nt
+#else
+#define PM_KNS kern
+#endif
+
 namespace pm {
+inline namespace PM_KNS {
 
 enum class Mode { kFitch, kSankoff, kBlockFitch };
 
@@ -179,6 +192,20 @@ __device__ __forceinline__ uint4 load_stream(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Set records are read once, by the next wave that needs them.  With levels of many waves
+// the lines are gone from L2 / MALL before anything reads them again, and non-temporal loads
+// keep them from displacing what is reused (N* Fitch 14.7 -> 14.06 ms, Sankoff 20.2 -> 19.7
+// ms); with small levels (a deep tree's) the next level finds the records it reads in cache,
+// and non-temporal loads cost C3 Fitch 0.12 ms, Sankoff 0.4 ms.  A branch per load on the
+// launch's size made every kernel slower (N* 16.7 ms), so the policy is per translation unit.
+__device__ __forceinline__ uint4 load_rec(const uint4* p) {
+#if PM_NT_LOADS
+    return load_stream(p);
+#else
+    return *p;
+#endif
+}
+
 struct RecMask {
     uint64_t x, s, d;   // complex lanes, simple (non-consensus) lanes, dirty lanes (below)
     uint64_t px, ps;    // the parent's x and s, pushed by the parent's post-order wave
@@ -249,7 +276,7 @@ __device__ __forceinline__ void store_kid_masks(uint64_t* cm, size_t rec, int la
 
 // Code planes of a non-complex lane: stored (simple) or the consensus word.
 __device__ __forceinline__ uint4 rec_code(const uint4* p, const RecMask& m, int lane, const uint4* cons, int64_t word) {
-    if ((m.s >> lane) & 1ull) return load_stream(p + lanes_below(m.s));
+    if ((m.s >> lane) & 1ull) return load_rec(p + lanes_below(m.s));
     return cons[word];
 }
 
@@ -279,7 +306,7 @@ __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t re
 __device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, int lane, const uint4* cons,
                                               int64_t word) {
     const uint4* src = ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
-    return load_stream(src);
+    return load_rec(src);
 }
 
 // Where a wave's complex-slot loads point: the record's complex area, or -- when the record
@@ -305,7 +332,7 @@ __device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m
     const uint4* base = cx_base(p, m, cons);
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
+    for (int q = 0; q < 4; ++q) f.v[q] = load_rec(base + q * kWave + k);
 }
 
 __device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s) {
@@ -329,7 +356,7 @@ __device__ __forceinline__ void load_fitch_set(const uint4* p, const RecMask& m,
     if (cx) {
         const uint32_t k = lanes_below(m.x);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = load_stream(p + kWave + q * kWave + k);
+        for (int q = 0; q < 4; ++q) v[q] = load_rec(p + kWave + q * kWave + k);
     }
     onehot_from_code(c.x, c.y, c.z, c.w, ~0u, s);
     if (cx) {
@@ -380,13 +407,13 @@ __device__ __forceinline__ void load_sankoff(const uint4* p, const RecMask& m, c
         const uint32_t k = lanes_below(m.x);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint4 v = load_stream(p + kWave + q * kWave + k);
+            const uint4 v = load_rec(p + kWave + q * kWave + k);
             z0[4 * q + 0] = v.x; z0[4 * q + 1] = v.y; z0[4 * q + 2] = v.z; z0[4 * q + 3] = v.w;
         }
         if (want_z1) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 v = load_stream(p + 5 * kWave + q * kWave + k);
+                const uint4 v = load_rec(p + 5 * kWave + q * kWave + k);
                 z1[4 * q + 0] = v.x; z1[4 * q + 1] = v.y; z1[4 * q + 2] = v.z; z1[4 * q + 3] = v.w;
             }
         }
@@ -511,7 +538,7 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 w = load_stream(p + kWave + q * kWave + k);
+                const uint4 w = load_rec(p + kWave + q * kWave + k);
                 const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -573,7 +600,7 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
         const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
+        for (int q = 0; q < 4; ++q) f.v[q] = load_rec(base + q * kWave + k);
     }
 }
 
@@ -595,7 +622,7 @@ __device__ __forceinline__ void fetch_child_ap_m(const UpArgs& a, int32_t c, int
     const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f.v[q] = load_stream(base + q * kWave + k);
+    for (int q = 0; q < 4; ++q) f.v[q] = load_rec(base + q * kWave + k);
 }
 
 // (the builtin returns int: each half goes through uint32_t, or the low half's bit 31 would
@@ -1654,4 +1681,5 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
+}  // namespace PM_KNS
 }  // namespace pm

@@ -13,6 +13,11 @@
 // node by out-degree class so binary nodes pay for 2-bit counters only.
 #include "pm_kernels.h"
 
+#if PM_NT_LOADS   // (pm_sankoff_nt.hip: the same passes, non-temporal set-record loads)
+#define launch_sankoff launch_sankoff_nt
+#define warm_sankoff warm_sankoff_nt
+#endif
+
 namespace pm {
 namespace {
 

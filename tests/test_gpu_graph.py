@@ -114,3 +114,30 @@ def test_warmup_then_run_and_write_probe(engine):
     assert recs.shape[0] > 0 and score.shape[0] == 1500
     gbs = panman_amd.stream_write_rate(0, gib=1, reps=2)
     assert 100.0 < gbs < 20000.0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_nt_load_builds_match(engine, mode):
+    """The two builds of the passes (ordinary / non-temporal set-record loads, PM_OPT_NT_LOADS)
+    give the same mutations, scores and root codes, with and without graph replay; small trees
+    take the ordinary build by default, so the non-temporal one is forced here."""
+    block = mode in (panman_amd.MODE_BLOCK_FITCH, panman_amd.MODE_BLOCK_SANKOFF)
+    rng = np.random.default_rng(300 + mode)
+    off, idx, root = random_tree(400, rng, max_children=6)
+    leaves = int((off[1:] == off[:-1]).sum())
+    engine.tree_upload(off, idx, root)
+    codes, present = _columns(rng, leaves, 3000, block)
+    _load(engine, off, idx, root, codes, present, block, rng)
+    engine.set_graph(False)
+    engine.set_nt_loads(0)
+    want = _results(engine, mode)
+    try:
+        for graph in (False, True):
+            engine.set_graph(graph)
+            engine.set_nt_loads(1)
+            got = _results(engine, mode)
+            for g, w in zip(got, want):
+                assert g.shape == w.shape and (g == w).all()
+    finally:
+        engine.set_nt_loads(-1)
+        engine.set_graph(False)
