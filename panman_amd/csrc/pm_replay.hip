@@ -516,6 +516,17 @@ __device__ __forceinline__ void dfs_write_out(const ReplayDev& d, DfsLds& S, int
     uint4* dst = reinterpret_cast<uint4*>(d.rows + (size_t)row * d.row_stride + c0);
     const uint4* cons16 = reinterpret_cast<const uint4*>(d.cons_row + c0);
     static_assert(kDfsTile / 16 % kWave == 0, "write-out: whole rounds of 64 lanes");
+    // (uniform) the common case -- a whole tile, no absent block: every round's LDS reads
+    // first, then the stores (C5 1.27 -> 1.20 ms, SARS-like 2.37 -> 2.31 ms against the loop)
+    if (am == 0 && n == kDfsTile) {
+        constexpr int R = kDfsTile / 16 / kWave;
+        uint4 v[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = S.tile[lane + kWave * j];
+#pragma unroll
+        for (int j = 0; j < R; ++j) store_stream(dst + lane + kWave * j, v[j]);
+        return;
+    }
     for (int j = 0; j < kDfsTile / 16 / kWave; ++j) {
         const int k = lane + kWave * j;
         if (k >= n / 16) break;
