@@ -762,6 +762,7 @@ __device__ __forceinline__ void dfs_fast_apply(DfsLds& S, const DfsFast& x, int3
 struct DfsState {
     int32_t psp, osp, prev_len, next_u, len, lp;   // stacks, previous path length, next group node, this leaf's path
     bool rebuild;
+    int32_t gc;   // the path prefix every leaf of the group shares (never undone inside the group)
 };
 
 // Leaf i of the group: its transition (cur: the fast one, prefetched two leaves ahead; or f:
@@ -777,16 +778,25 @@ __device__ __forceinline__ void dfs_leaf(const ReplayDev& d, DfsLds& S, DfsState
     char* buf = reinterpret_cast<char*>(S.tile);
 #ifndef PM_DFS_NOEDITS
     int32_t np = 0, no = 0;
+    // the group's first leaf: its positions [0, gc) are every leaf's and never undone inside
+    // the group, so they are applied without pushes (with the prefetched first chunk) and the
+    // stacks hold only what later leaves undo -- a deep tree's long shared stem would otherwise
+    // overflow them and make every leaf of the group rebuild its row
+    int32_t lo = lp;
+    if (i == i0 && st.gc > 0 && !st.rebuild) {
+        lo = min(st.gc, len);
+        dfs_apply<false>(d, S, 0, lo, c0, lane, st.psp, st.osp, true, f);
+    }
     if (!st.rebuild) {
         if (cur.on) {   // (the counts from the prefetched bounds)
             int32_t pre;
             fast_prefix(lane / kFastEdits < len - lp ? cur.b.y - cur.b.x : 0, lane, pre, np);
             fast_prefix(lane / kFastEdits < len - lp ? cur.b.w - cur.b.z : 0, lane, pre, no);
         } else {
-            dfs_counts(S, lp, len, lane, np, no);
+            dfs_counts(S, lo, len, lane, np, no);
         }
-        const int32_t psp_x = lp < st.prev_len ? (int32_t)S.psp_at[lp] : st.psp;
-        const int32_t osp_x = lp < st.prev_len ? (int32_t)S.osp_at[lp] : st.osp;
+        const int32_t psp_x = lo < st.prev_len ? (int32_t)S.psp_at[lo] : st.psp;
+        const int32_t osp_x = lo < st.prev_len ? (int32_t)S.osp_at[lo] : st.osp;
         st.rebuild = psp_x + np > kDfsPCap || osp_x + no > kDfsOCap;
     }
     if (!st.rebuild) {
@@ -809,7 +819,7 @@ __device__ __forceinline__ void dfs_leaf(const ReplayDev& d, DfsLds& S, DfsState
             st.psp = a;
         }
         if (cur.on) dfs_fast_apply(S, cur, lp, len - lp, c0, lane, st.psp, st.osp);
-        else dfs_apply<true>(d, S, lp, len, c0, lane, st.psp, st.osp, true, f);
+        else dfs_apply<true>(d, S, lo, len, c0, lane, st.psp, st.osp, lo == lp, f);
     } else {
         // rebuild: the consensus again, the whole path, nothing pushed
         dfs_copy_in(d, S, c0, n, lane);
@@ -854,11 +864,14 @@ __global__ __launch_bounds__(kWave, PM_DFS_WAVES) void k_replay_dfs(ReplayDev d)
     dfs_copy_in(d, S, c0, n, lane);
     dfs_leaf_tables(d, S, i0, i1 - i0, t, c0, n, lane);
     __syncthreads();   // (one wave: the copy-in and the tables landed)
-    DfsState st{0, 0, 0, 0, S.llen[0], 0, false};
+    int32_t gc = S.llen[0];   // (a one-leaf group: its whole path)
+    for (int32_t k = 1; k < i1 - i0; ++k) gc = min(gc, (int32_t)S.llp[k]);
+    DfsState st{0, 0, 0, 0, S.llen[0], 0, false, gc};
     DfsPrefetch f;
     DfsFast xa, xb;
     xa.on = false;   // (the first leaf: its whole path, the general path)
-    dfs_prefetch(d, S, 0, min(kWave, st.len), c0, lane, f);
+    // (its first chunk: of the shared prefix when there is one, applied first)
+    dfs_prefetch(d, S, 0, min(kWave, gc > 0 ? gc : st.len), c0, lane, f);
     xb.on = false;
     if (i0 + 1 < i1) dfs_fast_prefetch(d, S, st.len, S.llen[1] - S.llp[1], lane, xb);
     // two leaves per trip, the roles of the two transition buffers swapped by the code rather
