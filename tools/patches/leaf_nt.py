@@ -20,6 +20,7 @@ if which in ("up", "all"):
 if which in ("down", "all"):
     down = pat.sub(r"load_stream(a.leaf_planes + (\1))", down)
 s = up + down
-anchor = "struct RecMask {"
-s = s.replace(anchor, helper + anchor, 1)
+if "uint4 load_stream(" not in s:   # (the library has its own since the non-temporal record loads)
+    anchor = "struct RecMask {"
+    s = s.replace(anchor, helper + anchor, 1)
 open(p, "w").write(s)
