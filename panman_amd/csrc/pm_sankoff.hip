@@ -169,8 +169,10 @@ __device__ __forceinline__ void sankoff_up_node(const UpArgs& a, const NodeDesc&
 #ifndef PM_SK_UP_WAVES
 #define PM_SK_UP_WAVES 1
 #endif
+// the plain kernel at 8 waves per SIMD (64 VGPRs, 8 B spilled): N* Sankoff 19.46 -> 19.34-19.38 ms,
+// C3 6.15 -> 6.09-6.11 ms against 7 (r05aj)
 #ifndef PM_SK_PLAIN_UP_WAVES
-#define PM_SK_PLAIN_UP_WAVES 7
+#define PM_SK_PLAIN_UP_WAVES 8
 #endif
 // GROUP: 4 waves per SIMD (3: no scratch spills, C3 Sankoff 2-3 % slower; see PM_GROUP_UP_WAVES)
 #ifndef PM_SK_GROUP_UP_WAVES
