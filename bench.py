@@ -262,6 +262,10 @@ def workload_label(mode: str, tree: str, L: int, S: int, world: int) -> str:
             return f"C2 {mode}: {shape} (RSV-like size)"
     elif world == 1 and (L, S) == (100_000, 30_000):
         return f"C3 {mode}: {shape} (T2, SARS-like)"
+    elif world == 1 and (L, S) == (8_000_000, 3_750):
+        return f"C4 rank share (T2) {mode}: {shape} (one rank of --gpus 8 on the SARS-like tree)"
+    elif world > 1 and L == world * 1_000_000 and S == 30_000:
+        return f"C4 (T2) {mode} weak scaling: {shape}, columns over {world} GPUs"
     return f"{mode}: {shape} (not a BASELINE config size)"
 
 
@@ -799,11 +803,15 @@ def replay_block(args, world, rank, local):
             acc[v] += acc[parent[v]]
     path_recs = float(acc[leaf_nodes[lo:hi]].sum())
     # bytes the replay must move: every row byte written once, the consensus row read once
-    # (it stays cache-resident across leaves), 5 B (column u32 + char) per distinct edit (the
-    # depth-first kernel reads an edit once per leaf group, not once per leaf below it; round 4
-    # counted 5 B per edit on each leaf's path, `path_model_bytes` below)
-    alg_bytes = units + float(cols) + 5.0 * float(edits)
+    # (it stays cache-resident across leaves), 5 B (column u32 + char) per edit read: the
+    # depth-first kernel reads each edit of a leaf group's path-node union once per group
+    # (`replay.group_edits`, counted by replay_prepare), not once per leaf below it; k_replay
+    # reads every edit on each leaf's path (round 4's model, `path_model_bytes` below)
+    edits_read = float(prep.get("replay.group_edits", 0.0)) if dfs_groups else 0.0
+    alg_bytes = units + float(cols) + 5.0 * (edits_read if dfs_groups else 0.0)
     path_model_bytes = units + float(cols) + 5.0 * path_recs
+    if not dfs_groups:
+        alg_bytes = path_model_bytes
     kms = ms[3] / args.steps
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     # host formatting (aligned FASTA of every leaf)
@@ -867,7 +875,10 @@ def replay_block(args, world, rank, local):
         "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_note": traffic_note, "design_bytes_per_launch": alg_bytes,
-                     "bytes_model": "row bytes written once + consensus row once + 5 B per distinct edit",
+                     "bytes_model": "row bytes written once + consensus row once + 5 B per edit read (k_replay_dfs: "
+                                    "each edit of a leaf group's path-node union once per group; k_replay: every "
+                                    "edit on each leaf's path)",
+                     "edits_read": edits_read if dfs_groups else path_recs, "distinct_edits": edits,
                      "path_model_frac": round(path_model_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "leaf_groups": dfs_groups,
                      "traffic_GBs": round(traffic / (kms * 1e-3) / 1e9, 1) if traffic else None,

@@ -455,6 +455,21 @@ int run(int argc, char** argv);
 
 }  // namespace
 
+// Builds whose tools write their results at exit always take the normal exit: sanitizers
+// (LeakSanitizer's report) are detected; a coverage build (gcc defines no macro for
+// --coverage) adds -DPM_CLI_NORMAL_EXIT.
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__) || defined(PM_CLI_NORMAL_EXIT)
+constexpr bool kFastExitAllowed = false;
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer) || __has_feature(thread_sanitizer) || __has_feature(memory_sanitizer)
+constexpr bool kFastExitAllowed = false;
+#else
+constexpr bool kFastExitAllowed = true;
+#endif
+#else
+constexpr bool kFastExitAllowed = true;
+#endif
+
 // PANMAN_PHASES=1: the library's phase log (pm_phase_report: HIP init, parse, upload, GPU
 // run, grouping, capnp, xz, download ...) and the CLI's own wall time, on stderr.
 int main(int argc, char** argv) {
@@ -470,10 +485,11 @@ int main(int argc, char** argv) {
     // Every output file is closed and every context destroyed by now; what a normal exit adds
     // is the HIP / HSA runtime's own teardown in static destructors, which the kernel driver
     // does anyway when the process ends.  Skipped, unless a profiler whose results are written
-    // at exit is preloaded (or PM_CLI_FULL_EXIT=1).
+    // at exit is preloaded, the build carries a sanitizer or coverage (kFastExitAllowed), or
+    // PM_CLI_FULL_EXIT=1.
     const char* pre = std::getenv("LD_PRELOAD");
     const char* full = std::getenv("PM_CLI_FULL_EXIT");
-    if (!(full && full[0] == '1') && !(pre && std::strstr(pre, "rocprof"))) {
+    if (kFastExitAllowed && !(full && full[0] == '1') && !(pre && std::strstr(pre, "rocprof"))) {
         std::cout.flush();
         std::cerr.flush();
         std::fflush(nullptr);

@@ -124,4 +124,15 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t& to
     return incl - v;
 }
 
+// A workgroup barrier that orders LDS only: each wave's LDS accesses are complete (lgkmcnt)
+// and visible to the others, while its global stores and loads stay in flight.  __syncthreads()
+// is a workgroup release / acquire over global memory too, which on gfx950 waits for every
+// outstanding vector memory operation (vmcnt(0)): in the replay (behind a tile's write-out) and the
+// post-order sweeps (behind a round's record stores) a full HBM write round trip.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 }  // namespace pm

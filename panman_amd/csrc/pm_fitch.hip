@@ -402,6 +402,195 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
     }
 }
 
+// ---- LDS-staged post-order sweeps (PM_OPT_CLUSTER; schedule: pm_cluster.cpp) --------------
+// One workgroup of kClWaves waves = one (cluster, tile); the cluster's rounds bottom-up, one
+// node per wave (a node of out-degree > 3: every wave), an LDS-only barrier between rounds.
+// A child of the same cluster comes from its LDS slot (16 planes, 4 KiB per (node, tile));
+// every other child as in fitch_up_node (leaf words, a leaf-parent's or S2 / S3 subtree's
+// leaves, or an earlier launch's compressed record).  Records and masks go to HBM exactly as
+// the level kernels write them (the pre-order pass and the tail read them), without a wait.
+struct ClArgs {
+    const NodeDesc* items;
+    const int32_t* wg_off;
+    const int32_t* slot_of;
+    int32_t wg0;
+};
+typedef uint4 ClSlots[kClSlots][4][kWave];
+
+__device__ __forceinline__ void slot_read(const ClSlots& S, int s, int lane, uint32_t* x) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = S[s][q][lane];
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void slot_write(ClSlots& S, int s, int lane, const uint32_t* x) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[s][q][lane] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+}
+
+// AND if non-empty else OR, forced root, the record + masks to HBM (as fitch_up_node / wide_finish
+// write them; no up slot: every parent of a cluster node is a cluster node, whose children come
+// from a slot or their mask records), the set into the node's slot.
+__device__ __forceinline__ void cluster_finish(const UpArgs& a, const NodeDesc& d, ClSlots& S, int tile, int lane,
+                                               int64_t word, const uint4& cw, uint32_t* both, const uint32_t* either,
+                                               uint32_t vd, uint32_t vd0, uint32_t vd1, bool split) {
+    const int32_t n = d.node;
+    const uint32_t nz = any_plane(both);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) both[v] |= either[v] & ~nz;
+    if (n == a.root_dense && a.forced != nullptr) {   // refState (src/fitchSankoff.cpp:45-47)
+        const uint4 F = a.forced[word];
+        onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
+    }
+    uint64_t mx, ms, md;
+    store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, vd != 0u, mx, ms, md);
+    uint64_t md0 = md, md1 = md;
+    if (split) {
+        md0 = mx | __ballot(vd0 != 0u);
+        md1 = mx | __ballot(vd1 != 0u);
+    }
+    push_children2(a, tile, lane, d.e0, d.e1, d.c0, d.c1, mx, ms, md0, md1, n == a.root_dense);
+    store_kid_masks(a.cmask, (size_t)n * a.tiles + tile, lane, sub_shaped(d.c0) ? md1 : md0, md1);
+    if (d.parent >= 0) slot_write(S, d.parent, lane, both);
+}
+
+// A node of out-degree <= 3 (one wave).
+__device__ __forceinline__ void cluster_node(const UpArgs& a, const ClArgs& c, const NodeDesc& d, ClSlots& S, int tile,
+                                             int lane, int64_t word, const uint4& cw) {
+    const bool two = d.e1 - d.e0 > 1;
+    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
+    ChildFetch f0, f1;   // the children from memory: both loads in flight before either is used
+    if (d.pad0 < 0) fetch_child_ap<kFitchRec, false, true>(a, d.c0, vl0, tile, lane, word, f0);
+    if (two && d.pad1 < 0) fetch_child_ap<kFitchRec, false, true>(a, d.c1, vl1, tile, lane, word, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t both[16], either[16], vd0 = 0, vd1 = 0;
+    if (d.pad0 >= 0) slot_read(S, d.pad0, lane, both);
+    else child_set_ap<true>(d.c0, vl0, f0, both, vd0);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) either[v] = both[v];
+    if (two) {
+        uint32_t y[16];
+        if (d.pad1 >= 0) slot_read(S, d.pad1, lane, y);
+        else child_set_ap<true>(d.c1, vl1, f1, y, vd1);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
+    }
+    uint32_t vd = vd0 | vd1;
+    for (int32_t e = d.e0 + 2; e < d.e1; ++e) {   // an out-degree-3 node's third child
+        const int32_t ch = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int32_t s = materialised(ch) ? __builtin_amdgcn_readfirstlane(c.slot_of[ch]) : -1;
+        if (s >= 0) {
+            uint32_t y[16];
+            slot_read(S, s, lane, y);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
+        } else {
+            const int4 vl = ch >= 0 && (ch & kVirtualBit) ? a.vleaf[ch & kDenseMask] : make_int4(-1, -1, -1, -1);
+            fold_child<true>(a, ch, vl, tile, lane, word, both, either, vd);
+        }
+    }
+    cluster_finish(a, d, S, tile, lane, word, cw, both, either, vd, vd0, vd1, true);
+}
+
+// A node of out-degree > 3: its round's waves take children wave, wave + kClWaves, ...; the
+// accumulators meet in LDS (AND / OR atomics, src/fitchSankoff.cpp:39-55 is commutative), wave 0
+// finishes.  Every wave of the workgroup runs this (the round is the node's alone).
+__device__ __forceinline__ void cluster_wide(const UpArgs& a, const ClArgs& c, const NodeDesc& d, ClSlots& S,
+                                             uint32_t (*acc)[kWave], int wave, int tile, int lane, int64_t word,
+                                             const uint4& cw) {
+    uint32_t both[16], either[16], vd = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
+    for (int32_t base = d.e0 + wave; base < d.e1; base += kClWaves * kWave) {
+        const int32_t my = base + kClWaves * lane;
+        const int32_t enc = my < d.e1 ? a.child_enc[my] : 0;
+        const bool mat = my < d.e1 && materialised(enc);
+        const int32_t sl = mat ? c.slot_of[enc] : -1;
+        const int4 vl = my < d.e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask] : make_int4(-1, -1, -1, -1);
+        uint64_t cmx = 0, cms = 0;   // a record child's masks, one child per lane
+        if (mat && sl < 0) {
+            const uint64_t* q = a.cmask + kMaskWords * ((size_t)enc * a.tiles + tile);
+            cmx = q[0];
+            cms = q[1];
+        }
+        const int cnt = min(kWave, (d.e1 - base + kClWaves - 1) / kClWaves);
+        for (int k = 0; k < cnt; k += 2) {
+            const bool two = k + 1 < cnt;
+            const int32_t c0 = __builtin_amdgcn_readlane(enc, k), c1 = two ? __builtin_amdgcn_readlane(enc, k + 1) : 0;
+            const int32_t s0 = __builtin_amdgcn_readlane(sl, k), s1 = two ? __builtin_amdgcn_readlane(sl, k + 1) : -1;
+            const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
+            const int4 v1 = two ? make_int4(__builtin_amdgcn_readlane(vl.x, k + 1), __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1)
+                                : make_int4(-1, -1, -1, -1);
+            ChildFetch f0, f1;
+            if (s0 < 0) fetch_child_ap_m(a, c0, v0, readlane64(cmx, k), readlane64(cms, k), tile, lane, word, f0);
+            if (two && s1 < 0) fetch_child_ap_m(a, c1, v1, readlane64(cmx, k + 1), readlane64(cms, k + 1), tile, lane, word, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t y[16];
+            if (s0 >= 0) {
+                slot_read(S, s0, lane, y);
+#pragma unroll
+                for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
+            } else {
+                fold_child_ap(c0, v0, f0, both, either, vd);
+            }
+            if (two) {
+                if (s1 >= 0) {
+                    slot_read(S, s1, lane, y);
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
+                } else {
+                    fold_child_ap(c1, v1, f1, both, either, vd);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        atomicAnd(&acc[v][lane], both[v]);
+        atomicOr(&acc[16 + v][lane], either[v]);
+    }
+    atomicOr(&acc[32][lane], vd);
+    lds_barrier();
+    if (wave == 0) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            both[v] = acc[v][lane];
+            either[v] = acc[16 + v][lane];
+            acc[v][lane] = ~0u;   // (reset for the next wide round; read by wave 0 only until then)
+            acc[16 + v][lane] = 0u;
+        }
+        vd = acc[32][lane];
+        acc[32][lane] = 0u;
+        cluster_finish(a, d, S, tile, lane, word, cw, both, either, vd, 0, 0, false);
+    }
+}
+
+__global__ __launch_bounds__(kClWaves * kWave) void k_fitch_up_cluster(UpArgs a, ClArgs c) {
+    __shared__ ClSlots S;
+    __shared__ uint32_t acc[33][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int32_t b = (int32_t)blockIdx.x;
+    const int32_t wl = b / a.tiles;
+    const int tile = b - wl * a.tiles;
+    const int32_t i0 = c.wg_off[c.wg0 + wl], rounds = (c.wg_off[c.wg0 + wl + 1] - i0) / kClWaves;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint4 cw = a.cons[word];
+    if (wave == 0) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) { acc[v][lane] = ~0u; acc[16 + v][lane] = 0u; }
+        acc[32][lane] = 0u;
+    }
+    lds_barrier();
+    for (int32_t r = 0; r < rounds; ++r) {
+        const NodeDesc& d = c.items[i0 + r * kClWaves + wave];
+        if (d.e1 - d.e0 > 3) cluster_wide(a, c, d, S, acc, wave, tile, lane, word, cw);   // (uniform over the workgroup)
+        else if (d.node >= 0) cluster_node(a, c, d, S, tile, lane, word, cw);
+        lds_barrier();
+    }
+}
+
 #if !PM_NT_LOADS   // (the score kernel: once, in pm_fitch.hip)
 // Per-site score = mutated edges below the root.  Records of a shard are histogrammed in
 // LDS (sites fit) or straight into global counters.  1024-thread workgroups: the LDS
@@ -465,8 +654,12 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     const bool virt = !block && c->virtual_leaf_parents;
     const bool sub = virt && c->subtree_form && c->leaves_all_present && ht.num_sshape > 0;
     const int32_t* child_enc = sub ? dt.child_enc_k : virt ? dt.child_enc_v : dt.child_enc;
-    // subtree form: grouped post-order launches (PM_OPT_UP_GROUP) or one launch per height
-    const bool grp = sub && c->up_group;
+    // subtree form: LDS-staged sweeps above the plan's first level (PM_OPT_CLUSTER), the levels
+    // below them one launch per height; else grouped post-order launches (PM_OPT_UP_GROUP) or one
+    // launch per height
+    const ClusterPlan& cl = ht.cl;
+    const bool clu = sub && c->cluster && cl.band_wg.size() > 1;
+    const bool grp = sub && c->up_group && !clu;
     const NodeDesc* up_desc = grp ? dt.up_desc_g : sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
     // PM_OPT_SUB_DOWN: S2 / S3 children stay in their parent's pre-order descriptor (k_down<..,
     // SUB>) and leave the tail
@@ -500,7 +693,7 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     if (sub && c->upm == nullptr) return hipErrorInvalidValue;
     up.upm = sub ? c->upm : nullptr;
     up.pslot = grp ? dt.pslot_g : dt.pslot_k;
-    const int H = (int)up_off.size() - 1;
+    const int H = clu ? cl.h0 : (int)up_off.size() - 1;
     // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
     auto narrow_up = [&](int h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
@@ -595,6 +788,19 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
                 const hipError_t je = side_join(c);
                 if (je != hipSuccess) return je;
             }
+            timer_end(c, 0);
+        }
+    }
+
+    if (clu) {   // the sweeps, band by band
+        const ClArgs ca0{dt.cl_items, dt.cl_wg_off, dt.cl_slot_of, 0};
+        for (size_t bnd = 0; bnd + 1 < cl.band_wg.size(); ++bnd) {
+            ClArgs ca = ca0;
+            ca.wg0 = cl.band_wg[bnd];
+            const int64_t nwg = cl.band_wg[bnd + 1] - ca.wg0;
+            if (nwg == 0) continue;
+            timer_begin(c, 0);
+            hipLaunchKernelGGL(k_fitch_up_cluster, dim3((unsigned)(nwg * tiles)), dim3(kClWaves * kWave), 0, c->stream, up, ca);
             timer_end(c, 0);
         }
     }

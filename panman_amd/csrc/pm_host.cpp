@@ -86,6 +86,9 @@ void free_tree(DevTree& t) {
     dev_free(t.vinner);
     dev_free(t.tail_desc_k);
     dev_free(t.lvl);
+    dev_free(t.cl_items);
+    dev_free(t.cl_wg_off);
+    dev_free(t.cl_slot_of);
     t = DevTree{};
 }
 
@@ -224,6 +227,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
     const bool sankoff = mode == PM_MODE_SANKOFF || mode == PM_MODE_BLOCK_SANKOFF;
     const bool block = mode == PM_MODE_BLOCK_FITCH || mode == PM_MODE_BLOCK_SANKOFF;
     const bool nt = nt_policy(c);
+    phase_add("run.nt_loads", nt ? 1.0 : 0.0);   // which build of the passes a launch sequence took
     hipError_t e = sankoff ? (nt ? launch_sankoff_nt(c, block) : launch_sankoff(c, block))
                            : (nt ? launch_fitch_nt(c, block) : launch_fitch(c, block));
     if (e == hipSuccess) e = launch_score(c);
@@ -234,7 +238,7 @@ hipError_t launch_all(pm_ctx* c, int mode) {
 uint64_t graph_key_of(const pm_ctx* c, int mode) {
     const uint64_t parts[] = {(uint64_t)mode, (uint64_t)c->virtual_leaf_parents, (uint64_t)c->subtree_form,
                               (uint64_t)c->narrow_max, (uint64_t)c->group_waves, (uint64_t)c->group_levels, (uint64_t)c->up_group,
-                              (uint64_t)c->sub_down, (uint64_t)c->plain_up, (uint64_t)c->plain_min_waves,
+                              (uint64_t)c->sub_down, (uint64_t)c->plain_up, (uint64_t)c->plain_min_waves, (uint64_t)c->cluster,
                               (uint64_t)(uintptr_t)c->upm,
                               (uint64_t)(uintptr_t)c->sk_parts,
                               (uint64_t)c->leaves_all_present, (uint64_t)c->has_forced, (uint64_t)c->num_sites,
@@ -535,6 +539,12 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
     if (option == PM_OPT_NT_LOADS) {
         if (value < -1 || value > 1) return fail(c, PM_ERR_ARG, "PM_OPT_NT_LOADS: -1 (by level size), 0 or 1");
         c->nt_loads = (int32_t)value;
+        return PM_OK;
+    }
+    if (option == PM_OPT_CLUSTER) {   // 0 off, 1 on; >= 2: on, the plan's level threshold (next tree upload)
+        if (value < 0 || value > ((int64_t)1 << 30)) return fail(c, PM_ERR_ARG, "PM_OPT_CLUSTER: 0, 1 or a level size >= 2");
+        c->cluster = value != 0;
+        if (value >= 2) c->cluster_max_level = (int32_t)value;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
@@ -891,6 +901,14 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
     ht.sshape = sshape;
     upload_phase("subtree form");
+    // LDS-staged post-order sweeps of the subtree form (PM_OPT_CLUSTER, pm_cluster.cpp)
+    plan_clusters(ht, up_order_k, child_enc_k, parent_dense, vleaf, c->cluster_max_level, ht.cl);
+    upload_phase("clusters");
+    // (counts: the sweeps' first level, bands, workgroups per tile, longest workgroup in rounds)
+    phase_add("cluster.first_level", (double)ht.cl.h0);
+    phase_add("cluster.bands", (double)(ht.cl.band_wg.size() - 1));
+    phase_add("cluster.workgroups", (double)(ht.cl.wg_off.size() - 1));
+    phase_add("cluster.max_rounds", (double)ht.cl.max_rounds);
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<NodeDesc> desc(order.size());
         for (size_t k = 0; k < order.size(); ++k) {
@@ -1210,10 +1228,17 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.pslot_gs, pslot_gs)) != hipSuccess ||
         (e = up(&dt.vinner, vinner)) != hipSuccess ||
         (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
-        (e = up(&dt.lvl, lvl)) != hipSuccess) {
+        (e = up(&dt.lvl, lvl)) != hipSuccess ||
+        (e = up(&dt.cl_items, ht.cl.items)) != hipSuccess ||
+        (e = up(&dt.cl_wg_off, ht.cl.wg_off)) != hipSuccess ||
+        (e = up(&dt.cl_slot_of, ht.cl.slot_of)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
+    ht.cl.items.clear();   // (device only)
+    ht.cl.items.shrink_to_fit();
+    ht.cl.slot_of.clear();
+    ht.cl.slot_of.shrink_to_fit();
     c->dt = dt;
     c->tree_bytes = tree_bytes;
     c->ht = std::move(ht);

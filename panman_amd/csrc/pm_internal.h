@@ -132,9 +132,43 @@ struct DevTree {
     int32_t* pslot_g = nullptr;
     int32_t* pslot_gs = nullptr;      // ... of up_desc_gs (Sankoff's groups)
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
+    // LDS-staged post-order sweeps (ClusterPlan on the device)
+    NodeDesc* cl_items = nullptr;
+    int32_t* cl_wg_off = nullptr;
+    int32_t* cl_slot_of = nullptr;
     // level tables on the device (the narrow-band launches walk several levels): the host
     // arrays up_class_off{,_v,_k}, down_level_off{,_v,_k}, down_dense_base_k back to back
     int32_t* lvl = nullptr;
+};
+
+// LDS-staged post-order sweeps (PM_OPT_CLUSTER, pm_cluster.cpp): waves per cluster workgroup,
+// LDS set slots per workgroup (4 KiB each), most heights per band
+constexpr int kClWaves = 4;
+#ifndef PM_CL_SLOTS
+#define PM_CL_SLOTS 8
+#endif
+constexpr int kClSlots = PM_CL_SLOTS;
+#ifndef PM_CL_BAND
+#define PM_CL_BAND 32
+#endif
+constexpr int32_t kClBandHeights = PM_CL_BAND;
+// default PM_OPT_CLUSTER: the sweeps take the post-order from the first height whose level
+// and every level above it hold at most this many materialised nodes
+#ifndef PM_CL_MAX_LEVEL
+#define PM_CL_MAX_LEVEL 4096
+#endif
+constexpr int32_t kClMaxLevel = PM_CL_MAX_LEVEL;
+
+struct ClusterPlan {
+    int32_t h0 = 0;                  // first post-order level (subtree form) the sweeps take
+    int32_t max_rounds = 0;
+    std::vector<NodeDesc> items;     // per workgroup: rounds x kClWaves (node -1: idle wave);
+                                     // parent = the node's LDS slot, pad0 / pad1 its first two
+                                     // children's slots (-1: not in the cluster)
+    std::vector<int32_t> wg_off;     // [workgroups + 1] item offsets
+    std::vector<int32_t> band_wg;    // [bands + 1] workgroup offsets
+    std::vector<int32_t> band_level; // [bands + 1] first level of each band
+    std::vector<int32_t> slot_of;    // [I] a node's slot (children beyond the first two), -1
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
@@ -189,7 +223,15 @@ struct HostTree {
     // offsets of the level tables in DevTree::lvl: [form] = plain, leaf-parent, subtree form,
     // (up only) its Fitch groups, its Sankoff groups
     int64_t lvl_up[5] = {0, 0, 0, 0, 0}, lvl_down[3] = {0, 0, 0}, lvl_base_k = 0;
+    // LDS-staged post-order sweeps of the subtree form (items and slots on the device only)
+    ClusterPlan cl;
 };
+
+// pm_cluster.cpp: the band / cluster / round / slot schedule above the first level of at most
+// max_level nodes (0: none)
+int plan_clusters(const HostTree& ht, const std::vector<int32_t>& up_order_k, const std::vector<int32_t>& child_enc_k,
+                  const std::vector<int32_t>& parent_dense, const std::vector<int32_t>& vleaf, int32_t max_level,
+                  ClusterPlan& out);
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -222,6 +264,8 @@ struct pm_ctx {
     bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
     bool plain_up = true;             // grouped subtree form: plain nodes in the lean post-order kernels (PM_OPT_PLAIN_UP)
     int64_t plain_min_waves = 0;      // ... from this many (node, tile) waves (0: kPlainMinWaves)
+    bool cluster = false;             // Fitch subtree form: LDS-staged post-order sweeps above ht.cl.h0 (PM_OPT_CLUSTER)
+    int32_t cluster_max_level = pm::kClMaxLevel;   // ... their plan's level threshold (at tree upload)
 
     // column shard
     int64_t num_sites = 0;
@@ -405,6 +449,9 @@ struct ReplayDev {
     const int32_t* g_union = nullptr;
     const int64_t* path_off = nullptr;    // [leaves + 1] root-to-leaf node lists
     const int32_t* path = nullptr;
+    // (leaf, tile) rows k_replay_dfs rebuilt from the consensus because an undo stack would
+    // overflow, summed over the runs since replay_prepare (phase "replay.dfs_rebuilds")
+    int32_t* dfs_rebuilds = nullptr;
 };
 #ifndef PM_REPLAY_TILE
 #define PM_REPLAY_TILE 16384

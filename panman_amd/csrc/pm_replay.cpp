@@ -551,6 +551,8 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
         (e = dput(&r.d_g_leaf_off, h.g_leaf_off, c->stream)) != hipSuccess ||
         (e = dput(&r.d_g_union_off, h.g_union_off, c->stream)) != hipSuccess ||
         (e = dput(&r.d_g_union, h.g_union, c->stream)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&r.d_rebuilds), sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemsetAsync(r.d_rebuilds, 0, sizeof(int32_t), c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return hip_fail(c, e, "replay upload");
     clock.lap("replay.upload");
@@ -558,6 +560,11 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     phase_add("replay.max_depth", (double)h.max_depth);
     phase_add("replay.path_chunks", (double)((h.max_depth + kWave - 1) / kWave));
     phase_add("replay.dfs_groups", h.dfs ? (double)(h.g_leaf_off.size() - 1) : 0.0);   // 0: k_replay
+    if (h.dfs) {   // edits k_replay_dfs reads: every edit of each group's path-node union, once per group
+        double ge = 0.0;
+        for (int32_t v : h.g_union) ge += (double)(h.eoff[(size_t)v + 1] - h.eoff[(size_t)v]);
+        phase_add("replay.group_edits", ge);
+    }
     ReplayDev& d = r.dev;
     d.leaves = L;
     d.row_stride = h.stride;
@@ -590,6 +597,7 @@ int replay_prepare(pm_ctx* c, const pm_panmat* p, ReplayState& r, int64_t leaf_b
     d.g_leaf_off = r.d_g_leaf_off;
     d.g_union_off = r.d_g_union_off;
     d.g_union = r.d_g_union;
+    d.dfs_rebuilds = r.d_rebuilds;
     return PM_OK;
 }
 
@@ -616,6 +624,7 @@ void free_replay(pm_ctx* c) {
     dfree(r->d_g_leaf_off);
     dfree(r->d_g_union_off);
     dfree(r->d_g_union);
+    dfree(r->d_rebuilds);
     delete r;
     c->replay = nullptr;
 }
@@ -796,6 +805,12 @@ int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* l
         rc = pm_replay_run(c);
         if (rc == PM_OK && c && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, PM_ERR_HIP, "replay");
         clock.lap("replay.kernel");
+        int32_t rebuilds = 0;   // (a count: k_replay_dfs's (leaf, tile) rows rebuilt after a stack overflow)
+        if (rc == PM_OK && c->replay->dev.dfs) {
+            if (hipMemcpy(&rebuilds, c->replay->d_rebuilds, sizeof(rebuilds), hipMemcpyDeviceToHost) != hipSuccess)
+                rc = fail(c, PM_ERR_HIP, "replay rebuild count");
+            phase_add("replay.dfs_rebuilds", (double)rebuilds);
+        }
     }
     if (rc == PM_OK) rc = pm_replay_format(c, aligned, text, length);
     return rc;

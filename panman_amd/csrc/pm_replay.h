@@ -50,6 +50,7 @@ struct ReplayState {
     uint16_t *d_dfs_len = nullptr, *d_dfs_lpfx = nullptr;
     int64_t* d_path_off = nullptr;
     int32_t* d_path = nullptr;
+    int32_t* d_rebuilds = nullptr;   // [1] ReplayDev::dfs_rebuilds
     bool ran = false;
 };
 

@@ -191,16 +191,6 @@ __device__ __forceinline__ void restore_absent(const ReplayDev& d, int32_t leaf,
 #endif
 constexpr int kReplayGroup = PM_REPLAY_GROUP;
 
-// A workgroup barrier that orders LDS only: each wave's LDS accesses are complete (lgkmcnt)
-// and visible to the others, while its global stores and loads stay in flight.  __syncthreads()
-// is a workgroup release / acquire over global memory too, which on gfx950 waits for every
-// outstanding vector memory operation (vmcnt(0)): behind the write-out that is a full HBM
-// write round trip per tile, and before it the next tile's prefetched edit loads.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 // LDS-DMA copy-in of the consensus tile t (1 KiB per wave-instruction, all in flight).
 __device__ __forceinline__ void tile_copy_in(const ReplayDev& d, int32_t t, uint4* dst, int wave, int lane) {
@@ -429,6 +419,7 @@ __global__ __launch_bounds__(256, PM_REPLAY_WAVES) void k_replay(ReplayDev d) {
 // with the consensus at write-out.  A leaf whose edits would overflow a stack rebuilds its
 // row (consensus copy-in, whole path, nothing pushed), as do the group's later leaves.
 static_assert(kDfsLeaves <= kWave && kDfsUnionCap <= 256, "k_replay_dfs: a lane per leaf, u8 group node indices");
+static_assert(kDfsTile <= 32768, "k_replay_dfs: in-tile columns in 16 bits (undo stacks) and int16 block bounds");
 #ifndef PM_DFS_PCAP
 #define PM_DFS_PCAP 384
 #endif
@@ -822,6 +813,7 @@ __device__ __forceinline__ void dfs_leaf(const ReplayDev& d, DfsLds& S, DfsState
         else dfs_apply<true>(d, S, lo, len, c0, lane, st.psp, st.osp, lo == lp, f);
     } else {
         // rebuild: the consensus again, the whole path, nothing pushed
+        if (lane == 0) atomicAdd(d.dfs_rebuilds, 1);   // (rare; counted for the tests)
         dfs_copy_in(d, S, c0, n, lane);
         __syncthreads();
         dfs_apply<false>(d, S, 0, len, c0, lane, st.psp, st.osp, false, f);

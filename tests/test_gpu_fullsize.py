@@ -24,14 +24,18 @@ CONFIGS = {
     "c2": (panman_amd.random_join_tree, 4096, 15_000),
     "nstar": (panman_amd.random_join_tree, 1_000_000, 30_000),
     "c3": (panman_amd.sars_like_tree, 100_000, 30_000),
-    # C4 (8M leaves x 30k sites over 8 GPUs): one rank's column shard of 3 750 sites
+    # C4 (8M leaves x 30k sites over 8 GPUs): one rank's column shard of 3 750 sites, on the
+    # random-join tree (T1) and on the SARS-like tree (T2: height 442, polytomies of 3-64), the
+    # shape of the authors' 8 M SARS-CoV-2 run (scripts/experiments.sh:72, src/panman.cpp:1568-1613)
     "c4shard": (panman_amd.random_join_tree, 8_000_000, 3_750),
+    "c4shard_t2": (panman_amd.sars_like_tree, 8_000_000, 3_750),
 }
+BIG = ("c4shard", "c4shard_t2")
 
 
 def _samples(config, sites):
     """(first site, count) runs: first word, the tile 0/1 boundary, the ragged last word."""
-    if config == "c4shard":   # 16M nodes: the faithful oracle walks ~1 column per thread-minute
+    if config in BIG:   # 15-16M nodes: the faithful oracle walks ~1 column per thread-minute
         return [(0, 1), (2047, 2), (sites - 1, 1)]
     return [(0, 8), (2044, 8), (sites - 8, 8)]
 
@@ -41,6 +45,7 @@ def trees():
     return {}
 
 
+@pytest.mark.timeout(900)   # the 8M-leaf oracle columns: ~2-3 min on 16 host threads
 @pytest.mark.parametrize("config,mode", [(c, m) for c in CONFIGS for m in ("fitch", "sankoff")
                                          if c != "c4shard" or m == "fitch"])
 def test_full_size_run(oracle, trees, config, mode):
@@ -48,20 +53,48 @@ def test_full_size_run(oracle, trees, config, mode):
     if config not in trees:
         off, idx, root = make(leaves, seed=1)
         trees[config] = (off, idx, root, names_for(off))
-    off, idx, root, names = trees[config]
+    _check_run(oracle, trees[config], leaves, sites, mode, _samples(config, sites),
+               threads=16 if config in BIG else 8)
+
+
+@pytest.mark.parametrize("tree", ["random-join", "sars-like"])
+@pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("mode", ["fitch", "sankoff"])
+def test_forced_load_policy_vs_oracle(oracle, trees, tree, nt, mode):
+    """Both builds of the passes (ordinary set-record loads: pm_fitch.hip / pm_sankoff.hip; the
+    non-temporal copies pm_fitch_nt.hip / pm_sankoff_nt.hip, PM_NT_LOADS) forced on a tree whose
+    widest level holds >= 64k (node, tile) waves (200k leaves x 4096 sites = 2 tiles), each checked
+    against the ORACLE (not against the other build) at 40 sampled columns over every node."""
+    key = f"nt200k_{tree}"
+    make = panman_amd.random_join_tree if tree == "random-join" else panman_amd.sars_like_tree
+    if key not in trees:
+        off, idx, root = make(200_000, seed=3)
+        trees[key] = (off, idx, root, names_for(off))
+    sites = 4096
+    runs = [(0, 8), (1000, 8), (2044, 8), (3000, 8), (sites - 8, 8)]
+    _check_run(oracle, trees[key], 200_000, sites, mode, runs, threads=8, nt=nt)
+
+
+def _check_run(oracle, tree, leaves, sites, mode, runs, threads, nt=None):
+    off, idx, root, names = tree
     n = off.shape[0] - 1
     e = panman_amd.Engine(0)
     try:
         e.tree_upload(off, idx, root)
         e.synth_columns(0, sites, seed=2)
+        if nt is not None:
+            e.set_nt_loads(nt)
+        panman_amd.phase_reset()
         e.run(panman_amd.MODE_FITCH if mode == "fitch" else panman_amd.MODE_SANKOFF)
+        phases = dict(panman_amd.phase_report())
         got = e.mutations()
         score, rootc = e.site_results()
-        runs = _samples(config, sites)
         codes = np.hstack([e.leaf_codes(s0, ns, leaves) for s0, ns in runs])
         cons = np.concatenate([e.consensus(s0, ns) for s0, ns in runs])
     finally:
         e.close()
+    if nt is not None:   # the run took the forced build (phase log of launch_all)
+        assert phases.get("run.nt_loads") == nt, phases
 
     # all columns: order, uniqueness, ranges
     assert got.shape[0] > n // 10
@@ -77,7 +110,8 @@ def test_full_size_run(oracle, trees, config, mode):
     node_row = np.full(n, -1, np.int32)
     node_row[:leaves] = np.arange(leaves)
     _, want, want_root = oracle.csr_columns(off, idx, root, names, codes, node_row, cons, None,
-                                            algo=0 if mode == "fitch" else 1, threads=8, with_root=True)
+                                            algo=0 if mode == "fitch" else 1, threads=threads,
+                                            with_root=True)
     want[:, 1] = cols[want[:, 1]]
     sel = got[np.isin(got[:, 1], cols)]
     assert sel.shape == want.shape and (sel == want).all(), (sel.shape, want.shape)

@@ -54,7 +54,8 @@ def _fasta_checked(engine, pm, aligned, min_chunks=2):
     return text
 
 
-# 200: k_replay_deep (slice bounds in LDS, <= 512 path nodes); 600: k_replay_piped<true>
+# paths over kDfsUnionCap (128) nodes take k_replay: 200 leaves (path bounds in the LDS ring),
+# 600 (deeper than the ring's 512 nodes: bounds of the deeper path nodes from HBM)
 @pytest.mark.parametrize("leaves", [200, 600])
 @pytest.mark.parametrize("aligned", [True, False])
 def test_caterpillar_vs_oracle(engine, oracle, aligned, leaves):
@@ -146,3 +147,26 @@ def test_override_fallback_more_than_cap(engine, oracle, leaves):
             pm.add_nuc_mut(v, 0, start, -1, 0, [[1, 2, 4, 8][(k + i) % 4] for i in range(6)])
     for aligned in (True, False):
         assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_dfs_stack_overflow_rebuild_vs_oracle(engine, oracle, dense):
+    """k_replay_dfs (every path <= 128 nodes) on a 100-leaf caterpillar (paths of 65-99 nodes,
+    one long stem shared by each 16-leaf group): dense edits in one 4 KiB column tile overflow
+    the group-specific undo stacks (kDfsPCap / kDfsOCap), so the leaf that would overflow and the
+    group's later leaves rebuild their rows from the consensus (pm_replay.hip dfs_leaf); sparse
+    edits never do.  The phase log says which kernel ran and how many (leaf, tile) rows were
+    rebuilt; the text must equal the oracle's printFASTAUltraFast (src/fasta.cpp:1789-1979)."""
+    off, idx, root = caterpillar(100)
+    pm = random_panmat(np.random.default_rng(91), off, idx, root, names_for(off), blocks=2,
+                       block_len=(1500, 1800), mut_rate=0.02 if dense else 0.0005, block_rate=0.0)
+    for aligned in (True, False):
+        phase_reset()
+        text = engine.fasta(pm, aligned)
+        ph = dict(phase_report())
+        assert 64 < ph["replay.max_depth"] <= 128 and ph["replay.dfs_groups"] > 0, ph
+        if dense:
+            assert ph["replay.dfs_rebuilds"] > 0, ph
+        else:
+            assert ph["replay.dfs_rebuilds"] == 0, ph
+        assert _records(text) == _records(oracle.fasta(pm, aligned))
