@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--plain-up", type=int, default=-1,
                    help="Fitch: PM_OPT_PLAIN_UP, the grouped post-order's plain nodes in the lean kernel (1) or "
                         "not (0); >= 2: on for launches of at least that many waves; -1: library default")
+    p.add_argument("--cluster", type=int, default=-1,
+                   help="Fitch: PM_OPT_CLUSTER, the post-order's LDS-staged sweeps: 0 off, 1 on, >= 2 on with that "
+                        "level-size threshold; -1: library default")
     p.add_argument("--mode", choices=["fitch", "sankoff", "replay"], default="fitch")
     p.add_argument("--tree", choices=["random-join", "sars-like"], default="random-join",
                    help="SURVEY.md §8d tree family: T1 random-join (N*, C4) or T2 sars-like (C3)")
@@ -126,6 +129,8 @@ def main():
     eng = panman_amd.Engine(local)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
+    if args.cluster >= 0:   # (the plan is built at tree upload)
+        eng.set_cluster(args.cluster)
     panman_amd.phase_reset()
     eng.tree_upload(off, idx, root)
     eng.synth_columns(lo, s_local, seed=2)

@@ -403,8 +403,7 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
 }
 
 // ---- LDS-staged post-order sweeps (PM_OPT_CLUSTER; schedule: pm_cluster.cpp) --------------
-// One workgroup of kClWaves waves = one (cluster, tile); the cluster's rounds bottom-up, one
-// node per wave (a node of out-degree > 3: every wave), an LDS-only barrier between rounds.
+// One wave = one (cluster, tile): the cluster's nodes in depth-first post-order, one per step.
 // A child of the same cluster comes from its LDS slot (16 planes, 4 KiB per (node, tile));
 // every other child as in fitch_up_node (leaf words, a leaf-parent's or S2 / S3 subtree's
 // leaves, or an earlier launch's compressed record).  Records and masks go to HBM exactly as
@@ -413,6 +412,8 @@ struct ClArgs {
     const NodeDesc* items;
     const int32_t* wg_off;
     const int32_t* slot_of;
+    const int32_t* pslot;   // per item: the parent's up slot (parent in a later band), -1
+    int32_t upm_base;       // up slots of item i: UpArgs::upm item upm_base + i (after the level items')
     int32_t wg0;
 };
 typedef uint4 ClSlots[kClSlots][4][kWave];
@@ -431,11 +432,11 @@ __device__ __forceinline__ void slot_write(ClSlots& S, int s, int lane, const ui
 }
 
 // AND if non-empty else OR, forced root, the record + masks to HBM (as fitch_up_node / wide_finish
-// write them; no up slot: every parent of a cluster node is a cluster node, whose children come
-// from a slot or their mask records), the set into the node's slot.
-__device__ __forceinline__ void cluster_finish(const UpArgs& a, const NodeDesc& d, ClSlots& S, int tile, int lane,
-                                               int64_t word, const uint4& cw, uint32_t* both, const uint32_t* either,
-                                               uint32_t vd, uint32_t vd0, uint32_t vd1, bool split) {
+// write them), the (x, s) masks into the parent's up slot when the parent is in a later band
+// (ps = ClArgs::pslot[item]), the set into the node's LDS slot when it is in this cluster.
+__device__ __forceinline__ void cluster_finish(const UpArgs& a, const NodeDesc& d, int32_t ps, ClSlots& S, int tile,
+                                               int lane, int64_t word, const uint4& cw, uint32_t* both,
+                                               const uint32_t* either, uint32_t vd, uint32_t vd0, uint32_t vd1, bool split) {
     const int32_t n = d.node;
     const uint32_t nz = any_plane(both);
 #pragma unroll
@@ -444,8 +445,13 @@ __device__ __forceinline__ void cluster_finish(const UpArgs& a, const NodeDesc& 
         const uint4 F = a.forced[word];
         onehot_from_code(F.x, F.y, F.z, F.w, ~0u, both);
     }
+#ifdef PM_CL_NO_OUTPUT   // (timing-only variant: the chain's LDS work alone)
+    if (d.parent >= 0) slot_write(S, d.parent, lane, both);
+    return;
+#endif
     uint64_t mx, ms, md;
     store_fitch_set(a.sets, a.cmask, cw, n, a.tiles, tile, lane, both, vd != 0u, mx, ms, md);
+    push_up_slot(a, ps, tile, lane, mx, ms);   // (a parent in a later band)
     uint64_t md0 = md, md1 = md;
     if (split) {
         md0 = mx | __ballot(vd0 != 0u);
@@ -456,24 +462,83 @@ __device__ __forceinline__ void cluster_finish(const UpArgs& a, const NodeDesc& 
     if (d.parent >= 0) slot_write(S, d.parent, lane, both);
 }
 
-// A node of out-degree <= 3 (one wave).
-__device__ __forceinline__ void cluster_node(const UpArgs& a, const ClArgs& c, const NodeDesc& d, ClSlots& S, int tile,
-                                             int lane, int64_t word, const uint4& cw) {
+// A narrow item's first two children that are not in the cluster, from memory in two parts:
+// the first load of each (a leaf's word; a leaf-parent's or S2 / S3 subtree's first two leaves;
+// an earlier launch's record code word, addressed through the item's up slot) issued one round
+// ahead of the item's round, so a round waits on LDS only for the common children; the rest (an
+// S2 / S3 subtree's third and fourth leaves, a record's complex lanes) in the round itself.
+struct ClFetch {
+    uint4 c0, x0, c1, x1;
+};
+
+__device__ __forceinline__ void cl_fetch1(const UpArgs& a, int32_t ch, int4 vl, uint64_t mx, uint64_t ms, int tile, int lane,
+                                          int64_t word, uint4& cd, uint4& x) {
+    if (ch < 0) {
+        cd = a.leaf_planes[(size_t)(-ch - 1) * a.wpad + word];
+    } else if (ch & kVirtualBit) {
+        const int32_t l0 = __builtin_amdgcn_readfirstlane(vl.x), l1 = __builtin_amdgcn_readfirstlane(vl.y);
+        cd = a.leaf_planes[(size_t)l0 * a.wpad + word];
+        if (l1 >= 0) x = a.leaf_planes[(size_t)l1 * a.wpad + word];
+    } else {
+        const size_t rec = (size_t)ch * a.tiles + tile;
+        cd = rec_code_all(a.sets + rec * kFitchRec, RecMask{mx, ms, 0, 0, 0}, lane, a.cons, word);
+    }
+}
+
+// The child's 16-plane set from its first load (cd, x) and the rest; vd as child_set_ap's.
+__device__ __forceinline__ void cl_set1(const UpArgs& a, int32_t ch, int4 vl, uint64_t mx, const uint4& cd, const uint4& x,
+                                        int tile, int lane, int64_t word, uint32_t* out, uint32_t& vd) {
+    const LoHi t = lohi_of(cd.x, cd.y, cd.z, cd.w, ~0u);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) out[v] = t.lo[v & 3] & t.hi[v >> 2];
+    if (ch >= 0 && (ch & kVirtualBit)) {
+        const int shape = (ch >> kShapeShift) & 3;
+        if (shape) {   // S2 / S3 (subtree_set_ap): leaves a, b (prefetched), c, d
+            ChildFetch f;
+            f.code = cd;
+            f.v[0] = x;
+            const int32_t l2 = __builtin_amdgcn_readfirstlane(vl.z), l3 = __builtin_amdgcn_readfirstlane(vl.w);
+            f.v[1] = a.leaf_planes[(size_t)l2 * a.wpad + word];
+            if (l3 >= 0) f.v[2] = a.leaf_planes[(size_t)l3 * a.wpad + word];
+            subtree_set_ap(shape, f, out, vd);
+        } else if (__builtin_amdgcn_readfirstlane(vl.y) >= 0) {   // two leaves: their union
+            vd |= code_ne(cd, x);
+            const LoHi u = lohi_of(x.x, x.y, x.z, x.w, ~0u);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) out[v] |= u.lo[v & 3] & u.hi[v >> 2];
+        }
+    } else if (ch >= 0 && mx != 0 && ((mx >> lane) & 1ull)) {   // a record's complex lane
+        const uint4* p = a.sets + ((size_t)ch * a.tiles + tile) * kFitchRec + kWave + lanes_below(mx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 w = load_rec(p + q * kWave);
+            out[4 * q] = w.x; out[4 * q + 1] = w.y; out[4 * q + 2] = w.z; out[4 * q + 3] = w.w;
+        }
+    }
+}
+
+__device__ __forceinline__ void cluster_issue(const UpArgs& a, const NodeDesc& d, const UpSlots& sl, int tile, int lane,
+                                              int64_t word, ClFetch& p) {
+    if (d.node < 0 || d.e1 - d.e0 > 3) return;
+    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
+    if (d.pad0 < 0) cl_fetch1(a, d.c0, vl0, sl.x0, sl.s0, tile, lane, word, p.c0, p.x0);
+    if (d.e1 - d.e0 > 1 && d.pad1 < 0) cl_fetch1(a, d.c1, vl1, sl.x1, sl.s1, tile, lane, word, p.c1, p.x1);
+}
+
+// A node of out-degree <= 3 (one wave); its out-of-cluster first two children's first loads in `p`.
+__device__ __forceinline__ void cluster_node(const UpArgs& a, const ClArgs& c, const NodeDesc& d, const UpSlots& sl, int32_t ps,
+                                             const ClFetch& p, ClSlots& S, int tile, int lane, int64_t word, const uint4& cw) {
     const bool two = d.e1 - d.e0 > 1;
     const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
-    ChildFetch f0, f1;   // the children from memory: both loads in flight before either is used
-    if (d.pad0 < 0) fetch_child_ap<kFitchRec, false, true>(a, d.c0, vl0, tile, lane, word, f0);
-    if (two && d.pad1 < 0) fetch_child_ap<kFitchRec, false, true>(a, d.c1, vl1, tile, lane, word, f1);
-    __builtin_amdgcn_sched_barrier(0);
     uint32_t both[16], either[16], vd0 = 0, vd1 = 0;
     if (d.pad0 >= 0) slot_read(S, d.pad0, lane, both);
-    else child_set_ap<true>(d.c0, vl0, f0, both, vd0);
+    else cl_set1(a, d.c0, vl0, sl.x0, p.c0, p.x0, tile, lane, word, both, vd0);
 #pragma unroll
     for (int v = 0; v < 16; ++v) either[v] = both[v];
     if (two) {
         uint32_t y[16];
         if (d.pad1 >= 0) slot_read(S, d.pad1, lane, y);
-        else child_set_ap<true>(d.c1, vl1, f1, y, vd1);
+        else cl_set1(a, d.c1, vl1, sl.x1, p.c1, p.x1, tile, lane, word, y, vd1);
 #pragma unroll
         for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
     }
@@ -491,103 +556,130 @@ __device__ __forceinline__ void cluster_node(const UpArgs& a, const ClArgs& c, c
             fold_child<true>(a, ch, vl, tile, lane, word, both, either, vd);
         }
     }
-    cluster_finish(a, d, S, tile, lane, word, cw, both, either, vd, vd0, vd1, true);
+    cluster_finish(a, d, ps, S, tile, lane, word, cw, both, either, vd, vd0, vd1, true);
 }
 
-// A node of out-degree > 3: its round's waves take children wave, wave + kClWaves, ...; the
-// accumulators meet in LDS (AND / OR atomics, src/fitchSankoff.cpp:39-55 is commutative), wave 0
-// finishes.  Every wave of the workgroup runs this (the round is the node's alone).
-__device__ __forceinline__ void cluster_wide(const UpArgs& a, const ClArgs& c, const NodeDesc& d, ClSlots& S,
-                                             uint32_t (*acc)[kWave], int wave, int tile, int lane, int64_t word,
-                                             const uint4& cw) {
+// A node of out-degree > 3.  Such nodes' children are mostly leaves (T2: 96 %): eight leaf
+// words are loaded at a time before any is folded; other children (a leaf-parent's leaves, an
+// LDS slot, a record) one at a time.
+constexpr int kClWideBatch = 8;
+__device__ __forceinline__ void cluster_wide(const UpArgs& a, const ClArgs& c, const NodeDesc& d, int32_t ps, ClSlots& S,
+                                             int tile, int lane, int64_t word, const uint4& cw) {
     uint32_t both[16], either[16], vd = 0;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { both[v] = ~0u; either[v] = 0u; }
-    for (int32_t base = d.e0 + wave; base < d.e1; base += kClWaves * kWave) {
-        const int32_t my = base + kClWaves * lane;
+    for (int32_t base = d.e0; base < d.e1; base += kWave) {
+        const int32_t my = base + lane;
         const int32_t enc = my < d.e1 ? a.child_enc[my] : 0;
-        const bool mat = my < d.e1 && materialised(enc);
-        const int32_t sl = mat ? c.slot_of[enc] : -1;
-        const int4 vl = my < d.e1 && enc >= 0 && (enc & kVirtualBit) ? a.vleaf[enc & kDenseMask] : make_int4(-1, -1, -1, -1);
-        uint64_t cmx = 0, cms = 0;   // a record child's masks, one child per lane
-        if (mat && sl < 0) {
-            const uint64_t* q = a.cmask + kMaskWords * ((size_t)enc * a.tiles + tile);
-            cmx = q[0];
-            cms = q[1];
-        }
-        const int cnt = min(kWave, (d.e1 - base + kClWaves - 1) / kClWaves);
-        for (int k = 0; k < cnt; k += 2) {
-            const bool two = k + 1 < cnt;
-            const int32_t c0 = __builtin_amdgcn_readlane(enc, k), c1 = two ? __builtin_amdgcn_readlane(enc, k + 1) : 0;
-            const int32_t s0 = __builtin_amdgcn_readlane(sl, k), s1 = two ? __builtin_amdgcn_readlane(sl, k + 1) : -1;
-            const int4 v0 = make_int4(__builtin_amdgcn_readlane(vl.x, k), __builtin_amdgcn_readlane(vl.y, k), -1, -1);
-            const int4 v1 = two ? make_int4(__builtin_amdgcn_readlane(vl.x, k + 1), __builtin_amdgcn_readlane(vl.y, k + 1), -1, -1)
-                                : make_int4(-1, -1, -1, -1);
-            ChildFetch f0, f1;
-            if (s0 < 0) fetch_child_ap_m(a, c0, v0, readlane64(cmx, k), readlane64(cms, k), tile, lane, word, f0);
-            if (two && s1 < 0) fetch_child_ap_m(a, c1, v1, readlane64(cmx, k + 1), readlane64(cms, k + 1), tile, lane, word, f1);
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t y[16];
-            if (s0 >= 0) {
-                slot_read(S, s0, lane, y);
+        const int cnt = min(kWave, d.e1 - base);
+        for (int k = 0; k < cnt; k += kClWideBatch) {
+            uint4 L[kClWideBatch];
 #pragma unroll
-                for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
-            } else {
-                fold_child_ap(c0, v0, f0, both, either, vd);
+            for (int j = 0; j < kClWideBatch; ++j) {
+                const int32_t ch = k + j < cnt ? __builtin_amdgcn_readlane(enc, k + j) : 0;
+                if (k + j < cnt && ch < 0) L[j] = a.leaf_planes[(size_t)(-ch - 1) * a.wpad + word];
             }
-            if (two) {
-                if (s1 >= 0) {
-                    slot_read(S, s1, lane, y);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < kClWideBatch; ++j) {
+                if (k + j >= cnt) break;
+                const int32_t ch = __builtin_amdgcn_readlane(enc, k + j);
+                if (ch < 0) {   // a leaf (src/fitchSankoff.cpp:32-38)
+                    const LoHi t = lohi_of(L[j].x, L[j].y, L[j].z, L[j].w, ~0u);
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) {
+                        const uint32_t x = t.lo[v & 3] & t.hi[v >> 2];
+                        both[v] &= x;
+                        either[v] |= x;
+                    }
+                    continue;
+                }
+                const int32_t sl = materialised(ch) ? __builtin_amdgcn_readfirstlane(c.slot_of[ch]) : -1;
+                if (sl >= 0) {
+                    uint32_t y[16];
+                    slot_read(S, sl, lane, y);
 #pragma unroll
                     for (int v = 0; v < 16; ++v) { either[v] |= y[v]; both[v] &= y[v]; }
                 } else {
-                    fold_child_ap(c1, v1, f1, both, either, vd);
+                    const int4 vl = (ch & kVirtualBit) ? a.vleaf[ch & kDenseMask] : make_int4(-1, -1, -1, -1);
+                    fold_child<true>(a, ch, vl, tile, lane, word, both, either, vd);
                 }
             }
         }
     }
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        atomicAnd(&acc[v][lane], both[v]);
-        atomicOr(&acc[16 + v][lane], either[v]);
-    }
-    atomicOr(&acc[32][lane], vd);
-    lds_barrier();
-    if (wave == 0) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            both[v] = acc[v][lane];
-            either[v] = acc[16 + v][lane];
-            acc[v][lane] = ~0u;   // (reset for the next wide round; read by wave 0 only until then)
-            acc[16 + v][lane] = 0u;
-        }
-        vd = acc[32][lane];
-        acc[32][lane] = 0u;
-        cluster_finish(a, d, S, tile, lane, word, cw, both, either, vd, 0, 0, false);
-    }
+    cluster_finish(a, d, ps, S, tile, lane, word, cw, both, either, vd, 0, 0, false);
 }
 
-__global__ __launch_bounds__(kClWaves * kWave) void k_fitch_up_cluster(UpArgs a, ClArgs c) {
+// An item's descriptor, up slots and up-slot target, fetched as one VECTOR load (lane k < 16:
+// descriptor dword k; 16..23: the up slots' dwords; 24..: the target) and moved to scalar
+// registers one round later: a scalar load in flight would hold every LDS barrier of the round
+// (s_waitcnt lgkmcnt(0) covers both).
+struct ClMeta {
+    NodeDesc d;
+    UpSlots s;
+    int32_t ps;
+};
+
+__device__ __forceinline__ uint32_t cl_meta_load(const UpArgs& a, const ClArgs& c, int32_t it, int tile, int lane) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(c.pslot + it);
+    if (lane < 16) src = reinterpret_cast<const uint32_t*>(c.items + it) + lane;
+    else if (lane < 24) src = reinterpret_cast<const uint32_t*>(a.upm + ((size_t)(c.upm_base + it) * a.tiles + tile) * 4) + (lane - 16);
+    return *src;
+}
+
+__device__ __forceinline__ void cl_meta_get(uint32_t m, ClMeta& x) {
+    int32_t* p = reinterpret_cast<int32_t*>(&x.d);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] = __builtin_amdgcn_readlane((int)m, k);
+    auto u64 = [&](int k) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m, k + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)m, k);
+    };
+    x.s = UpSlots{u64(16), u64(18), u64(20), u64(22)};
+    x.ps = __builtin_amdgcn_readlane((int)m, 24);
+}
+
+__device__ __forceinline__ void cluster_step(const UpArgs& a, const ClArgs& c, const ClMeta& m, const ClFetch& p, ClSlots& S,
+                                             int tile, int lane, int64_t word, const uint4& cw) {
+    if (m.d.e1 - m.d.e0 > 3) cluster_wide(a, c, m.d, m.ps, S, tile, lane, word, cw);
+    else cluster_node(a, c, m.d, m.s, m.ps, p, S, tile, lane, word, cw);
+}
+
+#ifndef PM_CL_WAVES   // waves per SIMD (occupancy bound of the sweep kernel)
+#define PM_CL_WAVES 3
+#endif
+__global__ __launch_bounds__(kWave, PM_CL_WAVES) void k_fitch_up_cluster(UpArgs a, ClArgs c) {
     __shared__ ClSlots S;
-    __shared__ uint32_t acc[33][kWave];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lane = threadIdx.x;
     const int32_t b = (int32_t)blockIdx.x;
     const int32_t wl = b / a.tiles;
     const int tile = b - wl * a.tiles;
-    const int32_t i0 = c.wg_off[c.wg0 + wl], rounds = (c.wg_off[c.wg0 + wl + 1] - i0) / kClWaves;
+    const int32_t i0 = c.wg_off[c.wg0 + wl], steps = c.wg_off[c.wg0 + wl + 1] - i0;
     const int64_t word = (int64_t)tile * kWave + lane;
     const uint4 cw = a.cons[word];
-    if (wave == 0) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) { acc[v][lane] = ~0u; acc[16 + v][lane] = 0u; }
-        acc[32][lane] = 0u;
-    }
-    lds_barrier();
-    for (int32_t r = 0; r < rounds; ++r) {
-        const NodeDesc& d = c.items[i0 + r * kClWaves + wave];
-        if (d.e1 - d.e0 > 3) cluster_wide(a, c, d, S, acc, wave, tile, lane, word, cw);   // (uniform over the workgroup)
-        else if (d.node >= 0) cluster_node(a, c, d, S, tile, lane, word, cw);
-        lds_barrier();
+    // Software pipeline over steps: step r's children loads are issued at the start of step
+    // r - 1 (two fetch buffers whose roles alternate: a register copy of a load's destination
+    // would wait for the load), its descriptor one step before that.
+    ClMeta M0, M1;
+    ClFetch fA, fB;
+    cl_meta_get(cl_meta_load(a, c, i0, tile, lane), M0);
+    cluster_issue(a, M0.d, M0.s, tile, lane, word, fA);
+    uint32_t m1 = steps > 1 ? cl_meta_load(a, c, i0 + 1, tile, lane) : 0u;
+    for (int32_t r = 0; r < steps; r += 2) {
+        // step r (M0, fA); step r + 1's loads into fB; step r + 2's descriptor
+        const uint32_t m2 = r + 2 < steps ? cl_meta_load(a, c, i0 + r + 2, tile, lane) : 0u;
+        if (r + 1 < steps) {
+            cl_meta_get(m1, M1);
+            cluster_issue(a, M1.d, M1.s, tile, lane, word, fB);
+        }
+        cluster_step(a, c, M0, fA, S, tile, lane, word, cw);
+        if (r + 1 >= steps) break;
+        // step r + 1 (M1, fB); step r + 2's loads into fA; step r + 3's descriptor
+        m1 = r + 3 < steps ? cl_meta_load(a, c, i0 + r + 3, tile, lane) : 0u;
+        if (r + 2 < steps) {
+            cl_meta_get(m2, M0);
+            cluster_issue(a, M0.d, M0.s, tile, lane, word, fA);
+        }
+        cluster_step(a, c, M1, fB, S, tile, lane, word, cw);
     }
 }
 
@@ -657,9 +749,12 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     // subtree form: LDS-staged sweeps above the plan's first level (PM_OPT_CLUSTER), the levels
     // below them one launch per height; else grouped post-order launches (PM_OPT_UP_GROUP) or one
     // launch per height
+    // (with a sweep plan the grouped order stops below the sweeps: without them, one launch per
+    // height)
     const ClusterPlan& cl = ht.cl;
-    const bool clu = sub && c->cluster && cl.band_wg.size() > 1;
-    const bool grp = sub && c->up_group && !clu;
+    const bool planned = cl.band_wg.size() > 1;
+    const bool clu = sub && c->cluster && planned;
+    const bool grp = sub && c->up_group && (clu || !planned);
     const NodeDesc* up_desc = grp ? dt.up_desc_g : sub ? dt.up_desc_k : virt ? dt.up_desc_v : dt.up_desc;
     // PM_OPT_SUB_DOWN: S2 / S3 children stay in their parent's pre-order descriptor (k_down<..,
     // SUB>) and leave the tail
@@ -692,8 +787,8 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     // up slots: the subtree form's kernels (alloc_work sizes them for its two up orders)
     if (sub && c->upm == nullptr) return hipErrorInvalidValue;
     up.upm = sub ? c->upm : nullptr;
-    up.pslot = grp ? dt.pslot_g : dt.pslot_k;
-    const int H = clu ? cl.h0 : (int)up_off.size() - 1;
+    up.pslot = grp ? (clu ? dt.pslot_gc : dt.pslot_g) : clu ? dt.pslot_kc : dt.pslot_k;
+    const int H = clu && !grp ? cl.h0 : (int)up_off.size() - 1;   // (the grouped order holds the levels below h0 only)
     // runs of >= 2 narrow levels (PM_OPT_NARROW): one band launch each
     auto narrow_up = [&](int h) {
         const int32_t b = class_off[h * kDegreeClasses], m = class_off[h * kDegreeClasses + 1],
@@ -793,14 +888,14 @@ hipError_t launch_fitch(pm_ctx* c, bool block) {
     }
 
     if (clu) {   // the sweeps, band by band
-        const ClArgs ca0{dt.cl_items, dt.cl_wg_off, dt.cl_slot_of, 0};
+        const ClArgs ca0{dt.cl_items, dt.cl_wg_off, dt.cl_slot_of, dt.cl_pslot, cl.upm_base, 0};
         for (size_t bnd = 0; bnd + 1 < cl.band_wg.size(); ++bnd) {
             ClArgs ca = ca0;
             ca.wg0 = cl.band_wg[bnd];
             const int64_t nwg = cl.band_wg[bnd + 1] - ca.wg0;
             if (nwg == 0) continue;
             timer_begin(c, 0);
-            hipLaunchKernelGGL(k_fitch_up_cluster, dim3((unsigned)(nwg * tiles)), dim3(kClWaves * kWave), 0, c->stream, up, ca);
+            hipLaunchKernelGGL(k_fitch_up_cluster, dim3((unsigned)(nwg * tiles)), dim3(kWave), 0, c->stream, up, ca);
             timer_end(c, 0);
         }
     }

@@ -89,6 +89,9 @@ void free_tree(DevTree& t) {
     dev_free(t.cl_items);
     dev_free(t.cl_wg_off);
     dev_free(t.cl_slot_of);
+    dev_free(t.pslot_kc);
+    dev_free(t.pslot_gc);
+    dev_free(t.cl_pslot);
     t = DevTree{};
 }
 
@@ -175,7 +178,8 @@ int alloc_work(pm_ctx* c, int mode) {
     }
     // up slots: Fitch / Sankoff, subtree form (every leaf present, some S2 / S3 node)
     if ((mode == PM_MODE_FITCH || mode == PM_MODE_SANKOFF) && c->subtree_form && c->ht.num_sshape > 0) {
-        const size_t items = (size_t)std::max(c->ht.up_items_k, std::max(c->ht.up_items_g, c->ht.up_items_gs));
+        const size_t items = (size_t)std::max(c->ht.cl.upm_base + c->ht.cl.n_items,
+                                              std::max(c->ht.up_items_k, std::max(c->ht.up_items_g, c->ht.up_items_gs)));
         const size_t need = items * (wpad / kWave) * 4 * sizeof(uint64_t);
         if (need > c->upm_bytes) {
             dev_free(c->upm);
@@ -541,10 +545,13 @@ int pm_set_option(pm_ctx* c, int option, int64_t value) {
         c->nt_loads = (int32_t)value;
         return PM_OK;
     }
-    if (option == PM_OPT_CLUSTER) {   // 0 off, 1 on; >= 2: on, the plan's level threshold (next tree upload)
+    // 0 off (and no plan at the next tree upload: the grouped post-order covers every level);
+    // 1 on (the default plan); >= 2 on, that level threshold and no bushiness test (next tree upload)
+    if (option == PM_OPT_CLUSTER) {
         if (value < 0 || value > ((int64_t)1 << 30)) return fail(c, PM_ERR_ARG, "PM_OPT_CLUSTER: 0, 1 or a level size >= 2");
         c->cluster = value != 0;
-        if (value >= 2) c->cluster_max_level = (int32_t)value;
+        c->cluster_max_level = value == 0 ? 0 : value == 1 ? kClMaxLevel : (int32_t)value;
+        c->cluster_chain = value == 1;
         return PM_OK;
     }
     if (option == PM_OPT_GRAPH) {
@@ -902,12 +909,12 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.sshape = sshape;
     upload_phase("subtree form");
     // LDS-staged post-order sweeps of the subtree form (PM_OPT_CLUSTER, pm_cluster.cpp)
-    plan_clusters(ht, up_order_k, child_enc_k, parent_dense, vleaf, c->cluster_max_level, ht.cl);
+    plan_clusters(ht, up_order_k, child_enc_k, parent_dense, vleaf, c->cluster_max_level, c->cluster_chain, ht.cl);
     upload_phase("clusters");
     // (counts: the sweeps' first level, bands, workgroups per tile, longest workgroup in rounds)
     phase_add("cluster.first_level", (double)ht.cl.h0);
-    phase_add("cluster.bands", (double)(ht.cl.band_wg.size() - 1));
-    phase_add("cluster.workgroups", (double)(ht.cl.wg_off.size() - 1));
+    phase_add("cluster.bands", ht.cl.band_wg.empty() ? 0.0 : (double)(ht.cl.band_wg.size() - 1));
+    phase_add("cluster.workgroups", ht.cl.wg_off.empty() ? 0.0 : (double)(ht.cl.wg_off.size() - 1));
     phase_add("cluster.max_rounds", (double)ht.cl.max_rounds);
     auto make_desc = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<NodeDesc> desc(order.size());
@@ -953,14 +960,19 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     // (height order).  Only nodes of heights with at most kUpGroupNodes nodes join a child's
     // launch: big levels fill the chip by themselves and pay for the recomputation (measured
     // at N*).
+    // `levels`: only the subtree form's first `levels` post-order levels (Fitch with the LDS-staged
+    // sweeps: the levels below them; the sweeps take the rest).
+    const std::vector<int32_t>& up_order_k_all = up_order_k;
     auto make_groups = [&](int32_t max_rc, std::vector<int32_t>& level_off, std::vector<int32_t>& class_off,
                            std::vector<uint8_t>& leafy_out, std::vector<uint8_t>& recomp_out,
-                           std::vector<int32_t>& plain_out) {
+                           std::vector<int32_t>& plain_out, int32_t levels) {
+        levels = std::min<int32_t>(levels, (int32_t)ht.up_level_off_k.size() - 1);
+        const std::vector<int32_t> up_order_k(up_order_k_all.begin(), up_order_k_all.begin() + ht.up_level_off_k[levels]);
         auto is_mat = [](int32_t x) { return x >= 0 && !(x & kVirtualBit); };
         auto narrow = [&](int32_t d) { return degree_class(ht.child_off[d + 1] - ht.child_off[d]) == 0; };
         auto recomputable = [&](int32_t d) { return ht.child_off[d + 1] - ht.child_off[d] <= max_rc; };
         std::vector<int32_t> lv(I, -1), inl((size_t)I * 2, -1), hsize(I, 0);
-        for (size_t h = 0; h + 1 < ht.up_level_off_k.size(); ++h)
+        for (int32_t h = 0; h < levels; ++h)
             for (int32_t i = ht.up_level_off_k[h]; i < ht.up_level_off_k[h + 1]; ++i)
                 hsize[up_order_k[i]] = ht.up_level_off_k[h + 1] - ht.up_level_off_k[h];
         std::vector<uint8_t> gen(I, 0);
@@ -1034,7 +1046,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         }
         return std::make_pair(desc, order);
     };
-    const auto groups_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g, ht.up_plain_g);
+    // (with a sweep plan the grouped Fitch launches stop below its first level: ht.cl.h0)
+    const int32_t all_levels = (int32_t)ht.up_level_off_k.size() - 1;
+    const auto groups_g = make_groups(3, ht.up_level_off_g, ht.up_class_off_g, ht.up_leafy_g, ht.up_recomp_g, ht.up_plain_g,
+                                      ht.cl.band_wg.size() > 1 ? ht.cl.h0 : all_levels);
     const std::vector<NodeDesc>& up_desc_g = groups_g.first;
     // up slots: each descriptor's parent item and child slot (the parent's first / second
     // child) in the same array, for the subtree form's two up orders
@@ -1049,11 +1064,37 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         return ps;
     };
     const std::vector<int32_t> pslot_k = make_pslot(up_order_k, up_desc_k), pslot_g = make_pslot(groups_g.second, up_desc_g);
+    // with the sweeps: a level item (either up order) whose parent is swept pushes into the
+    // parent's sweep item's up slot (item cl.upm_base + item); a swept node whose parent is in a
+    // later band likewise (a parent in its own cluster reads its LDS slot instead)
+    std::vector<int32_t> pslot_kc(pslot_k), pslot_gc(pslot_g), cl_pslot(ht.cl.items.size(), -1);
+    ht.cl.upm_base = (int32_t)std::max(up_desc_k.size(), up_desc_g.size());
+    {
+        std::vector<int32_t> pos_k(I, -1), pos_g(I, -1);
+        for (size_t k = 0; k < up_desc_k.size(); ++k) pos_k[up_order_k[k]] = (int32_t)k;
+        for (size_t k = 0; k < groups_g.second.size(); ++k) pos_g[groups_g.second[k]] = (int32_t)k;
+        for (int32_t p = 0; p < I && !ht.cl.item_of.empty(); ++p) {
+            if (ht.cl.item_of[p] < 0) continue;   // swept parents: their first two materialised children
+            const int32_t e0 = ht.child_off[p], e1 = ht.child_off[p + 1];
+            for (int j = 0; j < 2 && e0 + j < e1; ++j) {
+                const int32_t x = child_enc_k[e0 + j];
+                if (x < 0 || (x & kVirtualBit)) continue;
+                const int32_t to = (ht.cl.upm_base + ht.cl.item_of[p]) * 2 + j;
+                if (ht.cl.item_of[x] >= 0) {
+                    cl_pslot[ht.cl.item_of[x]] = ht.cl.slot_of[x] >= 0 ? -1 : to;
+                } else {
+                    if (pos_k[x] >= 0) pslot_kc[pos_k[x]] = to;
+                    if (pos_g[x] >= 0) pslot_gc[pos_g[x]] = to;
+                }
+            }
+        }
+    }
     ht.up_items_k = (int32_t)up_desc_k.size();
     ht.up_items_g = (int32_t)up_desc_g.size();
     // Sankoff: binary recomputed children; its part descriptors are the subtree form's (nodes
     // above 255 children never group), so pad0 / pad1 here index the grouped array only
-    auto groups_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs, ht.up_plain_gs);
+    auto groups_gs = make_groups(2, ht.up_level_off_gs, ht.up_class_off_gs, ht.up_leafy_gs, ht.up_recomp_gs, ht.up_plain_gs,
+                                 all_levels);
     std::vector<NodeDesc> up_desc_gs = groups_gs.first;
     const std::vector<int32_t> pslot_gs = make_pslot(groups_gs.second, up_desc_gs);
     ht.up_items_gs = (int32_t)up_desc_gs.size();
@@ -1231,7 +1272,10 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.lvl, lvl)) != hipSuccess ||
         (e = up(&dt.cl_items, ht.cl.items)) != hipSuccess ||
         (e = up(&dt.cl_wg_off, ht.cl.wg_off)) != hipSuccess ||
-        (e = up(&dt.cl_slot_of, ht.cl.slot_of)) != hipSuccess) {
+        (e = up(&dt.cl_slot_of, ht.cl.slot_of)) != hipSuccess ||
+        (e = up(&dt.pslot_kc, pslot_kc)) != hipSuccess ||
+        (e = up(&dt.pslot_gc, pslot_gc)) != hipSuccess ||
+        (e = up(&dt.cl_pslot, cl_pslot)) != hipSuccess) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
@@ -1239,6 +1283,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     ht.cl.items.shrink_to_fit();
     ht.cl.slot_of.clear();
     ht.cl.slot_of.shrink_to_fit();
+    ht.cl.item_of.clear();
+    ht.cl.item_of.shrink_to_fit();
     c->dt = dt;
     c->tree_bytes = tree_bytes;
     c->ht = std::move(ht);

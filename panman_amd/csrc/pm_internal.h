@@ -136,39 +136,55 @@ struct DevTree {
     NodeDesc* cl_items = nullptr;
     int32_t* cl_wg_off = nullptr;
     int32_t* cl_slot_of = nullptr;
+    // up slots with the sweeps (UpArgs::upm: the level items', then the sweep items' at
+    // up_items_k + item): the level items' pslot, and each sweep item's (its parent in a later band)
+    int32_t* pslot_kc = nullptr;
+    int32_t* pslot_gc = nullptr;
+    int32_t* cl_pslot = nullptr;
     // level tables on the device (the narrow-band launches walk several levels): the host
     // arrays up_class_off{,_v,_k}, down_level_off{,_v,_k}, down_dense_base_k back to back
     int32_t* lvl = nullptr;
 };
 
-// LDS-staged post-order sweeps (PM_OPT_CLUSTER, pm_cluster.cpp): waves per cluster workgroup,
-// LDS set slots per workgroup (4 KiB each), most heights per band
-constexpr int kClWaves = 4;
+// LDS-staged post-order sweeps (PM_OPT_CLUSTER, pm_cluster.cpp): LDS set slots per cluster wave
+// (4 KiB each), most nodes per cluster, most heights per band
 #ifndef PM_CL_SLOTS
-#define PM_CL_SLOTS 8
+#define PM_CL_SLOTS 4
 #endif
 constexpr int kClSlots = PM_CL_SLOTS;
+#ifndef PM_CL_MAX_STEPS
+#define PM_CL_MAX_STEPS 64
+#endif
+constexpr int32_t kClMaxSteps = PM_CL_MAX_STEPS;
 #ifndef PM_CL_BAND
 #define PM_CL_BAND 32
 #endif
 constexpr int32_t kClBandHeights = PM_CL_BAND;
 // default PM_OPT_CLUSTER: the sweeps take the post-order from the first height whose level
-// and every level above it hold at most this many materialised nodes
+// and every level above it hold at most this many materialised nodes (and above the last band
+// whose clusters are bushy: more than kClChain nodes per level in its longest cluster)
 #ifndef PM_CL_MAX_LEVEL
-#define PM_CL_MAX_LEVEL 4096
+#define PM_CL_MAX_LEVEL (1 << 20)
 #endif
+#ifndef PM_CL_CHAIN
+#define PM_CL_CHAIN 4
+#endif
+constexpr int32_t kClChain = PM_CL_CHAIN;
 constexpr int32_t kClMaxLevel = PM_CL_MAX_LEVEL;
 
 struct ClusterPlan {
     int32_t h0 = 0;                  // first post-order level (subtree form) the sweeps take
-    int32_t max_rounds = 0;
-    std::vector<NodeDesc> items;     // per workgroup: rounds x kClWaves (node -1: idle wave);
-                                     // parent = the node's LDS slot, pad0 / pad1 its first two
-                                     // children's slots (-1: not in the cluster)
-    std::vector<int32_t> wg_off;     // [workgroups + 1] item offsets
-    std::vector<int32_t> band_wg;    // [bands + 1] workgroup offsets
+    int32_t max_rounds = 0;          // steps of the longest cluster
+    std::vector<NodeDesc> items;     // per cluster: its nodes in step order; parent = the node's
+                                     // LDS slot, pad0 / pad1 its first two children's slots (-1:
+                                     // not in the cluster)
+    std::vector<int32_t> wg_off;     // [clusters + 1] item offsets
+    std::vector<int32_t> band_wg;    // [bands + 1] cluster offsets
     std::vector<int32_t> band_level; // [bands + 1] first level of each band
     std::vector<int32_t> slot_of;    // [I] a node's slot (children beyond the first two), -1
+    std::vector<int32_t> item_of;    // [I] a swept node's (first) item, -1
+    int32_t n_items = 0;
+    int32_t upm_base = 0;            // the items' up slots follow both up orders' (UpArgs::upm)
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
@@ -231,7 +247,7 @@ struct HostTree {
 // max_level nodes (0: none)
 int plan_clusters(const HostTree& ht, const std::vector<int32_t>& up_order_k, const std::vector<int32_t>& child_enc_k,
                   const std::vector<int32_t>& parent_dense, const std::vector<int32_t>& vleaf, int32_t max_level,
-                  ClusterPlan& out);
+                  bool chain_check, ClusterPlan& out);
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -264,8 +280,9 @@ struct pm_ctx {
     bool sub_down = false;            // Fitch subtree form: S2 / S3 records in their parent's pre-order wave (PM_OPT_SUB_DOWN)
     bool plain_up = true;             // grouped subtree form: plain nodes in the lean post-order kernels (PM_OPT_PLAIN_UP)
     int64_t plain_min_waves = 0;      // ... from this many (node, tile) waves (0: kPlainMinWaves)
-    bool cluster = false;             // Fitch subtree form: LDS-staged post-order sweeps above ht.cl.h0 (PM_OPT_CLUSTER)
+    bool cluster = true;              // Fitch subtree form: LDS-staged post-order sweeps above ht.cl.h0 (PM_OPT_CLUSTER)
     int32_t cluster_max_level = pm::kClMaxLevel;   // ... their plan's level threshold (at tree upload)
+    bool cluster_chain = true;        // ... and only above the last bushy band (the default; an explicit threshold: off)
 
     // column shard
     int64_t num_sites = 0;

