@@ -319,7 +319,11 @@ def parsimony_block(args, eng, mode, ctx):
         for _ in range(args.steps):
             eng.run(mode)
         torch.cuda.synchronize()
-    ms, launches = eng.kernel_times(3)
+    ms, launches = eng.kernel_times(6)
+    # the pre-order pass = its levels / sweeps (class 1) + its tail launch (class 5)
+    tail_ms, tail_launches = ms[5], launches[5]
+    ms[1] += tail_ms
+    launches[1] += tail_launches
     eng.set_profiling(False)
     design = eng.design_bytes()   # counted from the last run's record masks (untimed)
     if world > 1:
@@ -335,7 +339,7 @@ def parsimony_block(args, eng, mode, ctx):
     updates = float(S) * n_nodes * args.steps
     value = updates / elapsed
     ms_step = elapsed * 1e3 / args.steps
-    roofline = roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank)
+    roofline = roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail_ms, tail_launches)
     name = "fitch" if mode == panman_amd.MODE_FITCH else "sankoff"
     return {"metric": f"Fitch-Sankoff site*node updates/sec ({name} mode)", "value": value,
             "unit": "site*node updates/s", "ms_per_step": ms_step, "mutations_total": muts_total,
@@ -343,7 +347,7 @@ def parsimony_block(args, eng, mode, ctx):
             "config": {"workload": workload_label(name, args.tree, L, S, world), "sites_per_gpu": s_local}}
 
 
-def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
+def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail_ms=0.0, tail_launches=0):
     """Roofline of the dominant kernel.  `achieved` = the bytes THIS design must move per
     launch (pm_design_bytes: leaf words, compressed records written and read, compact
     finals, dirty-lane leaf words, 8 B per record -- counted from the run's record masks)
@@ -358,9 +362,10 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
     names = ("k_fitch_up", "k_down<Fitch>") if fitch else ("k_sankoff_up", "k_down<Sankoff>")
     # each timed class is a pass: every launch of these kernels (levels, narrow bands, wide
     # nodes, Sankoff parts, the tail of leaf-ish children) -- PMC bytes are summed per run
-    up_k = ("k_fitch_up", "k_fitch_up_wide", "k_fitch_up_band") if fitch else \
-        ("k_sankoff_up", "k_sankoff_up_wide", "k_sankoff_part", "k_sankoff_merge")
-    prof_names = {names[0]: up_k, names[1]: ("k_down", "k_down_band", "k_tail")}
+    up_k = ("k_fitch_up", "k_fitch_up_wide", "k_fitch_up_band", "k_fitch_up_mixed", "k_fitch_up_cluster") if fitch else \
+        ("k_sankoff_up", "k_sankoff_up_wide", "k_sankoff_part", "k_sankoff_merge", "k_sankoff_up_band", "k_sankoff_up_mixed")
+    down_k = ("k_down", "k_down_band", "k_down_cluster")
+    prof_names = {names[0]: up_k, names[1]: down_k + ("k_tail",)}
     key = "fitch" if fitch else "sankoff"
     classes = {
         names[0]: (ms[0] / steps, launches[0] / steps, design["up"]),
@@ -390,6 +395,37 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
         except (OSError, ValueError, KeyError):
             traffic_all = {}
     traffic = traffic_all[dom] / dl if traffic_all.get(dom) and dl else None   # per launch of the pass
+    # the pre-order pass by kernel: its levels / bands / sweeps (k_down*) and its tail launch,
+    # each kernel's design bytes (pm_design_bytes parts; the 8-B mutation records are written by
+    # both and counted apart) beside its PMC bytes, per step
+    parts = design.get("parts", {})
+    tail_design = parts.get("down_tail_items", 0.0) + parts.get("down_tail_leaf_words", 0.0)
+    levels_design = sum(parts.get(k, 0.0) for k in ("down_own_records", "down_parent_finals", "down_dirty_leaf_words",
+                                                       "down_finals_written"))
+    pmc_by_kernel = {}
+    if traffic_all:
+        try:
+            tj = json.load(open(args.traffic))
+            wk = f"{key}:{L}x{s_local}"
+            for kk in down_k + ("k_tail",):
+                v = tj.get(kk, {}).get(wk + ":step")
+                if v is not None and tj[kk].get(wk + ":build") == build:
+                    pmc_by_kernel[kk] = v
+        except (OSError, ValueError):
+            pmc_by_kernel = {}
+    lv_pmc = sum(pmc_by_kernel.get(k, 0.0) for k in down_k) if any(k in pmc_by_kernel for k in down_k) else None
+    tl_pmc = pmc_by_kernel.get("k_tail")
+    pre_split = {
+        "records_bytes_per_step": 8.0 * muts,
+        "records_note": "8-B mutation records: written by both kernels, not split",
+        "levels": {"kernels": " + ".join(down_k), "ms_per_step": round((ms[1] - tail_ms) / steps, 3),
+                   "launches_per_step": (launches[1] - tail_launches) / steps,
+                   "design_bytes_per_step": levels_design, "pmc_bytes_per_step": lv_pmc,
+                   "pmc_over_design": round(lv_pmc / levels_design, 3) if lv_pmc and levels_design else None},
+        "tail": {"kernels": "k_tail", "ms_per_step": round(tail_ms / steps, 3), "launches_per_step": tail_launches / steps,
+                 "design_bytes_per_step": tail_design, "pmc_bytes_per_step": tl_pmc,
+                 "pmc_over_design": round(tl_pmc / tail_design, 3) if tl_pmc and tail_design else None},
+    }
     if fitch:   # SURVEY.md §8d contract: 2-B sets through memory
         contract = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1)) + \
             s_local * (2.0 * n_int + 0.5 * n_int + 0.5 * (n_nodes - 1) + 0.5 * L) + 8.0 * muts
@@ -418,6 +454,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank):
         "kernel_ms_per_step": round(dms, 3),
         "other_kernels_ms_per_step": {k: round(v[0], 3) for k, v in classes.items() if k != dom},
         "score_kernel_ms_per_step": round(ms[2] / steps, 3),
+        "pre_order_by_kernel": pre_split,
         "step_design_bytes": step_design,
         "step_design_parts": {k: round(v / 1e9, 3) for k, v in design.get("parts", {}).items()},
         "step_design_parts_unit": "GB",

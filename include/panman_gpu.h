@@ -187,8 +187,9 @@ int pm_site_results(pm_ctx* ctx, int32_t* score, uint8_t* root_code);
  * host copy. */
 int pm_site_results_device(pm_ctx* ctx, void* score_device, void* root_code_device);
 /* Accumulated device milliseconds and launch counts per kernel class since the last
- * call; classes: 0 post-order, 1 pre-order + assignment, 2 score histogram, 3 replay,
- * 4 whole pm_run replayed from a hipGraph (PM_OPT_GRAPH). */
+ * call; classes: 0 post-order, 1 pre-order + assignment (levels, bands, sweeps), 2 score
+ * histogram, 3 replay, 4 whole pm_run replayed from a hipGraph (PM_OPT_GRAPH), 5 the
+ * pre-order's tail launch (children beyond the second, S2 / S3 subtrees). */
 int pm_kernel_times(pm_ctx* ctx, double* ms, int64_t* launches, int classes);
 
 /* ---- multi-GPU column shards ----------------------------------------- */
@@ -245,9 +246,12 @@ int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_s
  * child records read, own record + masks written), out[1] pre-order + assignment (own
  * record, parent final, dirty-lane leaf words, compact finals, 8 B per mutation record),
  * out[2] score histogram, out[3] floor = 0.5 B per leaf-site + 8 B per record, out[4] the
- * record count; with n >= 13, out[5..12] split them: post-order leaf words, child records read,
+ * record count; with n >= 14, out[5..13] split them: post-order leaf words, child records read,
  * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
- * words, finals written, tail items.  `n` >= 5.  Synchronises the ctx stream. */
+ * words of the nodes' first two children (k_down), finals written, tail items and their
+ * dirty-lane leaf words (k_tail).  With the LDS-staged sweeps (PM_OPT_CLUSTER) a child record
+ * read from an LDS slot, and a parent final likewise, is not counted.  `n` >= 5.
+ * Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
 /* FETCH_SIZE calibration for scattered reads: `lanes` threads each read 4 x 16 B, one 16-B
  * slot every `stride_bytes` (16 = a coalesced stream), and write 16 B coalesced; `reps`

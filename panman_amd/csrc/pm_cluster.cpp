@@ -220,3 +220,97 @@ int plan_clusters(const HostTree& ht, const std::vector<int32_t>& up_order_k, co
 }
 
 }  // namespace pm
+
+namespace pm {
+
+// The pre-order over the same clusters (k_down_cluster): per cluster its nodes in depth-first
+// pre-order (a node before its children, the child with the most in-cluster nodes last, so a
+// chain holds one final at a time), the pre-order descriptor of each (the subtree form's:
+// S2 / S3 children left to the tail launch) with pad0 = the LDS slot holding the parent's
+// final (-1: the parent is outside the cluster, its final in memory) and pad1 = the slot this
+// node's final goes to (-1: no child in the cluster).  A final occupies its slot from its
+// node's step to its last in-cluster child's.  False (no pre-order sweeps) when a cluster needs
+// more than kClFSlots slots.
+bool plan_cluster_down(const HostTree& ht, const std::vector<int32_t>& down_order_k, const std::vector<NodeDesc>& down_desc_k,
+                       const std::vector<int32_t>& child_enc_k, ClusterPlan& cl) {
+    cl.down_items.clear();
+    if (cl.wg_off.size() < 2 || cl.h0 != 0) return false;   // (every level swept: the pre-order runs the clusters only)
+    const int32_t I = (int32_t)ht.child_off.size() - 1;
+    std::vector<int32_t> pos(I, -1);
+    for (size_t k = 0; k < down_order_k.size(); ++k) pos[down_order_k[k]] = (int32_t)k;
+    cl.down_items.assign(cl.items.size(), NodeDesc{});
+    const int32_t W = (int32_t)cl.wg_off.size() - 1;
+    std::atomic<bool> ok{true};
+    const int tasks = std::min(W, 4 * host_threads());
+    host_parallel_for(tasks, [&](int t) {
+        std::vector<int32_t> size, step, seq, stack, kids, slot;
+        for (int32_t w = t; w < W && ok; w += tasks) {
+            const int32_t lo = cl.wg_off[w], hi = cl.wg_off[w + 1], n = hi - lo;
+            auto local = [&](int32_t x) {   // x's position in the cluster's post-order items, or -1
+                if (x < 0 || (x & kVirtualBit)) return -1;
+                const int32_t it = cl.item_of[x];
+                return it >= lo && it < hi ? it - lo : -1;
+            };
+            size.assign(n, 1);
+            for (int32_t j = 0; j < n; ++j) {   // (post-order: children first)
+                const int32_t d = cl.items[lo + j].node;
+                for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                    const int32_t c = local(child_enc_k[e]);
+                    if (c >= 0) size[j] += size[c];
+                }
+            }
+            seq.clear();
+            stack.assign(1, n - 1);   // the root: the last post-order item
+            while (!stack.empty()) {
+                const int32_t j = stack.back();
+                stack.pop_back();
+                seq.push_back(j);
+                const int32_t d = cl.items[lo + j].node;
+                kids.clear();
+                for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                    const int32_t c = local(child_enc_k[e]);
+                    if (c >= 0) kids.push_back(c);
+                }
+                std::sort(kids.begin(), kids.end(), [&](int32_t x, int32_t y) { return size[x] > size[y]; });
+                for (const int32_t c : kids) stack.push_back(c);   // (the largest pushed first: popped last)
+            }
+            step.assign(n, 0);
+            for (int32_t s = 0; s < n; ++s) step[seq[s]] = s;
+            // final slots: [step(d), the last in-cluster child's step]
+            slot.assign(n, -1);
+            int32_t busy_until[kClFSlots];
+            for (int q = 0; q < kClFSlots; ++q) busy_until[q] = -1;
+            for (int32_t s = 0; s < n; ++s) {
+                const int32_t j = seq[s];
+                const int32_t d = cl.items[lo + j].node;
+                int32_t last = -1;
+                for (int32_t e = ht.child_off[d]; e < ht.child_off[d + 1]; ++e) {
+                    const int32_t c = local(child_enc_k[e]);
+                    if (c >= 0) last = std::max(last, step[c]);
+                }
+                if (last < 0) continue;
+                int q = 0;
+                while (q < kClFSlots && busy_until[q] > s) ++q;
+                if (q == kClFSlots) {
+                    ok = false;
+                    return;
+                }
+                busy_until[q] = last;
+                slot[j] = q;
+            }
+            for (int32_t s = 0; s < n; ++s) {
+                const int32_t j = seq[s];
+                const int32_t d = cl.items[lo + j].node;
+                NodeDesc x = down_desc_k[pos[d]];
+                const int32_t pj = x.parent >= 0 ? local(x.parent) : -1;
+                x.pad0 = pj >= 0 ? slot[pj] : -1;
+                x.pad1 = slot[j];
+                cl.down_items[lo + s] = x;
+            }
+        }
+    });
+    if (!ok) cl.down_items.clear();
+    return ok;
+}
+
+}  // namespace pm

@@ -87,6 +87,7 @@ void free_tree(DevTree& t) {
     dev_free(t.tail_desc_k);
     dev_free(t.lvl);
     dev_free(t.cl_items);
+    dev_free(t.cl_down_items);
     dev_free(t.cl_wg_off);
     dev_free(t.cl_slot_of);
     dev_free(t.pslot_kc);
@@ -1124,6 +1125,9 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
             x.vl1[q] = nk > 1 ? keep_vl[1][q] : -1;
         }
     }
+    // the pre-order over the sweeps' clusters (every level swept only)
+    ht.cl.down = plan_cluster_down(ht, down_order_k, down_desc_k, child_enc_k, ht.cl);
+    phase_add("cluster.down", ht.cl.down ? 1.0 : 0.0);
     auto make_tail = [&](const std::vector<int32_t>& order, const std::vector<int32_t>& enc) {
         std::vector<TailDesc> tail;
         for (int32_t d : order)
@@ -1271,6 +1275,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         (e = up(&dt.tail_desc_k, tail_desc_k)) != hipSuccess ||
         (e = up(&dt.lvl, lvl)) != hipSuccess ||
         (e = up(&dt.cl_items, ht.cl.items)) != hipSuccess ||
+        (e = up(&dt.cl_down_items, ht.cl.down_items)) != hipSuccess ||
         (e = up(&dt.cl_wg_off, ht.cl.wg_off)) != hipSuccess ||
         (e = up(&dt.cl_slot_of, ht.cl.slot_of)) != hipSuccess ||
         (e = up(&dt.pslot_kc, pslot_kc)) != hipSuccess ||
@@ -1281,8 +1286,8 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
     }
     ht.cl.items.clear();   // (device only)
     ht.cl.items.shrink_to_fit();
-    ht.cl.slot_of.clear();
-    ht.cl.slot_of.shrink_to_fit();
+    ht.cl.down_items.clear();
+    ht.cl.down_items.shrink_to_fit();
     ht.cl.item_of.clear();
     ht.cl.item_of.shrink_to_fit();
     c->dt = dt;

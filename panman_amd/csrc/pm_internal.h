@@ -34,7 +34,7 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 #define PM_SHARDS 1024
 #endif
 constexpr int kShards = PM_SHARDS;
-constexpr int kClasses = 5;   // post-order, pre-order, score, replay, whole graph
+constexpr int kClasses = 6;   // post-order, pre-order levels, score, replay, whole graph, pre-order tail
 constexpr int kDegreeClasses = 4;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
                                   // complex, parent's simple, an S2 / S3 node's pushed dirty lanes,
@@ -134,6 +134,7 @@ struct DevTree {
     TailDesc* tail_desc_k = nullptr;  // tails of the leaf-parent form + every S2 / S3 node
     // LDS-staged post-order sweeps (ClusterPlan on the device)
     NodeDesc* cl_items = nullptr;
+    NodeDesc* cl_down_items = nullptr;
     int32_t* cl_wg_off = nullptr;
     int32_t* cl_slot_of = nullptr;
     // up slots with the sweeps (UpArgs::upm: the level items', then the sweep items' at
@@ -171,6 +172,10 @@ constexpr int32_t kClBandHeights = PM_CL_BAND;
 #endif
 constexpr int32_t kClChain = PM_CL_CHAIN;
 constexpr int32_t kClMaxLevel = PM_CL_MAX_LEVEL;
+#ifndef PM_CL_FSLOTS
+#define PM_CL_FSLOTS 8
+#endif
+constexpr int kClFSlots = PM_CL_FSLOTS;   // the pre-order sweeps' LDS final slots (1 KiB each)
 
 struct ClusterPlan {
     int32_t h0 = 0;                  // first post-order level (subtree form) the sweeps take
@@ -185,6 +190,11 @@ struct ClusterPlan {
     std::vector<int32_t> item_of;    // [I] a swept node's (first) item, -1
     int32_t n_items = 0;
     int32_t upm_base = 0;            // the items' up slots follow both up orders' (UpArgs::upm)
+    // the pre-order over the same clusters (plan_cluster_down; empty: the level kernels): per
+    // cluster its nodes in depth-first pre-order; pad0 = the slot of the parent's final, pad1
+    // = this node's (-1: none)
+    std::vector<NodeDesc> down_items;
+    bool down = false;
 };
 
 constexpr int32_t kVirtualBit = 1 << 30;
@@ -248,6 +258,8 @@ struct HostTree {
 int plan_clusters(const HostTree& ht, const std::vector<int32_t>& up_order_k, const std::vector<int32_t>& child_enc_k,
                   const std::vector<int32_t>& parent_dense, const std::vector<int32_t>& vleaf, int32_t max_level,
                   bool chain_check, ClusterPlan& out);
+bool plan_cluster_down(const HostTree& ht, const std::vector<int32_t>& down_order_k, const std::vector<NodeDesc>& down_desc_k,
+                       const std::vector<int32_t>& child_enc_k, ClusterPlan& cl);
 
 struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -327,7 +339,7 @@ struct pm_ctx {
     // profiling
     bool profiling = false;
     std::vector<pm::Timer> timers[pm::kClasses];
-    size_t timers_used[pm::kClasses] = {0, 0, 0, 0, 0};
+    size_t timers_used[pm::kClasses] = {0, 0, 0, 0, 0, 0};
 
     // hipGraph of one pm_run (PM_OPT_GRAPH): captured on first use, replayed while the
     // launch sequence and every buffer it touches stay the same (graph_key)

@@ -214,9 +214,16 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     const double cx_read_up = 64.0;                                // the parent reads Fitch planes / Z0
     double up = 0.0, down = 0.0;
     // components: up leaf words, up child records, up own records + pushes, down own records,
-    // down parent finals, down dirty leaf words, down finals written, down tail items
-    double part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // down parent finals, down dirty leaf words (a node's first two children: k_down), down
+    // finals written, down tail items (descriptor, parent masks and finals: k_tail), down tail
+    // items' dirty leaf words (k_tail)
+    double part[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
+    // LDS-staged sweeps: a node whose parent is in its cluster hands its set (post-order) and
+    // receives its parent's final (pre-order sweeps) through LDS
+    const bool clu = mode == PM_MODE_FITCH && sub && c->cluster && ht.cl.band_wg.size() > 1 && !ht.cl.slot_of.empty();
+    auto in_lds = [&](int32_t d) { return clu && ht.cl.slot_of[d] >= 0; };
+    const bool down_lds = clu && ht.cl.down && !c->sub_down;
     for (int32_t d = 0; d < I; ++d) {
         if (vnode[d]) continue;
         const int32_t e0 = ht.child_off[d], e1 = ht.child_off[d + 1];
@@ -234,11 +241,14 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             auto s_child = [&](int32_t e) { return sub && ht.child_enc[e] >= 0 && vnode[ht.child_enc[e]] > 2; };
             for (int32_t k = e0; k < e1; ++k) {
                 const int32_t ch = ht.child_enc[k];
+                // k_tail item (a leaf-ish child beyond the second, or an S2 / S3 child in the
+                // subtree form)
+                const bool tail = (k >= e0 + 2 && (ch < 0 || vnode[ch])) || (sub && ch >= 0 && vnode[ch] > 2);
                 if (ch < 0) {
                     up += word_row;
                     down += lane * dirty_leaf;
                     part[0] += word_row;
-                    part[5] += lane * dirty_leaf;
+                    part[tail ? 8 : 5] += lane * dirty_leaf;
                 } else if (vnode[ch]) {
                     const int32_t nl = vnode[ch];
                     // (Fitch, all present: the first two children's own masks, words 6 / 7)
@@ -248,17 +258,15 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                     up += word_row * nl;
                     down += lane * dv * nl;
                     part[0] += word_row * nl;
-                    part[5] += lane * dv * nl;
-                } else {
+                    part[tail ? 8 : 5] += lane * dv * nl;
+                } else if (!in_lds(ch)) {
                     const uint64_t* r = mk(ch, t);
                     const double b = 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
                     up += b;
                     part[1] += b;
                 }
-                // k_tail item (a leaf-ish child beyond the second, or an S2 / S3 child in the
-                // subtree form): descriptor + parent masks (64 B each), the parent's final on
-                // its dirty non-consensus lanes
-                const bool tail = (k >= e0 + 2 && (ch < 0 || vnode[ch])) || (sub && ch >= 0 && vnode[ch] > 2);
+                // a k_tail item: descriptor + parent masks (64 B each), the parent's final on its
+                // dirty non-consensus lanes
                 if (tail) {
                     const uint64_t dm = d == root ? ~0ull
                                         : ch >= 0 && vnode[ch] > 2 ? mk(ch, t)[5]
@@ -274,8 +282,9 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             if (d == root) {
                 down += 2.0 * word_row;   // forced / root final
             } else {
-                down += lane * popc(q[3] | q[4]) + lane * popc(q[0]);
-                part[4] += lane * popc(q[3] | q[4]);
+                const double pf = down_lds && in_lds(d) ? 0.0 : lane * popc(q[3] | q[4]);
+                down += pf + lane * popc(q[0]);
+                part[4] += pf;
                 part[6] += lane * popc(q[0]);
             }
         }
@@ -286,7 +295,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     out[2] = 8.0 * (double)records + 4.0 * (double)c->num_sites;   // score histogram
     out[3] = 0.5 * (double)L * (double)c->num_sites + 8.0 * (double)records;   // floor: leaf codes once + records
     out[4] = (double)records;
-    for (int k = 0; k < 8 && 5 + k < n; ++k) out[5 + k] = part[k];
+    for (int k = 0; k < 9 && 5 + k < n; ++k) out[5 + k] = part[k];
     return PM_OK;
 }
 

@@ -722,11 +722,11 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
         t.sbase = ht.sbase;
         t.sub_planes = c->sub_planes;
         const dim3 grid = wave_grid(t.count, tiles);
-        timer_begin(c, 1);
+        timer_begin(c, 5);
         if (sub) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true, true>), grid, dim3(kBlock), 0, c->stream, t);
         else if (c->leaves_all_present) hipLaunchKernelGGL((k_tail<Mode::kSankoff, true>), grid, dim3(kBlock), 0, c->stream, t);
         else hipLaunchKernelGGL((k_tail<Mode::kSankoff, false>), grid, dim3(kBlock), 0, c->stream, t);
-        timer_end(c, 1);
+        timer_end(c, 5);
     }
     return hipGetLastError();
 }

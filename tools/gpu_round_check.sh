@@ -5,7 +5,10 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 tag=$1
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_$tag.log 2>&1 \
+(while true; do date >> gpurun_out/heartbeat_$tag.txt; sleep 30; done) &
+hb=$!
+trap "kill $hb" EXIT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > gpurun_out/gputests_$tag.log 2>&1 \
   || { echo "GPU TESTS FAILED"; tail -60 gpurun_out/gputests_$tag.log; exit 1; }
 tail -2 gpurun_out/gputests_$tag.log
 timeout -k 10 900 python bench.py > gpurun_out/bench_default_$tag.json 2> gpurun_out/bench_default_$tag.err \
