@@ -362,6 +362,15 @@ int pm_replay_prepare(pm_ctx* ctx, const pm_panmat* panmat);
 int pm_replay_prepare_range(pm_ctx* ctx, const pm_panmat* panmat, int64_t leaf_begin, int64_t leaf_end);
 int pm_replay_run(pm_ctx* ctx);
 int pm_replay_format(pm_ctx* ctx, int aligned, char** text, int64_t* length);
+/* The same FASTA text written to the file descriptor `fd` (a pipe, stdout, a file) instead of
+ * returned: the device text streams through pinned slots to `fd` while later chunks are still
+ * in flight, with no host copy of the whole text.  `length` (nullable): the bytes written.
+ * pm_fasta_fd = pm_fasta to a descriptor; pm_fasta_multi_fd = pm_fasta_multi to a descriptor
+ * (the shards' texts in leaf order).  A failed write returns PM_ERR_ARG (errno kept). */
+int pm_replay_format_fd(pm_ctx* ctx, int aligned, int fd, int64_t* length);
+int pm_fasta_fd(pm_ctx* ctx, const pm_panmat* panmat, int aligned, int fd, int64_t* length);
+int pm_fasta_multi_fd(const pm_panmat* panmat, int aligned, const int* devices, int num_devices, int fd, int64_t* length,
+                      char* err, int64_t err_len);
 /* Canonical aligned columns per leaf of the prepared PanMAT (gap slots before each main
  * position, block sentinels included) and the number of leaves. */
 int pm_replay_shape(pm_ctx* ctx, int64_t* leaves, int64_t* columns, int64_t* edits);

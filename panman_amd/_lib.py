@@ -78,6 +78,10 @@ _SIGS = {
     "pm_replay_prepare": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pm_replay_run": (C.c_int, [C.c_void_p]),
     "pm_replay_format": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pm_replay_format_fd": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]),
+    "pm_fasta_fd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]),
+    "pm_fasta_multi_fd": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                    C.c_char_p, C.c_int64]),
     "pm_panman_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int64]),
     "pm_panman_load_old": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int64]),
     "pm_panman_tree_count": (C.c_int, [C.c_void_p]),

@@ -2,6 +2,8 @@
 // table, :1302-1325 PanMAN load, :1409-1465 MSA build, :271-299 writePanMAN, :385-415 and
 // :458-490 FASTA / aligned FASTA, :766-786 Newick).  Only the commands on the accelerated
 // path are implemented; any other reference command is rejected with a message.
+#include <fcntl.h>
+#include <unistd.h>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -430,20 +432,32 @@ int from_panman(const Options& o, const std::vector<int>& devices) {
         const auto f0 = Clock::now();
         for (int i = 0; i < trees && status == 0; ++i) {
             pm_panmat view;
-            char* text = nullptr;
             int64_t len = 0;
             char err[512] = {0};
-            if (pm_panman_tree(file, i, &view) != PM_OK ||
-                pm_fasta_multi(&view, aligned, devices.data(), (int)devices.size(), &text, &len, err, sizeof err) !=
-                    PM_OK) {
-                print_error(err[0] ? err : "FASTA extraction failed");
-                status = 1;
-                break;
+            // the text streams from the device(s) straight to stdout or the output file
+            // (pm_fasta_multi_fd): no host copy of the whole text, the write overlaps the download
+            int fd = 1;
+            if (to_file) {
+                const std::string p = "./info/" + o.get("output-file") + "_" + std::to_string(i) + (aligned ? ".msa" : ".fasta");
+                fd = ::open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+                if (fd < 0) {
+                    print_error("cannot write " + p);
+                    status = 1;
+                    break;
+                }
+            } else {
+                std::cout.flush();
+                std::fflush(stdout);
             }
             const auto w0 = Clock::now();
-            if (!sink(aligned ? ".msa" : ".fasta", i, text, (size_t)len)) status = 1;
-            pm_free(text);
-            cli_phase("cli.write_text", w0);
+            if (pm_panman_tree(file, i, &view) != PM_OK ||
+                pm_fasta_multi_fd(&view, aligned, devices.data(), (int)devices.size(), fd, &len, err, sizeof err) != PM_OK) {
+                print_error(err[0] ? err : "FASTA extraction failed");
+                status = 1;
+            }
+            if (to_file && ::close(fd) != 0) status = 1;
+            cli_phase("cli.fasta_stream", w0);
+            if (status) break;
         }
         std::cout << "\nFASTA execution time: " << ns_since(f0) << " nanoseconds\n";
     }

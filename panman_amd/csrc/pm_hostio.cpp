@@ -10,12 +10,14 @@
 // in parallel, so first-touch faults and the host copy are spread over the cores and
 // overlap the transfer.
 #include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -210,6 +212,58 @@ hipError_t d2h_large(pm_ctx* c, void* dst, const void* src, size_t n) {
     }
     if (e != hipSuccess) (void)hipStreamSynchronize(c->stream);
     return e;
+}
+
+// The same pinned slots, each chunk handed to `sink` (the caller's file descriptor) as soon as
+// it lands instead of copied into a host buffer: the device text streams to its destination
+// while the next chunks are in flight.  false from sink: stop (the write failed).
+hipError_t d2h_stream(pm_ctx* c, const void* src, size_t n, const std::function<bool(const char*, size_t)>& sink,
+                      bool& sink_ok) {
+    sink_ok = true;
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (!c->stage) {
+        if ((e = hipHostMalloc(&c->stage, kStageChunk * kStageSlots, hipHostMallocDefault)) != hipSuccess) {
+            c->stage = nullptr;
+            return e;
+        }
+        for (int s = 0; s < kStageSlots && e == hipSuccess; ++s)
+            e = hipEventCreateWithFlags(&c->stage_ev[s], hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    char* stage = static_cast<char*>(c->stage);
+    const char* from = static_cast<const char*>(src);
+    const int64_t K = (int64_t)((n + kStageChunk - 1) / kStageChunk);
+    auto len = [&](int64_t k) { return std::min(kStageChunk, n - (size_t)k * kStageChunk); };
+    auto issue = [&](int64_t k) {
+        const int s = (int)(k % kStageSlots);
+        hipError_t r = hipMemcpyAsync(stage + (size_t)s * kStageChunk, from + (size_t)k * kStageChunk, len(k),
+                                      hipMemcpyDeviceToHost, c->stream);
+        return r == hipSuccess ? hipEventRecord(c->stage_ev[s], c->stream) : r;
+    };
+    for (int64_t k = 0; k < std::min<int64_t>(K, kStageSlots) && e == hipSuccess; ++k) e = issue(k);
+    for (int64_t k = 0; k < K && e == hipSuccess; ++k) {
+        const int s = (int)(k % kStageSlots);
+        if ((e = hipEventSynchronize(c->stage_ev[s])) != hipSuccess) break;
+        if (sink_ok) sink_ok = sink(stage + (size_t)s * kStageChunk, len(k));
+        if (!sink_ok) break;
+        if (k + kStageSlots < K) e = issue(k + kStageSlots);
+    }
+    (void)hipStreamSynchronize(c->stream);   // (slots still in flight after a failed write)
+    return e;
+}
+
+bool write_all(int fd, const char* p, size_t n) {
+    while (n > 0) {
+        const ssize_t w = ::write(fd, p, n);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        p += w;
+        n -= (size_t)w;
+    }
+    return true;
 }
 
 void free_hostio(pm_ctx* c) {

@@ -431,6 +431,10 @@ void* host_alloc_large(size_t n);
 // dst (pageable host) <- src (device), n bytes, through pinned slots drained by host threads;
 // synchronous on the ctx stream
 hipError_t d2h_large(pm_ctx* c, void* dst, const void* src, size_t n);
+// (device) src, n bytes, through the same slots, each landed chunk handed to `sink` in order
+hipError_t d2h_stream(pm_ctx* c, const void* src, size_t n, const std::function<bool(const char*, size_t)>& sink,
+                      bool& sink_ok);
+bool write_all(int fd, const char* p, size_t n);   // write(2) until done; false on an error
 // *buf grown (contents dropped) to hold `need` bytes
 hipError_t grow_device(void** buf, size_t* cap, size_t need);
 void free_hostio(pm_ctx* c);

@@ -23,6 +23,7 @@
 //   Decoded by hand from the protobuf wire format (varint / 64-bit / length-delimited /
 //   32-bit records; repeated scalars packed or not), into the same PanmanTree as a .panman.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +32,7 @@
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "pm_internal.h"
@@ -95,7 +97,29 @@ namespace {
 constexpr int kLzmaOk = 0, kLzmaStreamEnd = 1, kLzmaFinish = 3, kLzmaCheckCrc64 = 4;
 constexpr uint32_t kLzmaConcatenated = 0x08;
 
-bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err);
+// Decoded messages: a byte vector whose resize leaves new bytes uninitialised (every byte is
+// written by the decoder; zero-filling a C5-sized message first cost a single-threaded pass).
+template <class T>
+struct DefaultInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInit<U>;
+    };
+    DefaultInit() = default;
+    template <class U>
+    DefaultInit(const DefaultInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, DefaultInit<uint8_t>>;
+
+bool xz_decode_serial(const std::vector<uint8_t>& in, Bytes& out, std::string& err);
 
 // ---- multi-block .xz in parallel --------------------------------------------------------
 // The writer (xz_encode) emits one stream of independent blocks; its index (at the end of the
@@ -169,7 +193,7 @@ bool xz_blocks(const std::vector<uint8_t>& in, std::vector<XzBlock>& blocks) {
     return off == idx_pos;   // one stream: the blocks end where the index starts
 }
 
-bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
+bool xz_decode(const std::vector<uint8_t>& in, Bytes& out, std::string& err) {
     std::vector<XzBlock> blocks;
     if (!xz_blocks(in, blocks)) return xz_decode_serial(in, out, err);
     try {
@@ -225,7 +249,7 @@ bool xz_decode(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::s
     return true;
 }
 
-bool xz_decode_serial(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, std::string& err) {
+bool xz_decode_serial(const std::vector<uint8_t>& in, Bytes& out, std::string& err) {
     pm_lzma_stream s{};
     if (lzma_stream_decoder(&s, UINT64_MAX, kLzmaConcatenated) != kLzmaOk) { err = "xz decoder init"; return false; }
     out.resize(std::max<size_t>(in.size() * 4, 1 << 20));
@@ -317,7 +341,7 @@ bool xz_encode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::stri
 
 // ---- Cap'n Proto reader ---------------------------------------------------------------
 struct Msg {
-    std::vector<uint8_t> bytes;
+    Bytes bytes;
     std::vector<const uint64_t*> seg;
     std::vector<size_t> len;
     std::string err;
@@ -514,16 +538,54 @@ bool load_tree(Msg& m, const Struct& t, PanmanTree& out) {
         out.names_blob.push_back('\0');
         index[topo.name[i]] = i;
     }
-    // nodes: assignMutationsToNodes walks the tree in pre-order (src/panman.cpp:576-618)
+    // nodes: assignMutationsToNodes walks the tree in pre-order (src/panman.cpp:576-618).  Two
+    // passes over node ranges on host threads: each node's mutation counts, then -- at offsets
+    // from their prefix sums -- the flattened mutations (the message is only read: no state)
     List nodes;
     if (!child_list(m, t, 1, nodes)) return false;
     out.bm_off.assign(N + 1, 0);
     out.nm_off.assign(N + 1, 0);
-    for (int32_t v = 0; v < N; ++v) {
-        if ((uint32_t)v < nodes.count) {
+    const int32_t NV = std::min<int32_t>(N, (int32_t)std::min<uint32_t>(nodes.count, (uint32_t)INT32_MAX));
+    const int32_t chunk = 4096, tasks = (NV + chunk - 1) / chunk;
+    std::atomic<bool> bad{false};
+    host_parallel_for(tasks, [&](int task) {
+        for (int32_t v = task * chunk; v < std::min(NV, (task + 1) * chunk) && !bad; ++v) {
             const Struct node = nodes.at((uint32_t)v);
             List muts;
-            if (!child_list(m, node, 0, muts)) return false;
+            if (!child_list(m, node, 0, muts)) { bad = true; return; }
+            int64_t nn = 0, nb = 0;
+            for (uint32_t k = 0; k < muts.count; ++k) {
+                const Struct mu = muts.at(k);
+                List nucs;
+                if (!child_list(m, mu, 0, nucs)) { bad = true; return; }
+                nn += nucs.count;
+                nb += mu.flag(65) ? 1 : 0;
+            }
+            out.nm_off[v + 1] = nn;
+            out.bm_off[v + 1] = nb;
+        }
+    });
+    if (bad) return false;
+    for (int32_t v = 0; v < N; ++v) {
+        out.nm_off[v + 1] += out.nm_off[v];
+        out.bm_off[v + 1] += out.bm_off[v];
+    }
+    const size_t NM = (size_t)out.nm_off[N], BM = (size_t)out.bm_off[N];
+    out.nm_primary.resize(NM);
+    out.nm_secondary.resize(NM);
+    out.nm_pos.resize(NM);
+    out.nm_gap.resize(NM);
+    out.nm_info.resize(NM);
+    out.nm_nucs.resize(NM);
+    out.bm_primary.resize(BM);
+    out.bm_info.resize(BM);
+    out.bm_inv.resize(BM);
+    host_parallel_for(tasks, [&](int task) {
+        for (int32_t v = task * chunk; v < std::min(NV, (task + 1) * chunk); ++v) {
+            const Struct node = nodes.at((uint32_t)v);
+            List muts;
+            (void)child_list(m, node, 0, muts);
+            size_t a = (size_t)out.nm_off[v], bi = (size_t)out.bm_off[v];
             for (uint32_t k = 0; k < muts.count; ++k) {
                 const Struct mu = muts.at(k);
                 const int64_t block_id = mu.i64(0);
@@ -531,28 +593,27 @@ bool load_tree(Msg& m, const Struct& t, PanmanTree& out) {
                 const int32_t primary = (int32_t)(block_id >> 32);
                 const int32_t secondary = gap_exist ? (int32_t)(block_id & 0xFFFFFFFF) : -1;
                 List nucs;
-                if (!child_list(m, mu, 0, nucs)) return false;
-                for (uint32_t j = 0; j < nucs.count; ++j) {
+                (void)child_list(m, mu, 0, nucs);
+                for (uint32_t j = 0; j < nucs.count; ++j, ++a) {
                     const Struct nm = nucs.at(j);
                     const uint32_t info = nm.u32(96);
                     const uint32_t len = (info & 0xFF) >> 4;
-                    out.nm_primary.push_back(primary);
-                    out.nm_secondary.push_back(secondary);
-                    out.nm_pos.push_back(nm.i32(0));
-                    out.nm_gap.push_back(nm.flag(64) ? nm.i32(32) : -1);
-                    out.nm_info.push_back((uint8_t)(info & 0xFF));
-                    out.nm_nucs.push_back(len <= 6 ? (info >> 8) << (24 - 4 * len) : 0);
+                    out.nm_primary[a] = primary;
+                    out.nm_secondary[a] = secondary;
+                    out.nm_pos[a] = nm.i32(0);
+                    out.nm_gap[a] = nm.flag(64) ? nm.i32(32) : -1;
+                    out.nm_info[a] = (uint8_t)(info & 0xFF);
+                    out.nm_nucs[a] = len <= 6 ? (info >> 8) << (24 - 4 * len) : 0;
                 }
                 if (mu.flag(65)) {   // blockMutExist
-                    out.bm_primary.push_back(primary);
-                    out.bm_info.push_back(mu.flag(66));
-                    out.bm_inv.push_back(mu.flag(67));
+                    out.bm_primary[bi] = primary;
+                    out.bm_info[bi] = mu.flag(66);
+                    out.bm_inv[bi] = mu.flag(67);
+                    ++bi;
                 }
             }
         }
-        out.bm_off[v + 1] = (int64_t)out.bm_primary.size();
-        out.nm_off[v + 1] = (int64_t)out.nm_primary.size();
-    }
+    });
     // blocks in (primary, secondary) order (std::map, src/panman.cpp:1668-1724)
     std::map<std::pair<int32_t, int32_t>, std::vector<uint32_t>> blocks;
     List cmap;
@@ -1074,7 +1135,7 @@ int pm_panman_load(const char* path, pm_panman** out, char* err, int64_t err_len
     if (is_xz) {
         if (!xz_decode(raw, m.bytes, e)) { set_err(e); return PM_ERR_ARG; }
     } else {
-        m.bytes.swap(raw);   // an uncompressed capnp message is accepted too
+        m.bytes.assign(raw.begin(), raw.end());   // an uncompressed capnp message is accepted too
     }
     clock.lap("panman.xz_decode");
     if (!m.init()) { set_err(m.err); return PM_ERR_ARG; }
@@ -1103,7 +1164,8 @@ int pm_panman_load_old(const char* path, pm_panman** out, char* err, int64_t err
     *out = nullptr;
     FILE* f = std::fopen(path, "rb");
     if (!f) { set_err(std::string("cannot open ") + path); return PM_ERR_ARG; }
-    std::vector<uint8_t> raw, bytes;
+    std::vector<uint8_t> raw;
+    Bytes bytes;
     uint8_t buf[1 << 16];
     size_t n;
     while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
@@ -1113,7 +1175,7 @@ int pm_panman_load_old(const char* path, pm_panman** out, char* err, int64_t err
     if (is_xz) {
         if (!xz_decode(raw, bytes, e)) { set_err(e); return PM_ERR_ARG; }
     } else {
-        bytes.swap(raw);   // an uncompressed message is accepted too
+        bytes.assign(raw.begin(), raw.end());   // an uncompressed message is accepted too
     }
     // treeGroup: trees (1), complexMutations (2: not on this path, as in pm_panman_load)
     std::vector<std::pair<const uint8_t*, const uint8_t*>> trees;

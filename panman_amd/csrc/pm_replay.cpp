@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cerrno>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -631,51 +632,13 @@ void free_replay(pm_ctx* c) {
 
 }  // namespace pm
 
-using namespace pm;
-
-extern "C" {
-
-int pm_replay_prepare_range(pm_ctx* c, const pm_panmat* p, int64_t leaf_begin, int64_t leaf_end) {
-    if (!c || !p) return PM_ERR_ARG;
-    (void)hipSetDevice(c->device);
-    free_replay(c);
-    c->replay = new ReplayState();
-    int rc = replay_prepare(c, p, *c->replay, leaf_begin, leaf_end);
-    if (rc != PM_OK) free_replay(c);
-    return rc;
-}
-
-int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) { return pm_replay_prepare_range(c, p, -1, -1); }
-
-int pm_replay_run(pm_ctx* c) {
+namespace pm {
+// The FASTA text of the replayed rows in the context's device text buffer (c->text_buf),
+// `total` bytes; `clock` carries on into the caller's download phase.
+int format_device(pm_ctx* c, int aligned, int64_t& total, PhaseClock& clock) {
     if (!c) return PM_ERR_ARG;
-    if (!c->replay) return fail(c, PM_ERR_STATE, "prepare a PanMAT first");
-    (void)hipSetDevice(c->device);
-    hipError_t e = launch_replay(c, c->replay->dev);
-    if (e != hipSuccess) return hip_fail(c, e, "replay launch");
-    c->replay->ran = true;
-    return PM_OK;
-}
-
-int pm_replay_shape(pm_ctx* c, int64_t* leaves, int64_t* columns, int64_t* edits) {
-    if (!c || !c->replay) return PM_ERR_ARG;
-    if (leaves) *leaves = (int64_t)c->replay->leaves.size();
-    if (columns) *columns = c->replay->columns;
-    if (edits) *edits = c->replay->edits;
-    return PM_OK;
-}
-
-// printFASTAUltraFast's output stage (src/fasta.cpp:1944-1975, 2089-2094) and
-// printSequenceLinesNew (:155-254) on the device: per leaf the blocks in print order
-// (rotation to the rotationIndexes-th existing block, reversal when inverted), forward or
-// reverse-complemented, '-' dropped when unaligned, absent blocks as blockLengths dashes
-// (indexed by print position, as the reference does), the line rotated by the circular
-// offset (unaligned only) and wrapped at 70 columns.  Host work: segment table, scans.
-int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
-    if (!c || !text || !length) return PM_ERR_ARG;
     if (!c->replay || !c->replay->ran) return fail(c, PM_ERR_STATE, "run the replay first");
     (void)hipSetDevice(c->device);
-    PhaseClock clock;
     const ReplayState& r = *c->replay;
     const int32_t L = (int32_t)r.leaves.size();
     const int32_t M = r.max_id + 1;
@@ -758,7 +721,7 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
         const int64_t hdr = name_off[li + 1] - name_off[li] + 2;
         text_off[li + 1] = text_off[li] + hdr + p + p / 70 + 1;
     }
-    const int64_t total = text_off[L];
+    total = text_off[L];
     clock.lap("fasta.count");
     if ((e = dput(&d_off, off, c->stream)) != hipSuccess || (e = dput(&d_line, line, c->stream)) != hipSuccess ||
         (e = dput(&d_start, start, c->stream)) != hipSuccess || (e = dput(&d_text_off, text_off, c->stream)) != hipSuccess ||
@@ -779,14 +742,63 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     e = launch_fmt_write(c, f, L);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     clock.lap("fasta.text_kernel");
-    char* out = e == hipSuccess ? static_cast<char*>(host_alloc_large((size_t)total + 1)) : nullptr;
-    if (e == hipSuccess && !out) {
-        cleanup();
-        return fail(c, PM_ERR_OOM, "FASTA text");
-    }
-    // the text through pinned slots drained by host threads (pm_hostio.cpp), not one pageable copy
-    if (e == hipSuccess) e = d2h_large(c, out, d_text, (size_t)total);
     cleanup();
+    if (e != hipSuccess) return hip_fail(c, e, "FASTA text kernel");
+    return PM_OK;
+}
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+int pm_replay_prepare_range(pm_ctx* c, const pm_panmat* p, int64_t leaf_begin, int64_t leaf_end) {
+    if (!c || !p) return PM_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    free_replay(c);
+    c->replay = new ReplayState();
+    int rc = replay_prepare(c, p, *c->replay, leaf_begin, leaf_end);
+    if (rc != PM_OK) free_replay(c);
+    return rc;
+}
+
+int pm_replay_prepare(pm_ctx* c, const pm_panmat* p) { return pm_replay_prepare_range(c, p, -1, -1); }
+
+int pm_replay_run(pm_ctx* c) {
+    if (!c) return PM_ERR_ARG;
+    if (!c->replay) return fail(c, PM_ERR_STATE, "prepare a PanMAT first");
+    (void)hipSetDevice(c->device);
+    hipError_t e = launch_replay(c, c->replay->dev);
+    if (e != hipSuccess) return hip_fail(c, e, "replay launch");
+    c->replay->ran = true;
+    return PM_OK;
+}
+
+int pm_replay_shape(pm_ctx* c, int64_t* leaves, int64_t* columns, int64_t* edits) {
+    if (!c || !c->replay) return PM_ERR_ARG;
+    if (leaves) *leaves = (int64_t)c->replay->leaves.size();
+    if (columns) *columns = c->replay->columns;
+    if (edits) *edits = c->replay->edits;
+    return PM_OK;
+}
+
+// printFASTAUltraFast's output stage (src/fasta.cpp:1944-1975, 2089-2094) and
+// printSequenceLinesNew (:155-254) on the device: per leaf the blocks in print order
+// (rotation to the rotationIndexes-th existing block, reversal when inverted), forward or
+// reverse-complemented, '-' dropped when unaligned, absent blocks as blockLengths dashes
+// (indexed by print position, as the reference does), the line rotated by the circular
+// offset (unaligned only) and wrapped at 70 columns.  Host work: segment table, scans.
+
+int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
+    if (!c || !text || !length) return PM_ERR_ARG;
+    PhaseClock clock;
+    int64_t total = 0;
+    int rc = format_device(c, aligned, total, clock);
+    if (rc != PM_OK) return rc;
+    char* out = static_cast<char*>(host_alloc_large((size_t)total + 1));
+    if (!out) return fail(c, PM_ERR_OOM, "FASTA text");
+    // the text through pinned slots drained by host threads (pm_hostio.cpp), not one pageable copy
+    const hipError_t e = d2h_large(c, out, c->text_buf, (size_t)total);
     if (e != hipSuccess) {
         std::free(out);
         return hip_fail(c, e, "FASTA write");
@@ -798,7 +810,25 @@ int pm_replay_format(pm_ctx* c, int aligned, char** text, int64_t* length) {
     return PM_OK;
 }
 
-int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* length) {
+int pm_replay_format_fd(pm_ctx* c, int aligned, int fd, int64_t* length) {
+    if (!c || fd < 0) return PM_ERR_ARG;
+    PhaseClock clock;
+    int64_t total = 0;
+    int rc = format_device(c, aligned, total, clock);
+    if (rc != PM_OK) return rc;
+    bool wrote = true;
+    const hipError_t e = d2h_stream(c, c->text_buf, (size_t)total,
+                                    [fd](const char* p, size_t n) { return write_all(fd, p, n); }, wrote);
+    if (e != hipSuccess) return hip_fail(c, e, "FASTA download");
+    if (!wrote) return fail(c, PM_ERR_ARG, "FASTA write: " + std::string(std::strerror(errno)));
+    clock.lap("fasta.download_write");
+    if (length) *length = total;
+    return PM_OK;
+}
+
+namespace {
+// prepare + replay (+ the depth-first kernel's rebuild count in the phase log)
+int fasta_replay(pm_ctx* c, const pm_panmat* p) {
     int rc = pm_replay_prepare(c, p);
     if (rc == PM_OK) {
         PhaseClock clock;
@@ -812,6 +842,18 @@ int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* l
             phase_add("replay.dfs_rebuilds", (double)rebuilds);
         }
     }
+    return rc;
+}
+}  // namespace
+
+int pm_fasta_fd(pm_ctx* c, const pm_panmat* p, int aligned, int fd, int64_t* length) {
+    int rc = fasta_replay(c, p);
+    if (rc == PM_OK) rc = pm_replay_format_fd(c, aligned, fd, length);
+    return rc;
+}
+
+int pm_fasta(pm_ctx* c, const pm_panmat* p, int aligned, char** text, int64_t* length) {
+    int rc = fasta_replay(c, p);
     if (rc == PM_OK) rc = pm_replay_format(c, aligned, text, length);
     return rc;
 }
@@ -894,6 +936,75 @@ int pm_fasta_multi(const pm_panmat* p, int aligned, const int* devices, int num_
     *text = out;
     *length = total;
     return PM_OK;
+}
+
+
+// pm_fasta_multi straight to a file descriptor: the shards are replayed and formatted on their
+// devices side by side, then each shard's text streams from its device to `fd` in leaf order
+// (the single-device text, byte for byte).
+int pm_fasta_multi_fd(const pm_panmat* p, int aligned, const int* devices, int num_devices, int fd, int64_t* length,
+                      char* err, int64_t err_len) {
+    auto set_err = [&](const std::string& e) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+    };
+    if (!p || !devices || num_devices < 1 || fd < 0 || p->num_nodes < 1 || !p->child_offsets) {
+        set_err("bad arguments");
+        return PM_ERR_ARG;
+    }
+    int64_t L = 0;
+    for (int32_t i = 0; i < p->num_nodes; ++i) L += p->child_offsets[i] == p->child_offsets[i + 1];
+    const int G = num_devices;
+    std::vector<pm_ctx*> ctx(G, nullptr);
+    std::vector<int64_t> plen(G, 0);
+    std::vector<int> rc(G, PM_OK);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g]() {
+            const int64_t lo = L * g / G, hi = L * (g + 1) / G;
+            if (hi == lo) return;   // more devices than leaves
+            if ((rc[g] = pm_create(devices[g], &ctx[g])) != PM_OK) {
+                msg[g] = "no HIP device " + std::to_string(devices[g]);
+                ctx[g] = nullptr;
+                return;
+            }
+            pm_ctx* c = ctx[g];
+            rc[g] = G == 1 ? fasta_replay(c, p) : pm_replay_prepare_range(c, p, lo, hi);
+            if (rc[g] == PM_OK && G > 1) rc[g] = pm_replay_run(c);
+            if (rc[g] == PM_OK) {
+                PhaseClock clock;
+                rc[g] = format_device(c, aligned, plen[g], clock);
+            }
+            if (rc[g] != PM_OK) msg[g] = pm_last_error(c);
+        });
+    for (auto& t : th) t.join();
+    int status = PM_OK;
+    for (int g = 0; g < G && status == PM_OK; ++g)
+        if (rc[g] != PM_OK) {
+            set_err(msg[g]);
+            status = rc[g];
+        }
+    int64_t total = 0;
+    PhaseClock clock;
+    for (int g = 0; g < G && status == PM_OK; ++g) {
+        if (!ctx[g] || plen[g] == 0) continue;
+        bool wrote = true;
+        const hipError_t e = d2h_stream(ctx[g], ctx[g]->text_buf, (size_t)plen[g],
+                                        [fd](const char* q, size_t n) { return write_all(fd, q, n); }, wrote);
+        if (e != hipSuccess) {
+            set_err(std::string("FASTA download: ") + hipGetErrorString(e));
+            status = PM_ERR_HIP;
+        } else if (!wrote) {
+            set_err(std::string("FASTA write: ") + std::strerror(errno));
+            status = PM_ERR_ARG;
+        }
+        total += plen[g];
+    }
+    clock.lap("fasta.download_write");
+    for (pm_ctx* c : ctx)
+        if (c) pm_destroy(c);
+    if (length) *length = total;
+    return status;
 }
 
 }  // extern "C"

@@ -168,3 +168,45 @@ def test_msa_build_multi_device_matches_single(tmp_path, mode):
     panman_amd.msa_to_panman(nwk, msa, one, ref, mode)
     panman_amd.msa_to_panman(nwk, msa, many, ref, mode, devices=[0, 0, 0])
     assert open(one, "rb").read() == open(many, "rb").read()
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_fasta_fd_streams_the_same_text(engine, tmp_path, aligned):
+    """pm_fasta_fd / pm_fasta_multi_fd (the CLI's path: the device text streamed through the
+    pinned slots to a descriptor) write pm_fasta's text byte for byte -- to a file, and through
+    a pipe read concurrently (more than one 64 MiB slot: a multi-chunk stream) -- and fail on a
+    descriptor that cannot be written."""
+    import os
+    import threading
+    from panman_amd.synth import c5_panmat
+    pm = c5_panmat(leaves=37, blocks=12, mean_len=900, seed=5)
+    want = engine.fasta(pm, aligned).encode()
+    path = tmp_path / "out.fa"
+    with open(path, "wb") as f:
+        n = engine.fasta_fd(pm, aligned, f.fileno())
+    assert n == len(want) and path.read_bytes() == want
+    for devices in ([0], [0, 0, 0], [0] * 50):
+        with open(path, "wb") as f:
+            assert panman_amd.engine.fasta_multi_fd(pm, aligned, devices, f.fileno()) == len(want)
+        assert path.read_bytes() == want, devices
+    big = c5_panmat(leaves=60, blocks=120, mean_len=12_000, seed=9)   # ~90 MB of aligned text
+    want_big = engine.fasta(big, True).encode()
+    assert len(want_big) > (64 << 20)
+    r, w = os.pipe()
+    got = []
+    reader = threading.Thread(target=lambda: got.append(b"".join(iter(lambda: os.read(r, 1 << 20), b""))))
+    reader.start()
+    try:
+        n = engine.fasta_fd(big, True, w)
+    finally:
+        os.close(w)
+        reader.join()
+        os.close(r)
+    assert n == len(want_big) and got[0] == want_big
+    rd, wr = os.pipe()
+    os.close(rd)   # a pipe without a reader: EPIPE (SIGPIPE is ignored by Python)
+    try:
+        with pytest.raises(panman_amd.PanmanError):
+            engine.fasta_fd(pm, aligned, wr)
+    finally:
+        os.close(wr)
