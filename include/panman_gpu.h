@@ -405,7 +405,12 @@ int pm_panman_write(const char* path, const pm_panmat* const* trees, int count, 
  * with the root forced to the leaf's states.  The result is a new one-tree pm_panman (in
  * the pre-order of the new topology; release with pm_panman_free).  Replaces the ctx's
  * tree, columns and replay state.  Within a node, block mutations are ordered by block
- * id (the reference's order is TBB-scheduled). */
+ * id (the reference's order is TBB-scheduled).  A PanMAT with secondary blocks (a nucleotide
+ * mutation with secondaryBlockId != -1) returns PM_ERR_UNSUPPORTED ("secondary blocks"):
+ * the reference rebuilds the secondary blocks' own sequences and block states
+ * (src/reroot.cpp:55-89, src/panman.cpp:4722-4890), a second block level this layout does
+ * not hold -- although pm_fasta, like printFASTAUltraFastHelper, replays such a PanMAT (the
+ * mutation lands on the primary block). */
 int pm_reroot(pm_ctx* ctx, const pm_panmat* tree, const char* leaf, pm_panman** out);
 
 /* Drop-in for Tree(pangraph.json, newick, FILE_TYPE::PANGRAPH, reference) (src/panman.cpp:

@@ -65,6 +65,19 @@ def test_secondary_block_mutation_lands_on_primary(engine, oracle, seed):
         assert _records(engine.fasta(pm, aligned)) == _records(oracle.fasta(pm, aligned))
 
 
+def test_reroot_refuses_secondary_blocks(engine):
+    """The same PanMAT replays (above) but reroot refuses it with PM_ERR_UNSUPPORTED and says
+    why: the reference rebuilds secondary blocks' sequences and states (src/reroot.cpp:55-89),
+    which this layout does not hold (include/panman_gpu.h, pm_reroot)."""
+    rng = np.random.default_rng(11)
+    off, idx, root = random_tree(12, rng, max_children=3)
+    pm = random_panmat(rng, off, idx, root, names_for(off), blocks=2, options=False)
+    leaves = pm.leaves()
+    pm.add_nuc_mut(leaves[0], 0, 1, -1, 0, [2], secondary=1)
+    with pytest.raises(panman_amd.PanmanError, match="secondary blocks"):
+        engine.reroot(pm, pm.names[leaves[1]])
+
+
 def test_long_blocks_wrap_vs_oracle(engine, oracle):
     rng = np.random.default_rng(5)
     off, idx, root = random_tree(30, rng, max_children=3)
