@@ -81,19 +81,19 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         cw = a.cons[word];
         // the accumulators start as the first child's set (no all-ones / zero planes live
         // beside the loads in flight)
-        if constexpr (PLAIN) child_set_plain(d.c0, vl0, f0, both, vd0);
-        else child_set_ap<SS>(d.c0, vl0, f0, both, vd0);
+        if constexpr (PLAIN) child_set_plain<kCxCompact>(d.c0, vl0, f0, both, vd0);
+        else child_set_ap<SS, kCxCompact>(d.c0, vl0, f0, both, vd0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) either[v] = both[v];
         if constexpr (PLAIN) {
             if (e1 - e0 > 1) {
                 uint32_t y[16];
-                child_set_plain(d.c1, vl1, f1, y, vd1);
+                child_set_plain<kCxCompact>(d.c1, vl1, f1, y, vd1);
 #pragma unroll
                 for (int v = 0; v < 16; ++v) { either[v] = both[v] | y[v]; both[v] &= y[v]; }
             }
         } else if (e1 - e0 > 1) {
-            fold_child_ap<SS>(d.c1, vl1, f1, both, either, vd1);
+            fold_child_ap<SS, kCxCompact>(d.c1, vl1, f1, both, either, vd1);
         }
         vd = vd0 | vd1;
         split = true;
@@ -110,7 +110,7 @@ __device__ __forceinline__ void fitch_up_node(const UpArgs& a, const NodeDesc& d
         if constexpr (LEAFY) {
             ChildFetch f;
             fetch_child_ap<kFitchRec, true>(a, c, vl, tile, lane, word, f);
-            fold_child_ap(c, vl, f, both, either, vd);
+            fold_child_ap<false, kCxCompact>(c, vl, f, both, either, vd);
         } else {
             fold_child<AP>(a, c, vl, tile, lane, word, both, either, vd);
         }
@@ -173,6 +173,8 @@ __global__ __launch_bounds__(kBlock, PLAIN ? PM_PLAIN_UP_WAVES : GROUP ? PM_GROU
 struct UpFetch {
     uint32_t w[16];
     bool complex_lane;
+    const uint4* p;   // compact records: A in w[0..3], B in w[5..8]; p / mx for cx_decode
+    uint64_t mx;
 };
 
 template <bool AP>
@@ -195,7 +197,13 @@ __device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, in
         const RecMask mk = rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * kFitchRec;
         f.complex_lane = (mk.x >> lane) & 1ull;
-        if (f.complex_lane) {
+        if constexpr (kCxCompact) {
+            const uint4 A = rec_code_all<true>(p, mk, lane, a.cons, word), B = cx_b_load(p, mk, lane, a.cons);
+            f.w[0] = A.x; f.w[1] = A.y; f.w[2] = A.z; f.w[3] = A.w;
+            f.w[5] = B.x; f.w[6] = B.y; f.w[7] = B.z; f.w[8] = B.w;
+            f.p = p;
+            f.mx = mk.x;
+        } else if (f.complex_lane) {
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -211,7 +219,11 @@ __device__ __forceinline__ void up_fetch(const UpArgs& a, int32_t c, int4 vl, in
 
 __device__ __forceinline__ void up_fold(int32_t c, const UpFetch& f, uint32_t* both, uint32_t* either, uint32_t& vd) {
     uint32_t x[16];
-    if (c >= 0 && !(c & kVirtualBit) && f.complex_lane) {
+    if (kCxCompact && c >= 0 && !(c & kVirtualBit)) {
+        onehot_from_code(f.w[0], f.w[1], f.w[2], f.w[3], ~0u, x);
+        cx_decode(x, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]), make_uint4(f.w[5], f.w[6], f.w[7], f.w[8]), f.complex_lane,
+                  f.p, f.mx);
+    } else if (c >= 0 && !(c & kVirtualBit) && f.complex_lane) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) x[v] = f.w[v];
     } else {
@@ -267,8 +279,8 @@ __device__ __forceinline__ void wide_fold(const UpArgs& a, int32_t e0, int32_t e
                 fetch_child_ap_m(a, c0, v0, readlane64(cmx, k), readlane64(cms, k), tile, lane, word, f0);
                 if (two) fetch_child_ap_m(a, c1, v1, readlane64(cmx, k + 1), readlane64(cms, k + 1), tile, lane, word, f1);
                 __builtin_amdgcn_sched_barrier(0);
-                fold_child_ap(c0, v0, f0, both, either, vd);
-                if (two) fold_child_ap(c1, v1, f1, both, either, vd);
+                fold_child_ap<false, kCxCompact>(c0, v0, f0, both, either, vd);
+                if (two) fold_child_ap<false, kCxCompact>(c1, v1, f1, both, either, vd);
             } else {
                 UpFetch f0, f1;
                 up_fetch<AP>(a, c0, v0, tile, lane, word, f0);
@@ -481,7 +493,9 @@ __device__ __forceinline__ void cl_fetch1(const UpArgs& a, int32_t ch, int4 vl, 
         if (l1 >= 0) x = a.leaf_planes[(size_t)l1 * a.wpad + word];
     } else {
         const size_t rec = (size_t)ch * a.tiles + tile;
-        cd = rec_code_all(a.sets + rec * kFitchRec, RecMask{mx, ms, 0, 0, 0}, lane, a.cons, word);
+        const RecMask m{mx, ms, 0, 0, 0};
+        cd = rec_code_all<kCxCompact>(a.sets + rec * kFitchRec, m, lane, a.cons, word);
+        if constexpr (kCxCompact) x = cx_b_load(a.sets + rec * kFitchRec, m, lane, a.cons);
     }
 }
 
@@ -507,6 +521,8 @@ __device__ __forceinline__ void cl_set1(const UpArgs& a, int32_t ch, int4 vl, ui
 #pragma unroll
             for (int v = 0; v < 16; ++v) out[v] |= u.lo[v & 3] & u.hi[v >> 2];
         }
+    } else if (kCxCompact && ch >= 0) {   // a record (x: its B word)
+        cx_decode(out, cd, x, (mx >> lane) & 1ull, a.sets + ((size_t)ch * a.tiles + tile) * kFitchRec, mx);
     } else if (ch >= 0 && mx != 0 && ((mx >> lane) & 1ull)) {   // a record's complex lane
         const uint4* p = a.sets + ((size_t)ch * a.tiles + tile) * kFitchRec + kWave + lanes_below(mx);
 #pragma unroll
@@ -753,7 +769,7 @@ __device__ __forceinline__ void cld_mask_get(uint32_t v, ClDownMeta& x) {
 // A step's loads issued one step ahead: its record's code word, the cluster root's parent final,
 // its first two children's leaf words at their dirty lanes.
 struct ClDownFetch {
-    uint4 code, pf;
+    uint4 code, pf, cxb;   // (cxb: compact records' B word)
     Kid k0, k1;
 };
 
@@ -762,7 +778,8 @@ __device__ __forceinline__ void cld_issue(const DownArgs& a, const ClDownMeta& x
     const NodeDesc& d = x.d;
     const bool is_root = d.parent < 0;
     const uint4* p = a.sets + ((size_t)d.node * a.tiles + tile) * kFitchRec;
-    f.code = rec_code_all(p, x.m, lane, a.cons, word);
+    f.code = rec_code_all<kCxCompact>(p, x.m, lane, a.cons, word);
+    if constexpr (kCxCompact) f.cxb = cx_b_load(p, x.m, lane, a.cons);
     if (d.pad0 < 0) f.pf = is_root ? a.cons[word] : parent_final<kFitchRec>(a, d.parent, x.m, tile, lane, word);
     // every leaf present: a leaf child differs from the final only at the complex lanes, a
     // virtual one there and where its own leaves disagree (mask words 6, 7; see down_node)
@@ -781,7 +798,9 @@ __device__ __forceinline__ void cld_step(const DownArgs& a, const ClDownMeta& x,
     uint4* const p = a.sets + ((size_t)d.node * a.tiles + tile) * kFitchRec;
     uint32_t own[16];
     onehot_from_code(f.code.x, f.code.y, f.code.z, f.code.w, ~0u, own);
-    if (x.m.x != 0 && ((x.m.x >> lane) & 1ull)) {   // a complex lane: its 16 planes
+    if constexpr (kCxCompact) {
+        cx_decode(own, f.code, f.cxb, (x.m.x >> lane) & 1ull, p, x.m.x);
+    } else if (x.m.x != 0 && ((x.m.x >> lane) & 1ull)) {   // a complex lane: its 16 planes
         const uint4* q = p + kWave + lanes_below(x.m.x);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

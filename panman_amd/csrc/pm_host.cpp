@@ -161,7 +161,7 @@ int alloc_columns(pm_ctx* c, int64_t sites) {
 int alloc_work(pm_ctx* c, int mode) {
     const int64_t wpad = wpad_of(c);
     const bool fitch = mode == PM_MODE_FITCH || mode == PM_MODE_BLOCK_FITCH;
-    const size_t planes = fitch ? 20 : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
+    const size_t planes = fitch ? 4 * kFitchRecQuads : 36;   // records of kFitchRec / kSankoffRec uint4 per tile
     const size_t need_sets = (size_t)c->dt.num_internal * wpad * planes * 4;
     const size_t need_mask = (size_t)c->dt.num_internal * (wpad / kWave) * kMaskWords * sizeof(uint64_t);
     hipError_t e;

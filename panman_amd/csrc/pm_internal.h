@@ -3,8 +3,9 @@
 // HBM layout (one pm_ctx = one GPU = one shard of S sites, W = ceil(S/32) words):
 //   leaf planes   [L][W] uint4     4 code bit-planes of 32 sites (16 B / 32 sites)
 //   leaf present  [L][W] uint32    only for leaves with partially present columns
-//   Fitch sets    [I][tile] records: 4 code planes per word + dense 16-plane sets for the
-//                 words holding a multi-code or empty set (pm_kernels.h store_fitch_set)
+//   Fitch sets    [I][tile] records: 4 code planes per word; a word holding a multi-code or
+//                 empty set adds its multi-code sites' 16-bit sets (compact complex lanes,
+//                 pm_kernels.h store_fitch_set)
 //   Sankoff sets  [I][W][32] u32   Z0 (optimal codes) + Z1 (one above optimal) planes
 //   finals        the root's in root_final [W] uint4; every other internal node's in its
 //                 record (complex lanes: quad 0 of the lane's slot; others: the record code)
@@ -36,6 +37,14 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kShards = PM_SHARDS;
 constexpr int kClasses = 6;   // post-order, pre-order levels, score, replay, whole graph, pre-order tail
 constexpr int kDegreeClasses = 4;
+// Compact complex lanes (Fitch records, pm_kernels.h cx_store): a complex word stores its code
+// planes, its multi-code-site mask and up to kCxSets 16-bit sets (32 B) instead of 16 planes
+// (64 B); 0 = the 16-plane format.  Record quads per word: simple area + complex areas.
+#ifndef PM_CX_COMPACT
+#define PM_CX_COMPACT 0
+#endif
+constexpr bool kCxCompact = PM_CX_COMPACT != 0;
+constexpr int kFitchRecQuads = kCxCompact ? 6 : 5;
 constexpr int kMaskWords = 8;     // record masks per (node, tile): complex, simple, dirty, parent's
                                   // complex, parent's simple, an S2 / S3 node's pushed dirty lanes,
                                   // Fitch: the first / second child's dirty lanes (one 64-B line)

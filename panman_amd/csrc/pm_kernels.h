@@ -179,7 +179,15 @@ __device__ __forceinline__ void store_set16(uint4* sets, int64_t node, int32_t t
 // Two u64 ballots per (node, tile) mark the complex and simple lanes (mbcnt gives a lane
 // its rank).  Traffic per record: 16 B per simple and 64 / 128 B per complex word
 // instead of 64 / 128 B for every word.  (At N*, 93 % of Fitch words are single-code.)
-constexpr int kFitchRec = 5 * kWave;     // uint4 per (node, tile)
+// Fitch, compact complex lanes (kCxCompact): a complex word is its code planes A (area 1; a
+// multi-code site's bits there are unused) and B = {M, s0|s1<<16, s2|s3<<16, s4|s5<<16}
+// (area 2): M marks its multi-code (or empty) sites, s_i is the 16-bit set of M's i-th site.
+// A word with more than kCxSets such sites is "full": B.x = kCxFull, its 16 planes in areas
+// 1, 3, 4, 5.  32 B per complex word instead of 64; the reader loads A in place of the code
+// word it loads anyway, plus B, and patches the one-hot expansion of A at M's sites.
+constexpr int kFitchRec = kFitchRecQuads * kWave;   // uint4 per (node, tile)
+constexpr int kCxSets = 6;
+constexpr uint32_t kCxFull = ~0u;
 constexpr int kSankoffRec = 9 * kWave;   // uint4 per (node, tile)
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
@@ -302,11 +310,83 @@ __device__ __forceinline__ void rec_store_head(uint4* p, uint64_t* cm, size_t re
 
 // Code planes of any lane of a record (complex lanes: unused), one load from a per-lane
 // address: the stored word of a simple lane or the consensus word (see kid_fetch on why
-// loads are not selected between branches).
+// loads are not selected between branches).  CX (compact Fitch records): a complex lane's A.
+template <bool CX = false>
 __device__ __forceinline__ uint4 rec_code_all(const uint4* p, const RecMask& m, int lane, const uint4* cons,
                                               int64_t word) {
     const uint4* src = ((m.s >> lane) & 1ull) ? p + lanes_below(m.s) : cons + word;
+    if (CX && ((m.x >> lane) & 1ull)) src = p + kWave + lanes_below(m.x);
     return load_rec(src);
+}
+
+// A compact record's B word (area 2) for every lane: complex lanes their own, the others the
+// first complex lane's (unused) -- or, no complex lane at all, a consensus word (see cx_base).
+__device__ __forceinline__ uint4 cx_b_load(const uint4* p, const RecMask& m, int lane, const uint4* cons) {
+    const bool cx = (m.x >> lane) & 1ull;
+    return load_rec((m.x ? p + 2 * kWave : cons + kWave) + (cx ? lanes_below(m.x) : 0u));
+}
+
+// Compact complex lanes: x = the one-hot expansion of the lane's A (every lane: its code's);
+// at a complex lane (cx) clear M's sites and set each one's 16-bit set from B.  A full lane
+// (B.x == kCxFull) takes A as planes 0-3 and loads planes 4-15 from areas 3-5 of record p
+// (mx: its complex lanes) -- a second round trip, taken only by a wave holding such a lane.
+// Wave-uniform trip count: the most multi-code sites any lane of the wave has.
+__device__ __forceinline__ void cx_decode(uint32_t* x, const uint4& A, const uint4& B, bool cx, const uint4* p, uint64_t mx) {
+    const uint32_t M = cx ? B.x : 0u;
+    if (__ballot(M != 0u) == 0) return;
+    const bool full = M == kCxFull;
+    uint32_t rem = full ? 0u : M;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] &= ~rem;
+    const uint32_t w[3] = {B.y, B.z, B.w};
+#pragma unroll
+    for (int i = 0; i < kCxSets; ++i) {
+        if (__ballot(rem != 0u) == 0) break;
+        const uint32_t bit = rem & (0u - rem);   // M's i-th site (0 once the lane has none left)
+        const uint32_t set = w[i >> 1] >> (16 * (i & 1));
+#pragma unroll
+        for (int v = 0; v < 16; ++v) x[v] |= bit & (uint32_t)((int32_t)(set << (31 - v)) >> 31);
+        rem &= rem - 1u;
+    }
+    if (__ballot(full) != 0) {
+        if (full) {
+            const uint4* q = p + kWave + lanes_below(mx);
+            x[0] = A.x; x[1] = A.y; x[2] = A.z; x[3] = A.w;
+#pragma unroll
+            for (int j = 1; j < 4; ++j) {
+                const uint4 t = load_rec(q + (j + 1) * kWave);
+                x[4 * j] = t.x; x[4 * j + 1] = t.y; x[4 * j + 2] = t.z; x[4 * j + 3] = t.w;
+            }
+        }
+    }
+}
+
+// Compact complex lanes, the writer (every lane calls; cx: the lane's word is complex, k its
+// rank among the complex lanes, s its 16 planes, multi its multi-code / empty sites, code its
+// code planes).  The sets are gathered site by site, as many rounds as the wave's most.
+__device__ __forceinline__ void cx_store(uint4* p, uint32_t k, const uint32_t* s, uint32_t multi, bool cx,
+                                         const uint32_t* code) {
+    const bool full = cx && __builtin_popcount(multi) > kCxSets;
+    uint32_t rem = cx && !full ? multi : 0u;
+    uint32_t w[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < kCxSets; ++i) {
+        if (__ballot(rem != 0u) == 0) break;
+        const uint32_t b = rem ? (uint32_t)__builtin_ctz(rem) : 0u;
+        uint32_t set = 0u;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) set |= ((s[v] >> b) & 1u) << v;
+        w[i >> 1] |= (rem ? set : 0u) << (16 * (i & 1));
+        rem &= rem - 1u;
+    }
+    if (!cx) return;
+    store_stream(p + kWave + k, full ? make_uint4(s[0], s[1], s[2], s[3]) : make_uint4(code[0], code[1], code[2], code[3]));
+    store_stream(p + 2 * kWave + k, full ? make_uint4(kCxFull, 0u, 0u, 0u) : make_uint4(multi, w[0], w[1], w[2]));
+    if (full) {
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+            store_stream(p + (j + 2) * kWave + k, make_uint4(s[4 * j], s[4 * j + 1], s[4 * j + 2], s[4 * j + 3]));
+    }
 }
 
 // Where a wave's complex-slot loads point: the record's complex area, or -- when the record
@@ -317,14 +397,24 @@ __device__ __forceinline__ const uint4* cx_base(const uint4* p, const RecMask& m
 }
 
 // A record lane in flight: its code planes and, for a complex lane, its 16 planes.
+// (compact records: c = A, v[0] = B; p / mx for a full lane's second load)
 struct SetFetch {
     uint4 c, v[4];
     bool cx;
+    const uint4* p;
+    uint64_t mx;
 };
 
 __device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m, const uint4* cons, int lane,
                                                 int64_t word, SetFetch& f) {
     f.cx = (m.x >> lane) & 1ull;
+    if constexpr (kCxCompact) {
+        f.c = rec_code_all<true>(p, m, lane, cons, word);
+        f.v[0] = cx_b_load(p, m, lane, cons);
+        f.p = p;
+        f.mx = m.x;
+        return;
+    }
     f.c = rec_code_all(p, m, lane, cons, word);
     // every lane loads (a branch here makes the compiler copy the results out of the load
     // registers and wait for them): lanes that are not complex read the first complex slot
@@ -337,6 +427,10 @@ __device__ __forceinline__ void fetch_fitch_set(const uint4* p, const RecMask& m
 
 __device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s) {
     onehot_from_code(f.c.x, f.c.y, f.c.z, f.c.w, ~0u, s);
+    if constexpr (kCxCompact) {
+        cx_decode(s, f.c, f.v[0], f.cx, f.p, f.mx);
+        return;
+    }
     if (f.cx) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -350,6 +444,12 @@ __device__ __forceinline__ void expand_fitch_set(const SetFetch& f, uint32_t* s)
 
 __device__ __forceinline__ void load_fitch_set(const uint4* p, const RecMask& m, const uint4* cons, int lane,
                                                int64_t word, uint32_t* s) {
+    if constexpr (kCxCompact) {
+        SetFetch f;
+        fetch_fitch_set(p, m, cons, lane, word, f);
+        expand_fitch_set(f, s);
+        return;
+    }
     const bool cx = (m.x >> lane) & 1ull;
     const uint4 c = rec_code_all(p, m, lane, cons, word);
     uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
@@ -392,6 +492,10 @@ __device__ __forceinline__ void store_fitch_set(uint4* sets, uint64_t* cmask, co
     uint32_t code[4];
     code_from_onehot(s, code[0], code[1], code[2], code[3]);
     rec_store_head(p, cmask, rec, lane, complex_word, dirty_extra, code, cw, mx, ms, md);
+    if constexpr (kCxCompact) {
+        cx_store(p, lanes_below(mx), s, ~one | two, complex_word, code);
+        return;
+    }
     if (complex_word) {
         const uint32_t k = lanes_below(mx);
 #pragma unroll
@@ -534,7 +638,17 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
         const size_t rec = (size_t)c * a.tiles + tile;
         const RecMask mk = rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * REC;
-        if ((mk.x >> lane) & 1ull) {
+        if constexpr (kCxCompact && REC == kFitchRec) {
+            SetFetch f;
+            fetch_fitch_set(p, mk, a.cons, lane, word, f);
+            uint32_t x[16];
+            expand_fitch_set(f, x);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                both[v] &= x[v];
+                either[v] |= x[v];
+            }
+        } else if ((mk.x >> lane) & 1ull) {
             const uint32_t k = lanes_below(mk.x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -567,6 +681,8 @@ __device__ __forceinline__ void fold_child(const UpArgs& a, int32_t c, int4 vl, 
 struct ChildFetch {
     uint4 code, v[4];
     bool cx;
+    const uint4* p;   // compact Fitch records: code = A, v[0] = B; p / mx for cx_decode
+    uint64_t mx;
 };
 
 // LEAFY: the caller knows c is a leaf or a virtual leaf-parent (no record, fewer registers).
@@ -596,6 +712,13 @@ __device__ __forceinline__ void fetch_child_ap(const UpArgs& a, int32_t c, int4 
         const RecMask m = SLOT ? RecMask{sx, ss, 0, 0, 0} : rec_mask(a.cmask, rec);
         const uint4* p = a.sets + rec * REC;   // Sankoff: the Z0 planes
         f.cx = (m.x >> lane) & 1ull;
+        if constexpr (kCxCompact && REC == kFitchRec) {
+            f.code = rec_code_all<true>(p, m, lane, a.cons, word);
+            f.v[0] = cx_b_load(p, m, lane, a.cons);
+            f.p = p;
+            f.mx = m.x;
+            return;
+        }
         f.code = rec_code_all(p, m, lane, a.cons, word);
         const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
         const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
@@ -618,6 +741,13 @@ __device__ __forceinline__ void fetch_child_ap_m(const UpArgs& a, int32_t c, int
     const RecMask m{mx, ms, 0, 0, 0};
     const uint4* p = a.sets + rec * REC;
     f.cx = (m.x >> lane) & 1ull;
+    if constexpr (kCxCompact && REC == kFitchRec) {
+        f.code = rec_code_all<true>(p, m, lane, a.cons, word);
+        f.v[0] = cx_b_load(p, m, lane, a.cons);
+        f.p = p;
+        f.mx = m.x;
+        return;
+    }
     f.code = rec_code_all(p, m, lane, a.cons, word);
     const uint4* base = cx_base(p, m, a.cons);   // see fetch_fitch_set
     const uint32_t k = f.cx ? lanes_below(m.x) : 0u;
@@ -665,7 +795,8 @@ __device__ __forceinline__ void subtree_set_ap(int shape, const ChildFetch& f, u
 }
 
 // A fetched child's 16-plane set (Fitch) / optimal set Z0 (Sankoff); vd as fold_child's.
-template <bool SUB = false>
+// CXC: a record child is a compact Fitch record (fetch_child_ap<kFitchRec>).
+template <bool SUB = false, bool CXC = false>
 __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
     const LoHi t = lohi_of(f.code.x, f.code.y, f.code.z, f.code.w, ~0u);
 #pragma unroll
@@ -680,6 +811,8 @@ __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetc
 #pragma unroll
             for (int v = 0; v < 16; ++v) x[v] |= u.lo[v & 3] & u.hi[v >> 2];
         }
+    } else if (CXC && c >= 0) {
+        cx_decode(x, f.code, f.v[0], f.cx, f.p, f.mx);
     } else if (c >= 0 && f.cx) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -690,9 +823,10 @@ __device__ __forceinline__ void child_set_ap(int32_t c, int4 vl, const ChildFetc
 
 // A child of a plain node (leaf, leaf-parent of one or two leaves, or record), branch-free over
 // its kind (wave-uniform) and the lane's complex flag: one select per plane.
+template <bool CXC = false>
 __device__ __forceinline__ void child_set_plain(int32_t c, int4 vl, const ChildFetch& f, uint32_t* x, uint32_t& vd) {
     const bool virt2 = c >= 0 && (c & kVirtualBit) && __builtin_amdgcn_readfirstlane(vl.y) >= 0;
-    const bool rec_cx = c >= 0 && !(c & kVirtualBit) && f.cx;
+    const bool rec_cx = !CXC && c >= 0 && !(c & kVirtualBit) && f.cx;
     const uint32_t m2 = virt2 ? ~0u : 0u;
     const uint4 L1 = f.v[0];
     vd |= m2 & code_ne(f.code, L1);
@@ -707,13 +841,14 @@ __device__ __forceinline__ void child_set_plain(int32_t c, int4 vl, const ChildF
             x[v] = rec_cx ? w[k] : y;
         }
     }
+    if (CXC && c >= 0 && !(c & kVirtualBit)) cx_decode(x, f.code, f.v[0], f.cx, f.p, f.mx);
 }
 
-template <bool SUB = false>
+template <bool SUB = false, bool CXC = false>
 __device__ __forceinline__ void fold_child_ap(int32_t c, int4 vl, const ChildFetch& f, uint32_t* both, uint32_t* either,
                                               uint32_t& vd) {
     uint32_t x[16];
-    child_set_ap<SUB>(c, vl, f, x, vd);
+    child_set_ap<SUB, CXC>(c, vl, f, x, vd);
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         both[v] &= x[v];
@@ -809,7 +944,7 @@ __device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& 
             const int4 vl = first ? vl0 : vl1;
             ChildFetch f;
             fetch_child_ap<REC, false, SUB, SLOT>(a, c, vl, tile, lane, word, f, first ? sl.x0 : sl.x1, first ? sl.s0 : sl.s1);
-            fold_child_ap<SUB>(c, vl, f, both, either, vd);
+            fold_child_ap<SUB, kCxCompact && REC == kFitchRec>(c, vl, f, both, either, vd);
         }
         return;
     }
@@ -819,8 +954,8 @@ __device__ __forceinline__ void fold_first_two(const UpArgs& a, const NodeDesc& 
     fetch_child_ap<REC, false, SUB, SLOT>(a, d.c0, vl0, tile, lane, word, f0, sl.x0, sl.s0);
     if (two) fetch_child_ap<REC, false, SUB, SLOT>(a, d.c1, vl1, tile, lane, word, f1, sl.x1, sl.s1);
     __builtin_amdgcn_sched_barrier(0);
-    fold_child_ap<SUB>(d.c0, vl0, f0, both, either, vd);
-    if (two) fold_child_ap<SUB>(d.c1, vl1, f1, both, either, vd);
+    fold_child_ap<SUB, kCxCompact && REC == kFitchRec>(d.c0, vl0, f0, both, either, vd);
+    if (two) fold_child_ap<SUB, kCxCompact && REC == kFitchRec>(d.c1, vl1, f1, both, either, vd);
 }
 
 // bit-sliced a < b for 4-bit codes
