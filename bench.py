@@ -402,7 +402,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail
     tail_design = parts.get("down_tail_items", 0.0) + parts.get("down_tail_leaf_words", 0.0)
     levels_design = sum(parts.get(k, 0.0) for k in ("down_own_records", "down_parent_finals", "down_dirty_leaf_words",
                                                        "down_finals_written"))
-    pmc_by_kernel = {}
+    pmc_by_kernel, fetch_by_kernel = {}, {}
     if traffic_all:
         try:
             tj = json.load(open(args.traffic))
@@ -411,20 +411,31 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail
                 v = tj.get(kk, {}).get(wk + ":step")
                 if v is not None and tj[kk].get(wk + ":build") == build:
                     pmc_by_kernel[kk] = v
+                    fetch_by_kernel[kk] = tj[kk].get(wk + ":fetch_step")
         except (OSError, ValueError):
             pmc_by_kernel = {}
     lv_pmc = sum(pmc_by_kernel.get(k, 0.0) for k in down_k) if any(k in pmc_by_kernel for k in down_k) else None
     tl_pmc = pmc_by_kernel.get("k_tail")
+    lv_fetch = sum(fetch_by_kernel.get(k) or 0.0 for k in down_k) if any(fetch_by_kernel.get(k) for k in down_k) else None
+    tl_fetch = fetch_by_kernel.get("k_tail")
+    lines = design.get("line_reads", {})
     pre_split = {
         "records_bytes_per_step": 8.0 * muts,
         "records_note": "8-B mutation records: written by both kernels, not split",
         "levels": {"kernels": " + ".join(down_k), "ms_per_step": round((ms[1] - tail_ms) / steps, 3),
                    "launches_per_step": (launches[1] - tail_launches) / steps,
                    "design_bytes_per_step": levels_design, "pmc_bytes_per_step": lv_pmc,
-                   "pmc_over_design": round(lv_pmc / levels_design, 3) if lv_pmc and levels_design else None},
+                   "pmc_over_design": round(lv_pmc / levels_design, 3) if lv_pmc and levels_design else None,
+                   "line_read_bytes_per_step": lines.get("levels"), "pmc_fetch_bytes_per_step": lv_fetch,
+                   "pmc_fetch_over_line_reads": round(lv_fetch / lines["levels"], 3) if lv_fetch and lines.get("levels") else None},
         "tail": {"kernels": "k_tail", "ms_per_step": round(tail_ms / steps, 3), "launches_per_step": tail_launches / steps,
                  "design_bytes_per_step": tail_design, "pmc_bytes_per_step": tl_pmc,
-                 "pmc_over_design": round(tl_pmc / tail_design, 3) if tl_pmc and tail_design else None},
+                 "pmc_over_design": round(tl_pmc / tail_design, 3) if tl_pmc and tail_design else None,
+                 "line_read_bytes_per_step": lines.get("tail"), "pmc_fetch_bytes_per_step": tl_fetch,
+                 "pmc_fetch_over_line_reads": round(tl_fetch / lines["tail"], 3) if tl_fetch and lines.get("tail") else None},
+        "line_read_parts_per_step": lines.get("parts"),
+        "line_note": "line reads: the pass's loads at 128-B line granularity (pm_design_bytes out[14..19]; a scattered "
+                     "16-B read draws a whole line, tools/calib_fetch.hip, profiles/r06_calib_fetch.txt)",
     }
     if fitch:   # SURVEY.md §8d contract: 2-B sets through memory
         contract = s_local * (0.5 * L + 2.0 * n_int + 2.0 * (n_int - 1)) + \

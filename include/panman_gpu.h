@@ -250,7 +250,11 @@ int pm_chunk_unpack(const uint64_t* all, int64_t per, int ranks, int64_t total_s
  * own records + pushed masks written; pre-order own records, parent finals, dirty-lane leaf
  * words of the nodes' first two children (k_down), finals written, tail items and their
  * dirty-lane leaf words (k_tail).  With the LDS-staged sweeps (PM_OPT_CLUSTER) a child record
- * read from an LDS slot, and a parent final likewise, is not counted.  `n` >= 5.
+ * read from an LDS slot, and a parent final likewise, is not counted.  With n >= 20, out[14..19]:
+ * the pre-order's reads at 128-B line granularity (every line a load touches, as the memory
+ * fetches them: tools/calib_fetch.hip) -- level kernels: descriptors + masks + own records,
+ * parent finals, dirty-lane leaf words; tail: descriptors + masks, dirty-lane leaf words,
+ * parent finals.  `n` >= 5.
  * Synchronises the ctx stream. */
 int pm_design_bytes(pm_ctx* ctx, double* out, int n);
 /* FETCH_SIZE calibration for scattered reads: `lanes` threads each read 4 x 16 B, one 16-B

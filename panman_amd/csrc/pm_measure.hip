@@ -218,6 +218,36 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     // finals written, down tail items (descriptor, parent masks and finals: k_tail), down tail
     // items' dirty leaf words (k_tail)
     double part[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // The pre-order's reads at the memory's granularity: every load draws whole 128-B lines
+    // (tools/calib_fetch.hip: one TCC read request per line touched, for 16-B and 64-B reads at
+    // any stride and for scattered ones), so a dirty lane's 16-B word costs a line unless a
+    // neighbour in the same line is read too.  The level kernels: line[0] descriptors, masks and
+    // own records, [1] parent finals, [2] dirty-lane leaf words; the tail: [3] descriptors and
+    // masks, [4] dirty-lane leaf words, [5] parent finals.
+    double line[6] = {0, 0, 0, 0, 0, 0};
+    const double LB = 128.0;
+    const int cx_areas = mode == PM_MODE_FITCH ? 4 : 8;   // complex planes read by the own-record load
+    auto groups8 = [](uint64_t v) {   // lines of a per-lane 16-B row (8 lanes a line)
+        int k = 0;
+        for (int b = 0; b < 8; ++b) k += ((v >> (8 * b)) & 0xFFull) != 0;
+        return k;
+    };
+    auto pairs = [](uint64_t v) { return popc((v | (v >> 1)) & 0x5555555555555555ull); };   // 64-B per-lane rows
+    auto ceil8 = [](int v) { return (v + 7) / 8; };
+
+    // lines of a record's area 0 read at lanes dm: simple lanes at their rank, complex lanes'
+    // finals after the simple codes (final_slot); consensus lanes read the cached consensus
+    auto rank_lines = [](uint64_t dm, uint64_t s, uint64_t x) {
+        const int ns = popc(s);
+        uint32_t seen = 0;
+        for (uint64_t r = dm & (s | x); r; r &= r - 1) {
+            const int l = __builtin_ctzll(r);
+            const uint64_t below = l ? (~0ull >> (64 - l)) : 0ull;
+            const int pos = ((s >> l) & 1ull) ? popc(s & below) : ns + popc(x & below);
+            seen |= 1u << (pos >> 3);
+        }
+        return popc(seen);
+    };
     auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
     // LDS-staged sweeps: a node whose parent is in its cluster hands its set (post-order) and
     // receives its parent's final (pre-order sweeps) through LDS
@@ -227,8 +257,15 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     for (int32_t d = 0; d < I; ++d) {
         if (vnode[d]) continue;
         const int32_t e0 = ht.child_off[d], e1 = ht.child_off[d + 1];
+        line[0] += 64.0;   // descriptor (a node's tiles run in adjacent waves)
         for (int t = 0; t < tiles; ++t) {
             const uint64_t* q = mk(d, t);
+            // level kernels: mask record (half a line), own record (simple codes by rank, then
+            // the complex areas), parent finals (every non-consensus lane)
+            line[0] += 64.0 + LB * (ceil8(popc(q[1])) + cx_areas * ceil8(popc(q[0])));
+            if (d != root && !(down_lds && in_lds(d))) line[1] += LB * rank_lines(q[3] | q[4], q[4], q[3]);
+            const uint64_t dirty_m = d == root ? ~0ull : q[2];
+            const uint64_t dleaf_m = leaf_rule && d != root ? q[0] : dirty_m;
             const double rec = 64.0 + lane * popc(q[1]) + cx_full * popc(q[0]);
             // post-order: children in, own record + masks out, parent masks pushed to children
             up += rec;
@@ -244,11 +281,16 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                 // k_tail item (a leaf-ish child beyond the second, or an S2 / S3 child in the
                 // subtree form)
                 const bool tail = (k >= e0 + 2 && (ch < 0 || vnode[ch])) || (sub && ch >= 0 && vnode[ch] > 2);
+                // a k_tail item's dirty lanes (as below)
+                const uint64_t tdm = d == root ? ~0ull
+                                     : ch >= 0 && vnode[ch] > 2 ? mk(ch, t)[5]
+                                     : ch < 0 && leaf_rule ? q[0] : q[2];
                 if (ch < 0) {
                     up += word_row;
                     down += lane * dirty_leaf;
                     part[0] += word_row;
                     part[tail ? 8 : 5] += lane * dirty_leaf;
+                    line[tail ? 4 : 2] += LB * groups8(tail ? tdm : dleaf_m);
                 } else if (vnode[ch]) {
                     const int32_t nl = vnode[ch];
                     // (Fitch, all present: the first two children's own masks, words 6 / 7)
@@ -259,6 +301,12 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                     down += lane * dv * nl;
                     part[0] += word_row * nl;
                     part[tail ? 8 : 5] += lane * dv * nl;
+                    const uint64_t dv_m = vnode[ch] > 2 ? mk(ch, t)[5]
+                                          : leaf_rule && d != root && k < e0 + 2 ? q[6 + (k - e0) - (k > e0 && s_child(e0))]
+                                                                                 : dirty_m;
+                    // an S2 / S3 item: its leaves side by side (64 B a lane, sub_planes); a
+                    // leaf-parent: one row per leaf
+                    line[tail ? 4 : 2] += vnode[ch] > 2 ? LB * pairs(dv_m) : LB * groups8(tail ? tdm : dv_m) * nl;
                 } else if (!in_lds(ch)) {
                     const uint64_t* r = mk(ch, t);
                     const double b = 64.0 + lane * popc(r[1]) + cx_read_up * popc(r[0]) + lane;   // + pushed masks
@@ -268,12 +316,14 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
                 // a k_tail item: descriptor + parent masks (64 B each), the parent's final on its
                 // dirty non-consensus lanes
                 if (tail) {
-                    const uint64_t dm = d == root ? ~0ull
-                                        : ch >= 0 && vnode[ch] > 2 ? mk(ch, t)[5]
-                                        : ch < 0 && leaf_rule ? q[0] : q[2];
+                    const uint64_t dm = tdm;
                     const double b = 128.0 + lane * popc((q[0] | q[1]) & dm);
                     down += b;
                     part[7] += b;
+                    // descriptor (adjacent tiles: once per item), masks; the parent's final at
+                    // the dirty lanes (by rank in its record, or the root's row)
+                    line[3] += (t == 0 ? 64.0 : 0.0) + 64.0;
+                    if (dm) line[5] += LB * (d == root ? groups8(dm) : rank_lines(dm, q[1], q[0]));
                 }
             }
             // pre-order: own record, parent final (non-consensus lanes), compact final out
@@ -296,6 +346,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     out[3] = 0.5 * (double)L * (double)c->num_sites + 8.0 * (double)records;   // floor: leaf codes once + records
     out[4] = (double)records;
     for (int k = 0; k < 9 && 5 + k < n; ++k) out[5 + k] = part[k];
+    for (int k = 0; k < 6 && 14 + k < n; ++k) out[14 + k] = line[k];
     return PM_OK;
 }
 

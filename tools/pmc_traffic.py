@@ -55,6 +55,7 @@ def main():
         step = ""
         if runs:
             res[k][key + ":step"] = (2.0 * bf + bw * nf / nw) / runs
+            res[k][key + ":fetch_step"] = 2.0 * bf / runs
             step = f"  {res[k][key + ':step'] / 1e9:8.3f} GB/run ({nf / runs:.1f} launches)"
         print(f"{k:32s} launches {nf:5d}  fetch(x2) {2 * bf / nf / 1e6:10.2f} MB  write {bw / nw / 1e6:10.2f} MB"
               f"  -> {per_launch / 1e6:10.2f} MB/launch{step}")
