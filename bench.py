@@ -347,6 +347,12 @@ def parsimony_block(args, eng, mode, ctx):
             "config": {"workload": workload_label(name, args.tree, L, S, world), "sites_per_gpu": s_local}}
 
 
+def traffic_key(mode: str, tree: str, leaves: int, sites: int) -> str:
+    """profiles/traffic_fitch.json's workload key (tools/profile_fitch.sh writes the same):
+    mode:leaves x sites-per-GPU, with the tree family unless it is the random-join default."""
+    return f"{mode}:{leaves}x{sites}" + ("" if tree == "random-join" else f":{tree}")
+
+
 def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail_ms=0.0, tail_launches=0):
     """Roofline of the dominant kernel.  `achieved` = the bytes THIS design must move per
     launch (pm_design_bytes: leaf words, compressed records written and read, compact
@@ -380,7 +386,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            wk = f"{key}:{L}x{s_local}"
+            wk = traffic_key(key, args.tree, L, s_local)
             # PMC bytes count only for the library build they were measured on
             stamps = {tj[n].get(wk + ":build") for kk in prof_names.values() for n in kk if wk in tj.get(n, {})}
             if stamps and stamps != {build}:
@@ -406,7 +412,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail
     if traffic_all:
         try:
             tj = json.load(open(args.traffic))
-            wk = f"{key}:{L}x{s_local}"
+            wk = traffic_key(key, args.tree, L, s_local)
             for kk in down_k + ("k_tail",):
                 v = tj.get(kk, {}).get(wk + ":step")
                 if v is not None and tj[kk].get(wk + ":build") == build:

@@ -8,9 +8,12 @@ mkdir -p gpurun_out
 (while true; do date >> gpurun_out/heartbeat_$tag.txt; sleep 30; done) &
 hb=$!
 trap "kill $hb" EXIT
+if [ -z "${ONLY_LINES:-}" ]; then
+if [ -z "${NOTESTS:-}" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > gpurun_out/gputests_$tag.log 2>&1 \
   || { echo "GPU TESTS FAILED"; tail -60 gpurun_out/gputests_$tag.log; exit 1; }
 tail -2 gpurun_out/gputests_$tag.log
+fi
 timeout -k 10 900 python bench.py > gpurun_out/bench_default_$tag.json 2> gpurun_out/bench_default_$tag.err \
   || { echo "bench failed"; tail -20 gpurun_out/bench_default_$tag.err; exit 2; }
 python3 -c "
@@ -19,6 +22,7 @@ print('N*', round(d['ms_per_step'],3), 'ms', r['kernel'], r['kernel_ms_per_step'
 print('cmds', json.dumps(d.get('commands'))[:1500])
 print('replay cpu', json.dumps(d['secondary']['replay']['cpu_baseline'])[:400])
 "
+fi
 # the other configs' lines (bench.py's labels), each against the same traffic file
 line() {  # NAME ARGS...
   local name=$1; shift

@@ -12,7 +12,8 @@ for path in sys.argv[2:]:
         res.setdefault(k, {}).update(v)
 clean = {}
 for k, v in res.items():
-    keep = {kk: vv for kk, vv in v.items() if (kk.split(":step")[0] + ":build") in v or kk.endswith(":build")}
+    base = lambda kk: kk.rsplit(":", 1)[0] if kk.endswith((":step", ":fetch_step")) else kk
+    keep = {kk: vv for kk, vv in v.items() if (base(kk) + ":build") in v or kk.endswith(":build")}
     keep = {kk: vv for kk, vv in keep.items() if not kk.endswith(":build") or kk[:-6] in keep}
     if keep:
         clean[k] = keep

@@ -24,8 +24,10 @@ run write --pmc WRITE_SIZE
 run sq --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS
 leaves=$(python3 -c "import json;d=json.load(open('$out/stats.json'));print(d['config']['leaves'])")
 sites=$(python3 -c "import json;d=json.load(open('$out/stats.json'));print(d['config']['sites_per_gpu'])")
+# (the tree family joins the key unless random-join: bench.py traffic_key)
+tsuf=$(python3 -c "import json;t=json.load(open('$out/stats.json'))['config']['tree'];print('' if t=='random-join' else ':'+t)")
 build=$(python3 -c "import json;print(json.load(open('$out/stats.json'))['build_id'])")
-python3 tools/pmc_traffic.py "$out/fetch" "$out/write" "$mode:${leaves}x${sites}" "$out/traffic.json" "$build" > "$out/traffic.txt"
+python3 tools/pmc_traffic.py "$out/fetch" "$out/write" "$mode:${leaves}x${sites}$tsuf" "$out/traffic.json" "$build" > "$out/traffic.txt"
 python3 tools/pmc_summary.py "$out/sq" > "$out/sq.txt"
 find "$out" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
 echo "profile $tag done"
