@@ -191,18 +191,21 @@ int plan_clusters(const HostTree& ht, const std::vector<int32_t>& up_order_k, co
             hi = lo;
             band(l0, hi, false);   // (its sizes)
         }
-        int32_t longest = 0;
+        int32_t longest = 0, roots = 0;
         for (int32_t l = l0; l < hi; ++l)
             for (int32_t i = ht.up_level_off_k[l]; i < ht.up_level_off_k[l + 1]; ++i) {
                 const int32_t d = up_order_k[i];
                 const int32_t p = parent_dense[d];
-                if (!(p >= 0 && level_of[p] >= l0 && level_of[p] < hi)) longest = std::max(longest, size[d]);
+                if (!(p >= 0 && level_of[p] >= l0 && level_of[p] < hi)) {
+                    longest = std::max(longest, size[d]);
+                    ++roots;
+                }
             }
         if (std::getenv("PM_CL_DEBUG"))
-            std::fprintf(stderr, "band [%d, %d) longest %d nodes %d\n", l0, hi, longest,
+            std::fprintf(stderr, "band [%d, %d) longest %d clusters %d nodes %d\n", l0, hi, longest, roots,
                          ht.up_level_off_k[hi] - ht.up_level_off_k[l0]);
         bands.emplace_back(l0, hi);
-        if (chain_check && longest > kClChain * (hi - l0)) start = (int32_t)bands.size();
+        if (chain_check && (longest > kClChain * (hi - l0) || roots > kClMaxClusters)) start = (int32_t)bands.size();
         l0 = hi;
     }
     if (start >= (int32_t)bands.size()) {

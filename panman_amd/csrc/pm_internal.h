@@ -180,6 +180,14 @@ constexpr int32_t kClBandHeights = PM_CL_BAND;
 #define PM_CL_CHAIN 4
 #endif
 constexpr int32_t kClChain = PM_CL_CHAIN;
+// ... or wide: more clusters than this (a level kernel's waves then fill the GPU as well, and
+// its nodes run side by side where a cluster's run one after another).  C4 (T2) share
+// 27.74 -> 26.88 ms (its bands below height 62 hold 25k-454k clusters), C3 unchanged (its
+// widest band: 5.2k clusters); 4096 / 32768: 27.44 / 27.10 ms (r06mc, tools/gpu_r06mc.sh)
+#ifndef PM_CL_MAX_CLUSTERS
+#define PM_CL_MAX_CLUSTERS 16384
+#endif
+constexpr int32_t kClMaxClusters = PM_CL_MAX_CLUSTERS;
 constexpr int32_t kClMaxLevel = PM_CL_MAX_LEVEL;
 #ifndef PM_CL_FSLOTS
 #define PM_CL_FSLOTS 8
