@@ -1816,5 +1816,222 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
+// ---- LDS-staged pre-order sweeps over the post-order's clusters (plan_cluster_down) -------
+// One wave = one (cluster, tile), the bands top-down: the cluster's nodes in depth-first
+// pre-order, one per step -- down_node's work for the node and its first two (non-S2 / S3)
+// children (Fitch: src/fitchSankoff.cpp:96-171; Sankoff: :487-531, :676-703), with the parent's final from the LDS slot its own
+// step wrote (the cluster root's from memory, stored by an earlier band), its own final into a
+// slot for its children and, compact, to memory for the tail launch.  Records are staged in
+// the wave's LDS entries across steps and flushed when full (one returned atomic per 128
+// entries, not per node).  The step's descriptor, masks and record node ids come from vector
+// loads two / one steps ahead; its own record code, the cluster root's parent final and its
+// children's dirty leaf words one step ahead.
+struct ClDownArgs {
+    const NodeDesc* items;
+    const int32_t* wg_off;
+    int32_t wg0;
+};
+typedef uint4 ClFinals[kClFSlots][kWave];
+
+// (vector) the item's descriptor: lane k < 16 = dword k
+__device__ __forceinline__ uint32_t cld_desc_load(const ClDownArgs& c, int32_t it, int lane) {
+    return reinterpret_cast<const uint32_t*>(c.items + it)[lane & 15];
+}
+
+// (vector) the node's masks (lanes 0..15: 8 u64 words), its node id (16), its first two
+// children's record node ids (17..19, 20..22: the child, a leaf-parent's leaves)
+__device__ __forceinline__ uint32_t cld_mask_load(const DownArgs& a, const NodeDesc& d, int tile, int lane) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cmask + kMaskWords * ((size_t)d.node * a.tiles + tile)) + (lane & 15);
+    const int k = lane >= 20 ? 1 : 0, j = lane - (k ? 20 : 17);
+    const int32_t enc = k ? d.c1 : d.c0;
+    const int32_t v0 = k ? d.vl1[0] : d.vl0[0], v1 = k ? d.vl1[1] : d.vl0[1];
+    const bool has = !k || d.e1 - d.e0 > 1;
+    if (lane == 16) src = reinterpret_cast<const uint32_t*>(a.internal_id + d.node);
+    else if (lane >= 17 && lane < 23 && has) {
+        if (enc < 0) src = reinterpret_cast<const uint32_t*>(a.leaf_id + (j == 0 ? -enc - 1 : 0));
+        else if (enc & kVirtualBit)
+            src = j == 0 ? reinterpret_cast<const uint32_t*>(a.internal_id + (enc & kDenseMask))
+                         : reinterpret_cast<const uint32_t*>(a.leaf_id + (j == 1 ? v0 : v1 >= 0 ? v1 : v0));
+    }
+    return *src;
+}
+
+struct ClDownMeta {
+    NodeDesc d;
+    RecMask m;
+    uint64_t w6, w7;
+    uint32_t id, kid[2][3];
+};
+
+__device__ __forceinline__ void cld_desc_get(uint32_t v, NodeDesc& d) {
+    int32_t* p = reinterpret_cast<int32_t*>(&d);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] = __builtin_amdgcn_readlane((int)v, k);
+}
+
+__device__ __forceinline__ void cld_mask_get(uint32_t v, ClDownMeta& x) {
+    auto u64 = [&](int k) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 2 * k + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 2 * k);
+    };
+    x.m = RecMask{u64(0), u64(1), u64(2), u64(3), u64(4)};
+    x.w6 = u64(6);
+    x.w7 = u64(7);
+    x.id = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) x.kid[k][j] = (uint32_t)__builtin_amdgcn_readlane((int)v, 17 + 3 * k + j);
+}
+
+// A step's loads issued one step ahead: its record's code word, the cluster root's parent final,
+// its first two children's leaf words at their dirty lanes.
+struct ClDownFetch {
+    uint4 code, pf, cxb;   // (cxb: compact records' B word)
+    Kid k0, k1;
+};
+
+template <Mode M>
+__device__ __forceinline__ void cld_issue(const DownArgs& a, const ClDownMeta& x, int tile, int lane, int64_t word,
+                                          ClDownFetch& f) {
+    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    constexpr bool CX = M == Mode::kFitch && kCxCompact;
+    const NodeDesc& d = x.d;
+    const bool is_root = d.parent < 0;
+    const uint4* p = a.sets + ((size_t)d.node * a.tiles + tile) * REC;
+    f.code = rec_code_all<CX>(p, x.m, lane, a.cons, word);
+    if constexpr (CX) f.cxb = cx_b_load(p, x.m, lane, a.cons);
+    if (d.pad0 < 0) f.pf = is_root ? a.cons[word] : parent_final<REC>(a, d.parent, x.m, tile, lane, word);
+    // Fitch, every leaf present: a leaf child differs from the final only at the complex lanes,
+    // a virtual one there and where its own leaves disagree (mask words 6, 7); Sankoff: the
+    // node's dirty lanes (see down_node)
+    const uint64_t k0 = M == Mode::kFitch ? (d.c0 < 0 ? x.m.x : x.w6) : x.m.d;
+    const uint64_t k1 = M == Mode::kFitch ? (d.c1 < 0 ? x.m.x : x.w7) : x.m.d;
+    kid_fetch<M, true, false, false>(a, d.c0, make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), word,
+                                     is_root || ((k0 >> lane) & 1ull), f.k0);
+    if (d.e1 - d.e0 > 1)
+        kid_fetch<M, true, false, false>(a, d.c1, make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]), word,
+                                         is_root || ((k1 >> lane) & 1ull), f.k1);
+}
+
+template <Mode M>
+__device__ __forceinline__ void cld_step(const DownArgs& a, const ClDownMeta& x, const ClDownFetch& f, ClFinals& FS, Emit& em,
+                                         int tile, int lane, int64_t word, uint32_t valid) {
+    constexpr int REC = M == Mode::kSankoff ? kSankoffRec : kFitchRec;
+    const NodeDesc& d = x.d;
+    const bool is_root = d.parent < 0;
+    uint4* const p = a.sets + ((size_t)d.node * a.tiles + tile) * REC;
+    uint32_t own[16], z1[16];
+    onehot_from_code(f.code.x, f.code.y, f.code.z, f.code.w, ~0u, own);
+    if constexpr (M == Mode::kSankoff) {   // (load_sankoff: a complex lane's Z0 and Z1 planes)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) z1[v] = 0u;
+        if ((x.m.x >> lane) & 1ull) {
+            const uint32_t k = lanes_below(x.m.x);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 w = load_rec(p + kWave + q * kWave + k);
+                own[4 * q] = w.x; own[4 * q + 1] = w.y; own[4 * q + 2] = w.z; own[4 * q + 3] = w.w;
+            }
+            if (!is_root) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 w = load_rec(p + 5 * kWave + q * kWave + k);
+                    z1[4 * q] = w.x; z1[4 * q + 1] = w.y; z1[4 * q + 2] = w.z; z1[4 * q + 3] = w.w;
+                }
+            }
+        }
+    } else if constexpr (kCxCompact) {
+        cx_decode(own, f.code, f.cxb, (x.m.x >> lane) & 1ull, p, x.m.x);
+    } else if (x.m.x != 0 && ((x.m.x >> lane) & 1ull)) {   // a complex lane: its 16 planes
+        const uint4* q = p + kWave + lanes_below(x.m.x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 w = load_rec(q + j * kWave);
+            own[4 * j] = w.x; own[4 * j + 1] = w.y; own[4 * j + 2] = w.z; own[4 * j + 3] = w.w;
+        }
+    }
+    const uint4 q = d.pad0 >= 0 ? FS[d.pad0][lane] : f.pf;
+    const uint32_t pc[4] = {q.x, q.y, q.z, q.w};
+    uint32_t F[4], pres;
+    resolve_final<M>(a, is_root, word, own, M == Mode::kSankoff ? z1 : nullptr, pc, F, pres);
+    store_final(a, is_root, p, x.m, lane, word, F);
+    if (d.pad1 >= 0) FS[d.pad1][lane] = make_uint4(F[0], F[1], F[2], F[3]);
+    if (is_root) {
+        for (int b = 0; b < 32; ++b) {
+            const int64_t site = word * 32 + b;
+            if (site < a.sites)
+                a.root_code[site] = ((pres >> b) & 1u) ? (uint8_t)code_at(F[0], F[1], F[2], F[3], b) : (uint8_t)255;
+        }
+    }
+    const uint32_t self_diff = pres & valid & ((F[0] ^ pc[0]) | (F[1] ^ pc[1]) | (F[2] ^ pc[2]) | (F[3] ^ pc[3]));
+    const uint32_t site0 = (uint32_t)(word * 32);
+    emit_stream(a, em, lane, x.id, self_diff, site0, F[0], F[1], F[2], F[3], pc);
+    kid_emit<M>(a, em, lane, f.k0, x.kid[0][0], x.kid[0][1], x.kid[0][2], valid, F, site0);
+    if (d.e1 - d.e0 > 1) kid_emit<M>(a, em, lane, f.k1, x.kid[1][0], x.kid[1][1], x.kid[1][2], valid, F, site0);
+}
+
+#ifndef PM_CLD_WAVES
+#define PM_CLD_WAVES 3
+#endif
+template <Mode M>
+__global__ __launch_bounds__(kWave, PM_CLD_WAVES) void k_down_cluster(DownArgs a, ClDownArgs c) {
+    __shared__ ClFinals FS;
+    __shared__ uint4 stage[kEntryQuads];
+    const int lane = threadIdx.x;
+    const int32_t b = (int32_t)blockIdx.x;
+    const int32_t wl = b / a.tiles;
+    const int tile = b - wl * a.tiles;
+    const int32_t i0 = c.wg_off[c.wg0 + wl], steps = c.wg_off[c.wg0 + wl + 1] - i0;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    const uint32_t valid = valid_mask(a, word);
+    Emit em{stage, shard_of((uint32_t)(c.wg0 + wl), tile), 0u, 0u};
+    // pipeline: descriptors three steps ahead (vector loads), masks / ids two, data one
+    ClDownMeta X0, X1;
+    ClDownFetch fA, fB;
+    NodeDesc dn;
+    cld_desc_get(cld_desc_load(c, i0, lane), X0.d);
+    cld_mask_get(cld_mask_load(a, X0.d, tile, lane), X0);
+    cld_issue<M>(a, X0, tile, lane, word, fA);
+    uint32_t vm1 = 0u, vd2 = 0u;
+    if (steps > 1) {
+        cld_desc_get(cld_desc_load(c, i0 + 1, lane), X1.d);
+        vm1 = cld_mask_load(a, X1.d, tile, lane);
+    }
+    if (steps > 2) vd2 = cld_desc_load(c, i0 + 2, lane);
+    for (int32_t r = 0; r < steps; r += 2) {
+        // step r (X0, fA); step r + 1's data into fB; step r + 2's masks; step r + 3's descriptor
+        const uint32_t vd3 = r + 3 < steps ? cld_desc_load(c, i0 + r + 3, lane) : 0u;
+        uint32_t vm2 = 0u;
+        if (r + 2 < steps) {
+            cld_desc_get(vd2, dn);
+            vm2 = cld_mask_load(a, dn, tile, lane);
+        }
+        if (r + 1 < steps) {
+            cld_mask_get(vm1, X1);
+            cld_issue<M>(a, X1, tile, lane, word, fB);
+        }
+        cld_step<M>(a, X0, fA, FS, em, tile, lane, word, valid);
+        if (r + 1 >= steps) break;
+        // step r + 1 (X1, fB); step r + 2's data into fA; step r + 3's masks; step r + 4's descriptor
+        const uint32_t vd4 = r + 4 < steps ? cld_desc_load(c, i0 + r + 4, lane) : 0u;
+        NodeDesc d3 = dn;
+        uint32_t vm3 = 0u;
+        if (r + 3 < steps) {
+            cld_desc_get(vd3, d3);
+            vm3 = cld_mask_load(a, d3, tile, lane);
+        }
+        if (r + 2 < steps) {
+            X0.d = dn;
+            cld_mask_get(vm2, X0);
+            cld_issue<M>(a, X0, tile, lane, word, fA);
+        }
+        cld_step<M>(a, X1, fB, FS, em, tile, lane, word, valid);
+        X1.d = d3;
+        vm1 = vm3;
+        vd2 = vd4;
+    }
+    emit_flush<M != Mode::kSankoff>(a, em, lane);
+}
+
 }  // namespace PM_KNS
 }  // namespace pm

@@ -251,9 +251,12 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
     // LDS-staged sweeps: a node whose parent is in its cluster hands its set (post-order) and
     // receives its parent's final (pre-order sweeps) through LDS
-    const bool clu = mode == PM_MODE_FITCH && sub && c->cluster && ht.cl.band_wg.size() > 1 && !ht.cl.slot_of.empty();
-    auto in_lds = [&](int32_t d) { return clu && ht.cl.slot_of[d] >= 0; };
-    const bool down_lds = clu && ht.cl.down && !c->sub_down;
+    // (post-order sweeps: Fitch; pre-order sweeps: both modes)
+    const bool planned = sub && c->cluster && ht.cl.band_wg.size() > 1 && !ht.cl.slot_of.empty();
+    const bool clu = mode == PM_MODE_FITCH && planned;
+    auto in_cluster = [&](int32_t d) { return planned && ht.cl.slot_of[d] >= 0; };
+    auto in_lds = [&](int32_t d) { return clu && in_cluster(d); };
+    const bool down_lds = planned && ht.cl.down && (mode == PM_MODE_SANKOFF || !c->sub_down);
     for (int32_t d = 0; d < I; ++d) {
         if (vnode[d]) continue;
         const int32_t e0 = ht.child_off[d], e1 = ht.child_off[d + 1];
@@ -263,7 +266,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             // level kernels: mask record (half a line), own record (simple codes by rank, then
             // the complex areas), parent finals (every non-consensus lane)
             line[0] += 64.0 + LB * (ceil8(popc(q[1])) + cx_areas * ceil8(popc(q[0])));
-            if (d != root && !(down_lds && in_lds(d))) line[1] += LB * rank_lines(q[3] | q[4], q[4], q[3]);
+            if (d != root && !(down_lds && in_cluster(d))) line[1] += LB * rank_lines(q[3] | q[4], q[4], q[3]);
             const uint64_t dirty_m = d == root ? ~0ull : q[2];
             const uint64_t dleaf_m = leaf_rule && d != root ? q[0] : dirty_m;
             const double rec = 64.0 + lane * popc(q[1]) + cx_full * popc(q[0]);
@@ -332,7 +335,7 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
             if (d == root) {
                 down += 2.0 * word_row;   // forced / root final
             } else {
-                const double pf = down_lds && in_lds(d) ? 0.0 : lane * popc(q[3] | q[4]);
+                const double pf = down_lds && in_cluster(d) ? 0.0 : lane * popc(q[3] | q[4]);
                 down += pf + lane * popc(q[0]);
                 part[4] += pf;
                 part[6] += lane * popc(q[0]);

@@ -649,7 +649,21 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     dn.all_present = c->leaves_all_present;
     dn.vleaf = reinterpret_cast<const int4*>(dt.vleaf);
     dn.vinner = dt.vinner;
-    const int D = (int)down_off.size() - 1;
+    // pre-order sweeps over the planner's clusters (PM_OPT_CLUSTER, every level swept: the
+    // same schedule as the Fitch pre-order's, k_down_cluster<Sankoff>), the bands top-down
+    const ClusterPlan& cl = ht.cl;
+    const bool cld = sub && c->cluster && cl.band_wg.size() > 1 && cl.down;
+    if (cld) {
+        for (size_t bnd = cl.band_wg.size() - 1; bnd-- > 0;) {
+            const ClDownArgs ca{dt.cl_down_items, dt.cl_wg_off, cl.band_wg[bnd]};
+            const int64_t nwg = cl.band_wg[bnd + 1] - ca.wg0;
+            if (nwg == 0) continue;
+            timer_begin(c, 1);
+            hipLaunchKernelGGL(k_down_cluster<Mode::kSankoff>, dim3((unsigned)(nwg * tiles)), dim3(kWave), 0, c->stream, dn, ca);
+            timer_end(c, 1);
+        }
+    }
+    const int D = cld ? 0 : (int)down_off.size() - 1;
     // a pre-order level = one range of dense indices: [down_off[d], down_off[d+1]) in the
     // leaf-parent form, from down_dense_base_k[d] in the subtree form
     const bool dense_all = sub ? ht.down_dense_k : virt && ht.down_dense_v;

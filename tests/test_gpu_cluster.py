@@ -21,7 +21,8 @@ def engine():
     e.close()
 
 
-def _run(engine, off, idx, root, cluster, sites=None, codes=None, cons=None, forced=None, seed=5):
+def _run(engine, off, idx, root, cluster, sites=None, codes=None, cons=None, forced=None, seed=5,
+         mode=panman_amd.MODE_FITCH):
     engine.set_cluster(cluster)
     phase_reset()
     engine.tree_upload(off, idx, root)
@@ -35,7 +36,7 @@ def _run(engine, off, idx, root, cluster, sites=None, codes=None, cons=None, for
         node_row[leaf_ids] = np.arange(len(leaf_ids), dtype=np.int32)
         engine.leaves_upload(codes, node_row)
         engine.sites_upload(cons, forced)
-    engine.run(panman_amd.MODE_FITCH)
+    engine.run(mode)
     got = engine.mutations()
     score, rootc = engine.site_results()
     return got, score, rootc, ph
@@ -110,3 +111,50 @@ def test_cluster_t2_100k_sampled_vs_oracle(engine, oracle):
     assert sel.shape == want.shape and (sel == want).all()
     assert (rootc[cols] == want_root).all()
     assert (score == np.bincount(got[got[:, 0] != root][:, 1], minlength=sites)).all()
+
+
+@pytest.mark.parametrize("threshold", [1, 1 << 20])
+@pytest.mark.parametrize("leaves,sites", [(3000, 4500), (20000, 2100)])
+def test_cluster_sankoff_equals_levels(engine, leaves, sites, threshold):
+    """Sankoff runs the pre-order over the same clusters (k_down_cluster<Sankoff>: Z0 / Z1 of
+    the node's record, the parent's final through LDS, src/fitchSankoff.cpp:487-531, :676-703)
+    whenever the plan sweeps every height: records, scores and root codes equal to the level
+    kernels'."""
+    off, idx, root = panman_amd.sars_like_tree(leaves, seed=31)
+    try:
+        want = _run(engine, off, idx, root, 0, sites, mode=panman_amd.MODE_SANKOFF)
+        got = _run(engine, off, idx, root, threshold, sites, mode=panman_amd.MODE_SANKOFF)
+    finally:
+        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT)
+    assert got[3]["cluster.bands"] > 0 and got[3]["cluster.down"] == 1, got[3]
+    assert want[0].shape[0] > 0
+    assert got[0].shape == want[0].shape and (got[0] == want[0]).all()
+    assert (got[1] == want[1]).all() and (got[2] == want[2]).all()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_cluster_sankoff_vs_oracle_polytomies(engine, oracle, seed):
+    """Sankoff with the pre-order sweeps on random polytomy trees (every leaf present, random
+    codes incl. gaps / ambiguity codes, a forced root on odd seeds) against the oracle."""
+    rng = np.random.default_rng(7300 + seed)
+    off, idx, root = random_tree(600, rng, max_children=[2, 3, 9, 40][seed], unary=0.0)
+    leaves = int((np.diff(off) == 0).sum())
+    sites = [97, 2049, 4100, 2048][seed]
+    codes, _ = _random_columns(rng, leaves, sites, absent_frac=0.0)
+    cons = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=sites)
+    forced = rng.integers(0, 16, size=sites).astype(np.uint8) if seed % 2 else None
+    try:
+        got, score, rootc, ph = _run(engine, off, idx, root, 1 << 20, codes=codes, cons=cons, forced=forced,
+                                     mode=panman_amd.MODE_SANKOFF)
+    finally:
+        engine.set_cluster(panman_amd.engine.CLUSTER_DEFAULT)
+    assert ph["cluster.bands"] > 0 and ph["cluster.down"] == 1, ph
+    n = off.shape[0] - 1
+    node_row = np.full(n, -1, np.int32)
+    node_row[[i for i in range(n) if off[i] == off[i + 1]]] = np.arange(leaves, dtype=np.int32)
+    _, want, want_root = oracle.csr_columns(off, idx, root, names_for(off), codes, node_row, cons, forced,
+                                            algo=1, threads=8, with_root=True)
+    assert got.shape == want.shape and (got == want).all()
+    assert (rootc == want_root).all()
+    nonroot = want[want[:, 0] != root]
+    assert (score == np.bincount(nonroot[:, 1], minlength=sites)).all()
