@@ -420,29 +420,6 @@ __global__ __launch_bounds__(kBandBlock) void k_fitch_up_band(UpArgs a, const in
 // every other child as in fitch_up_node (leaf words, a leaf-parent's or S2 / S3 subtree's
 // leaves, or an earlier launch's compressed record).  Records and masks go to HBM exactly as
 // the level kernels write them (the pre-order pass and the tail read them), without a wait.
-struct ClArgs {
-    const NodeDesc* items;
-    const int32_t* wg_off;
-    const int32_t* slot_of;
-    const int32_t* pslot;   // per item: the parent's up slot (parent in a later band), -1
-    int32_t upm_base;       // up slots of item i: UpArgs::upm item upm_base + i (after the level items')
-    int32_t wg0;
-};
-typedef uint4 ClSlots[kClSlots][4][kWave];
-
-__device__ __forceinline__ void slot_read(const ClSlots& S, int s, int lane, uint32_t* x) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 v = S[s][q][lane];
-        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-    }
-}
-
-__device__ __forceinline__ void slot_write(ClSlots& S, int s, int lane, const uint32_t* x) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) S[s][q][lane] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-}
-
 // AND if non-empty else OR, forced root, the record + masks to HBM (as fitch_up_node / wide_finish
 // write them), the (x, s) masks into the parent's up slot when the parent is in a later band
 // (ps = ClArgs::pslot[item]), the set into the node's LDS slot when it is in this cluster.
@@ -624,34 +601,6 @@ __device__ __forceinline__ void cluster_wide(const UpArgs& a, const ClArgs& c, c
         }
     }
     cluster_finish(a, d, ps, S, tile, lane, word, cw, both, either, vd, 0, 0, false);
-}
-
-// An item's descriptor, up slots and up-slot target, fetched as one VECTOR load (lane k < 16:
-// descriptor dword k; 16..23: the up slots' dwords; 24..: the target) and moved to scalar
-// registers one round later: a scalar load in flight would hold every LDS barrier of the round
-// (s_waitcnt lgkmcnt(0) covers both).
-struct ClMeta {
-    NodeDesc d;
-    UpSlots s;
-    int32_t ps;
-};
-
-__device__ __forceinline__ uint32_t cl_meta_load(const UpArgs& a, const ClArgs& c, int32_t it, int tile, int lane) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(c.pslot + it);
-    if (lane < 16) src = reinterpret_cast<const uint32_t*>(c.items + it) + lane;
-    else if (lane < 24) src = reinterpret_cast<const uint32_t*>(a.upm + ((size_t)(c.upm_base + it) * a.tiles + tile) * 4) + (lane - 16);
-    return *src;
-}
-
-__device__ __forceinline__ void cl_meta_get(uint32_t m, ClMeta& x) {
-    int32_t* p = reinterpret_cast<int32_t*>(&x.d);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) p[k] = __builtin_amdgcn_readlane((int)m, k);
-    auto u64 = [&](int k) {
-        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m, k + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)m, k);
-    };
-    x.s = UpSlots{u64(16), u64(18), u64(20), u64(22)};
-    x.ps = __builtin_amdgcn_readlane((int)m, 24);
 }
 
 __device__ __forceinline__ void cluster_step(const UpArgs& a, const ClArgs& c, const ClMeta& m, const ClFetch& p, ClSlots& S,

@@ -1284,6 +1284,7 @@ int pm_tree_upload(pm_ctx* c, const pm_tree* t) {
         free_tree(dt);
         return hip_fail(c, e, "tree upload");
     }
+    for (const NodeDesc& x : ht.cl.items) ht.cl.max_degree = std::max(ht.cl.max_degree, x.e1 - x.e0);
     ht.cl.items.clear();   // (device only)
     ht.cl.items.shrink_to_fit();
     ht.cl.down_items.clear();

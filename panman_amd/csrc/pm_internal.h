@@ -206,6 +206,7 @@ struct ClusterPlan {
     std::vector<int32_t> slot_of;    // [I] a node's slot (children beyond the first two), -1
     std::vector<int32_t> item_of;    // [I] a swept node's (first) item, -1
     int32_t n_items = 0;
+    int32_t max_degree = 0;          // the items' largest out-degree (Sankoff sweeps: <= 255)
     int32_t upm_base = 0;            // the items' up slots follow both up orders' (UpArgs::upm)
     // the pre-order over the same clusters (plan_cluster_down; empty: the level kernels): per
     // cluster its nodes in depth-first pre-order; pad0 = the slot of the parent's final, pad1

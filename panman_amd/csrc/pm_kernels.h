@@ -1816,6 +1816,61 @@ __global__ __launch_bounds__(kBlock, SUB ? PM_TAIL_WAVES : 1) void k_tail(DownAr
     emit_flush<M != Mode::kSankoff>(a, em, lane);
 }
 
+// ---- LDS-staged post-order sweeps: what the Fitch and Sankoff sweep kernels share (schedule:
+// pm_cluster.cpp).  One wave = one (cluster, tile): the cluster's nodes in depth-first
+// post-order, one per step; a child of the same cluster comes from its LDS slot (16 planes:
+// the Fitch set / the Sankoff Z0, 4 KiB per (node, tile)).
+struct ClArgs {
+    const NodeDesc* items;
+    const int32_t* wg_off;
+    const int32_t* slot_of;
+    const int32_t* pslot;   // per item: the parent's up slot (parent in a later band), -1
+    int32_t upm_base;       // up slots of item i: UpArgs::upm item upm_base + i (after the level items')
+    int32_t wg0;
+};
+typedef uint4 ClSlots[kClSlots][4][kWave];
+
+__device__ __forceinline__ void slot_read(const ClSlots& S, int s, int lane, uint32_t* x) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = S[s][q][lane];
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void slot_write(ClSlots& S, int s, int lane, const uint32_t* x) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[s][q][lane] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+}
+
+// An item's descriptor, up slots and up-slot target, fetched as one VECTOR load (lane k < 16:
+// descriptor dword k; 16..23: the up slots' dwords; 24..: the target) and moved to scalar
+// registers one round later: a scalar load in flight would hold every LDS barrier of the round
+// (s_waitcnt lgkmcnt(0) covers both).
+struct ClMeta {
+    NodeDesc d;
+    UpSlots s;
+    int32_t ps;
+};
+
+__device__ __forceinline__ uint32_t cl_meta_load(const UpArgs& a, const ClArgs& c, int32_t it, int tile, int lane) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(c.pslot + it);
+    if (lane < 16) src = reinterpret_cast<const uint32_t*>(c.items + it) + lane;
+    else if (lane < 24) src = reinterpret_cast<const uint32_t*>(a.upm + ((size_t)(c.upm_base + it) * a.tiles + tile) * 4) + (lane - 16);
+    return *src;
+}
+
+__device__ __forceinline__ void cl_meta_get(uint32_t m, ClMeta& x) {
+    int32_t* p = reinterpret_cast<int32_t*>(&x.d);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] = __builtin_amdgcn_readlane((int)m, k);
+    auto u64 = [&](int k) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m, k + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)m, k);
+    };
+    x.s = UpSlots{u64(16), u64(18), u64(20), u64(22)};
+    x.ps = __builtin_amdgcn_readlane((int)m, 24);
+}
+
 // ---- LDS-staged pre-order sweeps over the post-order's clusters (plan_cluster_down) -------
 // One wave = one (cluster, tile), the bands top-down: the cluster's nodes in depth-first
 // pre-order, one per step -- down_node's work for the node and its first two (non-S2 / S3)

@@ -328,6 +328,151 @@ __global__ __launch_bounds__(kBandBlock) void k_sankoff_up_band(UpArgs a, const 
     }
 }
 
+// ---- LDS-staged post-order sweeps (PM_OPT_CLUSTER; schedule pm_cluster.cpp, as
+// k_fitch_up_cluster): one wave per (cluster, tile) walks the cluster depth first; a child of the
+// same cluster hands its Z0 -- all a parent reads of it (src/fitchSankoff.cpp:376-402) -- through
+// an LDS slot, every other child is read as k_sankoff_up reads it.  Taken when the plan sweeps
+// every height (the level kernels' grouped order is not built around the clusters) and no swept
+// node has more than 255 children (8-bit counters; more: k_sankoff_part).
+template <int B>
+__device__ __forceinline__ void sankoff_z(const uint32_t (&cnt)[16][B], uint32_t finite, uint32_t* z0, uint32_t* z1) {
+    uint32_t cand[16], mx[B];   // maximum count per site, most significant bit first
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cand[v] = ~0u;
+#pragma unroll
+    for (int b = B - 1; b >= 0; --b) {
+        uint32_t hit = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) hit |= cand[v] & cnt[v][b];
+        mx[b] = hit;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) cand[v] &= cnt[v][b] | ~hit;
+    }
+    uint32_t mm1[B], borrow = ~0u;   // max - 1
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        mm1[b] = mx[b] ^ borrow;
+        borrow &= ~mx[b];
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        uint32_t eq = finite;
+#pragma unroll
+        for (int b = 0; b < B; ++b) eq &= ~(cnt[v][b] ^ mm1[b]);
+        z0[v] = cand[v] & finite;
+        z1[v] = eq;
+    }
+}
+
+// Z0 / Z1 to the record (as k_sankoff_up / k_sankoff_up_wide write them), the masks into the
+// parent's up slot (a parent in a later band) and to the materialised children, Z0 into the
+// node's LDS slot when its parent is in this cluster.
+__device__ __forceinline__ void sk_cluster_finish(const UpArgs& a, const NodeDesc& d, int32_t ps, ClSlots& S, int tile,
+                                                  int lane, int64_t word, const uint32_t* z0, const uint32_t* z1,
+                                                  bool dirty_extra) {
+    uint64_t rx, rs, rd;
+    store_sankoff(a.sets, a.cmask, a.cons, d.node, a.tiles, tile, lane, word, z0, z1, dirty_extra, rx, rs, rd);
+    push_up_slot(a, ps, tile, lane, rx, rs);
+    if (d.e1 - d.e0 > 3) push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, rx, rs);
+    else push_children(a, tile, lane, d.e0, d.e1, d.c0, d.c1, rx, rs, rd, d.node == a.root_dense);
+    if (d.parent >= 0) slot_write(S, d.parent, lane, z0);
+}
+
+// A node of out-degree <= 3: sankoff_up_node<2, true, true>'s reads, in-cluster children from LDS.
+__device__ __forceinline__ void sk_cluster_node(const UpArgs& a, const ClArgs& c, const ClMeta& m, ClSlots& S, int tile,
+                                                int lane, int64_t word) {
+    const NodeDesc& d = m.d;
+    const int32_t e0 = d.e0, e1 = d.e1;
+    uint32_t cnt[16][2], finite = 0, z[16], sd = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cnt[v][0] = cnt[v][1] = 0;
+    const int4 vl0 = make_int4(d.vl0[0], d.vl0[1], d.vl0[2], d.vl0[3]), vl1 = make_int4(d.vl1[0], d.vl1[1], d.vl1[2], d.vl1[3]);
+    ChildFetch f0, f1;
+    if (d.pad0 < 0) fetch_child_ap<kSankoffRec, false, true, true>(a, d.c0, vl0, tile, lane, word, f0, m.s.x0, m.s.s0);
+    if (e1 - e0 > 1 && d.pad1 < 0) fetch_child_ap<kSankoffRec, false, true, true>(a, d.c1, vl1, tile, lane, word, f1, m.s.x1, m.s.s1);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t vd = 0;
+    if (d.pad0 >= 0) slot_read(S, d.pad0, lane, z);
+    else {
+        child_set_ap<true>(d.c0, vl0, f0, z, vd);
+        if (kid_shape(d.c0)) sd |= vd;
+    }
+    count_child<2>(cnt, finite, z);
+    if (e1 - e0 > 1) {
+        vd = 0;
+        if (d.pad1 >= 0) slot_read(S, d.pad1, lane, z);
+        else {
+            child_set_ap<true>(d.c1, vl1, f1, z, vd);
+            if (kid_shape(d.c1)) sd |= vd;
+        }
+        count_child<2>(cnt, finite, z);
+    }
+    for (int32_t e = e0 + 2; e < e1; ++e) {   // an out-degree-3 node's third child
+        const int32_t ch = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int32_t s = materialised(ch) ? __builtin_amdgcn_readfirstlane(c.slot_of[ch]) : -1;
+        if (s >= 0) {
+            slot_read(S, s, lane, z);
+        } else {
+            const int4 vl = ch >= 0 && (ch & kVirtualBit) ? a.vleaf[ch & kDenseMask] : make_int4(-1, -1, -1, -1);
+            child_z0(a, ch, __builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y), tile, lane, word, z);
+        }
+        count_child<2>(cnt, finite, z);
+    }
+    uint32_t z0[16], z1[16];
+    sankoff_z<2>(cnt, finite, z0, z1);
+    sk_cluster_finish(a, d, m.ps, S, tile, lane, word, z0, z1, e1 - e0 > 2 || sd != 0u);
+}
+
+// A node of out-degree 4..255 (sankoff_wide_node's counts, one wave): B-bit counters.
+template <int B>
+__device__ __forceinline__ void sk_cluster_wide(const UpArgs& a, const ClArgs& c, const ClMeta& m, ClSlots& S, int tile,
+                                                int lane, int64_t word) {
+    const NodeDesc& d = m.d;
+    uint32_t cnt[16][B], finite = 0, z[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+#pragma unroll
+        for (int b = 0; b < B; ++b) cnt[v][b] = 0;
+    for (int32_t e = d.e0; e < d.e1; ++e) {
+        const int32_t ch = __builtin_amdgcn_readfirstlane(a.child_enc[e]);
+        const int32_t s = materialised(ch) ? __builtin_amdgcn_readfirstlane(c.slot_of[ch]) : -1;
+        if (s >= 0) {
+            slot_read(S, s, lane, z);
+        } else {
+            const int4 vl = ch >= 0 && (ch & kVirtualBit) ? a.vleaf[ch & kDenseMask] : make_int4(-1, -1, -1, -1);
+            child_z0(a, ch, __builtin_amdgcn_readfirstlane(vl.x), __builtin_amdgcn_readfirstlane(vl.y), tile, lane, word, z);
+        }
+        count_child<B>(cnt, finite, z);
+    }
+    uint32_t z0[16], z1[16];
+    sankoff_z<B>(cnt, finite, z0, z1);
+    sk_cluster_finish(a, d, m.ps, S, tile, lane, word, z0, z1, true);
+}
+
+#ifndef PM_SK_CL_WAVES   // waves per SIMD (occupancy bound of the Sankoff sweep kernel)
+#define PM_SK_CL_WAVES 2
+#endif
+__global__ __launch_bounds__(kWave, PM_SK_CL_WAVES) void k_sankoff_up_cluster(UpArgs a, ClArgs c) {
+    __shared__ ClSlots S;
+    const int lane = threadIdx.x;
+    const int32_t b = (int32_t)blockIdx.x;
+    const int32_t wl = b / a.tiles;
+    const int tile = b - wl * a.tiles;
+    const int32_t i0 = c.wg_off[c.wg0 + wl], steps = c.wg_off[c.wg0 + wl + 1] - i0;
+    const int64_t word = (int64_t)tile * kWave + lane;
+    // the next step's descriptor and up slots in flight during this one
+    uint32_t mv = cl_meta_load(a, c, i0, tile, lane);
+    for (int32_t r = 0; r < steps; ++r) {
+        ClMeta m;
+        cl_meta_get(mv, m);
+        if (r + 1 < steps) mv = cl_meta_load(a, c, i0 + r + 1, tile, lane);
+        const int32_t deg = m.d.e1 - m.d.e0;
+        if (deg <= 3) sk_cluster_node(a, c, m, S, tile, lane, word);
+        else if (deg <= 15) sk_cluster_wide<4>(a, c, m, S, tile, lane, word);
+        else sk_cluster_wide<8>(a, c, m, S, tile, lane, word);
+    }
+}
+
 // Nodes of any out-degree above 255 (src/fitchSankoff.cpp:391-402 sums over every child,
 // whatever their number): the children are cut into parts of kPartChildren; one wave per
 // (part, tile) counts its part into 8-bit bit-sliced counters (k_sankoff_part) and writes
@@ -504,7 +649,23 @@ hipError_t launch_sankoff(pm_ctx* c, bool block) {
     if (sub && c->upm == nullptr) return hipErrorInvalidValue;
     up.upm = sub ? c->upm : nullptr;
     up.pslot = grp ? dt.pslot_gs : dt.pslot_k;
-    const int H = (int)(grp ? ht.up_level_off_gs : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off).size() - 1;
+    // LDS-staged sweeps over every height (k_sankoff_up_cluster) when the plan covers the whole
+    // post-order and no swept node has more than 255 children; the level kernels otherwise
+    const ClusterPlan& clp = ht.cl;
+    const bool sk_clu = sub && c->cluster && clp.band_wg.size() > 1 && clp.h0 == 0 && clp.max_degree <= 255;
+    const int H = sk_clu ? 0 : (int)(grp ? ht.up_level_off_gs : sub ? ht.up_level_off_k : virt ? ht.up_level_off_v : ht.up_level_off).size() - 1;
+    if (sk_clu) {
+        const ClArgs ca0{dt.cl_items, dt.cl_wg_off, dt.cl_slot_of, dt.cl_pslot, clp.upm_base, 0};
+        for (size_t bnd = 0; bnd + 1 < clp.band_wg.size(); ++bnd) {
+            ClArgs ca = ca0;
+            ca.wg0 = clp.band_wg[bnd];
+            const int64_t nwg = clp.band_wg[bnd + 1] - ca.wg0;
+            if (nwg == 0) continue;
+            timer_begin(c, 0);
+            hipLaunchKernelGGL(k_sankoff_up_cluster, dim3((unsigned)(nwg * tiles)), dim3(kWave), 0, c->stream, up, ca);
+            timer_end(c, 0);
+        }
+    }
     // nodes [b, e) of one level with more than 255 children: parts, then the merge
     auto launch_parts = [&](int32_t b, int32_t e, hipStream_t s) {
         const int32_t p0 = part_off[b], np = part_off[e] - p0;
