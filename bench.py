@@ -369,7 +369,7 @@ def roofline_of(args, mode, ms, launches, design, ctx, muts, ms_step, rank, tail
     # each timed class is a pass: every launch of these kernels (levels, narrow bands, wide
     # nodes, Sankoff parts, the tail of leaf-ish children) -- PMC bytes are summed per run
     up_k = ("k_fitch_up", "k_fitch_up_wide", "k_fitch_up_band", "k_fitch_up_mixed", "k_fitch_up_cluster") if fitch else \
-        ("k_sankoff_up", "k_sankoff_up_wide", "k_sankoff_part", "k_sankoff_merge", "k_sankoff_up_band", "k_sankoff_up_mixed")
+        ("k_sankoff_up", "k_sankoff_up_wide", "k_sankoff_part", "k_sankoff_merge", "k_sankoff_up_band", "k_sankoff_up_mixed", "k_sankoff_up_cluster")
     down_k = ("k_down", "k_down_band", "k_down_cluster")
     prof_names = {names[0]: up_k, names[1]: down_k + ("k_tail",)}
     key = "fitch" if fitch else "sankoff"

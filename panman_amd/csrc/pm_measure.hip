@@ -251,9 +251,10 @@ int pm_design_bytes(pm_ctx* c, double* out, int n) {
     auto mk = [&](int32_t d, int t) { return &m[((size_t)d * tiles + t) * kMaskWords]; };
     // LDS-staged sweeps: a node whose parent is in its cluster hands its set (post-order) and
     // receives its parent's final (pre-order sweeps) through LDS
-    // (post-order sweeps: Fitch; pre-order sweeps: both modes)
+    // (post-order sweeps: Fitch, and Sankoff when they cover every height with <= 255-child
+    // nodes, as launch_sankoff takes them; pre-order sweeps: both modes)
     const bool planned = sub && c->cluster && ht.cl.band_wg.size() > 1 && !ht.cl.slot_of.empty();
-    const bool clu = mode == PM_MODE_FITCH && planned;
+    const bool clu = planned && (mode == PM_MODE_FITCH || (ht.cl.h0 == 0 && ht.cl.max_degree <= 255));
     auto in_cluster = [&](int32_t d) { return planned && ht.cl.slot_of[d] >= 0; };
     auto in_lds = [&](int32_t d) { return clu && in_cluster(d); };
     const bool down_lds = planned && ht.cl.down && (mode == PM_MODE_SANKOFF || !c->sub_down);
