@@ -123,14 +123,16 @@ int pm_set_stream(pm_ctx* ctx, void* hip_stream);
  *                  loads (0), or by the tree's widest level (-1: non-temporal from 64k
  *                  (node, tile) waves up, where the records have left the caches by the time
  *                  they are read).
- *   PM_OPT_CLUSTER (default 1): Fitch, subtree form -- the post-order runs as LDS-staged
- *                  sweeps from the first height above which the tree's bands are chain-like
- *                  (deep ladder trees: every height; a random-join tree: none): bands of heights,
- *                  one wave per (connected cluster of the band, 2048-site tile) walking the
- *                  cluster's nodes depth first with its inner sets in LDS; 0 = the level kernels
- *                  everywhere.  A value >= 2 instead takes every height from the first whose
- *                  level (and every level above it) holds at most that many nodes.  Takes effect
- *                  at the next pm_tree_upload.
+ *   PM_OPT_CLUSTER (default 1): subtree form -- the Fitch post-order runs as LDS-staged
+ *                  sweeps from the first height above which the tree's bands are chain-like and
+ *                  hold at most 16384 clusters (deep ladder trees: every height; a random-join
+ *                  tree: none): bands of heights, one wave per (connected cluster of the band,
+ *                  2048-site tile) walking the cluster's nodes depth first with its inner sets
+ *                  in LDS.  When every height is swept, the pre-order (Fitch and Sankoff) and
+ *                  the Sankoff post-order (nodes of <= 255 children) run over the same clusters.
+ *                  0 = the level kernels everywhere.  A value >= 2 instead takes every height
+ *                  from the first whose level (and every level above it) holds at most that
+ *                  many nodes.  Takes effect at the next pm_tree_upload; results identical.
  * (Option ids 1, 4, 5 and 11 -- subtree-region, heavy-path-chain and level-band schedules,
  * tail records overlapped with the pre-order levels -- were measured slower than, or no
  * faster than, the level kernels on MI355X and removed.) */
