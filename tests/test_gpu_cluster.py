@@ -158,3 +158,29 @@ def test_cluster_sankoff_vs_oracle_polytomies(engine, oracle, seed):
     assert (rootc == want_root).all()
     nonroot = want[want[:, 0] != root]
     assert (score == np.bincount(nonroot[:, 1], minlength=sites)).all()
+
+
+def test_cluster_count_rule_leaves_wide_bands_to_levels(engine):
+    """Bands of more than 16384 clusters stay level kernels (PM_CL_MAX_CLUSTERS: their waves fill
+    the GPU as well): a 1M-leaf SARS-like tree's bottom bands are that wide, so its sweeps start
+    above height 0 -- and then the pre-order and the Sankoff post-order stay level kernels."""
+    off, idx, root = panman_amd.sars_like_tree(1_000_000, seed=1)
+    engine.set_cluster(1)
+    phase_reset()
+    engine.tree_upload(off, idx, root)
+    ph = dict(phase_report())
+    assert ph["cluster.bands"] > 0 and ph["cluster.first_level"] > 0 and ph["cluster.down"] == 0, ph
+
+
+def test_design_line_reads_cover_design_bytes(engine):
+    """pm_design_bytes out[14..19] (the pre-order's reads at 128-B line granularity) is at least
+    the 16-B-granular design of the same reads, class by class, and every class is counted."""
+    off, idx, root = panman_amd.sars_like_tree(20000, seed=4)
+    _run(engine, off, idx, root, 1, 4100)
+    d = engine.design_bytes()
+    parts, lines = d["parts"], d["line_reads"]["parts"]
+    assert all(v > 0 for v in lines.values()), lines
+    assert lines["levels_dirty_leaf_words"] >= parts["down_dirty_leaf_words"]
+    assert lines["tail_dirty_leaf_words"] >= parts["down_tail_leaf_words"]
+    assert lines["levels_own_records"] >= parts["down_own_records"]
+    assert d["line_reads"]["levels"] + d["line_reads"]["tail"] > 0
